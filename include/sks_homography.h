@@ -1,0 +1,103 @@
+/*
+ * sks_homography.h -- C ABI of the MI355X (gfx950) batched 4-point homography
+ * solver.  Library: sks-homography_amd/lib/libsks_homography_amd.so
+ *
+ * Every entry point:
+ *   - takes DEVICE pointers the caller owns (the library allocates nothing),
+ *   - enqueues its work on `stream` (a hipStream_t; NULL = the legacy default
+ *     stream) and returns without synchronising,
+ *   - returns 0 on success, otherwise a hipError_t code: hipErrorInvalidValue (1)
+ *     for bad arguments (n < 0, NULL pointer with n > 0, unknown layout/flags),
+ *     or the launch error.  Per-problem numerics are never checked: a degenerate
+ *     quad yields Inf/NaN exactly as the reference does (ACA_SKS.cpp:101 always
+ *     returns 0),
+ *   - is thread-safe (no global mutable state) and safe to capture in a hipGraph.
+ *
+ * A "problem" is 4 source + 4 target points ordered M, N, P, Q.
+ *   HG_LAYOUT_AOS: src/tar are (n,8) {Mx,My,Nx,Ny,Px,Py,Qx,Qy} rows, H is (n,9)
+ *                  row-major 3x3 -- the layout of the reference C++ API
+ *                  (C++ Codes/modules/ACA_SKS.hpp:17-20, one problem per call).
+ *   HG_LAYOUT_SOA: src/tar are (8,n), H is (9,n) -- the reference GPU layout
+ *                  (C++ Codes/Runtime Test/GPU_Runtime Test/GPU_Runtime Test.cu:87-95,
+ *                  :141-149).
+ * HG_FLAG_NORMALIZE scales H so that H[8] == 1 exactly as ACA_SKS.cpp:94-98
+ * (reciprocal of H[8], eight multiplies, H[8] := 1).  Without it H is returned up
+ * to scale, as the reference CUDA kernels and the PyTorch formulations do.
+ *
+ * Results are bit-identical to the reference's C++ CPU path (no FMA contraction,
+ * reference association order, IEEE division).
+ */
+#ifndef SKS_HOMOGRAPHY_H
+#define SKS_HOMOGRAPHY_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define HG_LAYOUT_AOS 0
+#define HG_LAYOUT_SOA 1
+#define HG_FLAG_NORMALIZE 1
+
+/* ACA, binary32.  Replaces sks::runKernel_ACA (C++ Codes/modules/ACA_SKS.cpp:24-102)
+ * batched; with HG_LAYOUT_SOA and no flag it is the FP32 analogue of
+ * cal_Homo_ACA (GPU_Runtime Test.cu:81-151). */
+int hg_aca_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
+               void* stream);
+
+/* ACA, binary64.  Replaces sks::runKernel_ACA_double (ACA_SKS.cpp:104-179); with
+ * HG_LAYOUT_SOA and no flag it replaces cal_Homo_ACA (GPU_Runtime Test.cu:81-151). */
+int hg_aca_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream);
+
+/* SKS, binary32.  Replaces sks::runKernel_SKS (ACA_SKS.cpp:189-303). */
+int hg_sks_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
+               void* stream);
+
+/* SKS, binary64.  Replaces sks::runKernel_SKS_double (ACA_SKS.cpp:305-418); with
+ * HG_LAYOUT_SOA and no flag it replaces cal_Homo_SKS (GPU_Runtime Test.cu:153-240). */
+int hg_sks_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream);
+
+/* TensorACA, rectangle -> quadrangle, binary32, unnormalised.  Replaces
+ * TensorACA_rect(bs, src, tar, scale, div) (PyTorch Codes/Modules_Runtime_Test.py:286-309).
+ * src, tar: (B,3,4) homogeneous point tensors (rows x, y, 1; columns M, N, P, Q);
+ * only src[:,0,0] and src[:,1,0] are read.  H: (B,3,3).  scale = rectangle width,
+ * div = width / height, both shared by the batch (.py:33-35); here they are DEVICE
+ * pointers to one float each, as the reference keeps them in (1,)-shaped tensors. */
+int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
+                           const float* scale, const float* div, void* stream);
+
+/* Same with host-side scalars. */
+int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float* H, int64_t B,
+                                      float scale, float div, void* stream);
+
+/* Synthetic input stream: out[i] = lo + (hi - lo) * u(i), u(i) = top 24 bits of
+ * splitmix64(seed * 0xD1B54A32D192ED03 + offset + i) * 2^-24.  Counter based, so a
+ * rank can generate its own shard (offset = first element) and a host can
+ * regenerate any slice bit for bit.  Plays the role of the reference's cuRAND
+ * draw + get_rand_list gather (GPU_Runtime Test.cu:1443-1451, :52-78). */
+int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
+                        float hi, void* stream);
+
+/* Fused RANSAC-style hypothesis generator + solver (GPU_Runtime Test.cu:52-78 fused
+ * with :81-151).  pool_src/pool_tar: (npool,2) correspondences; idx: (n,4) uint32
+ * indices, each reduced modulo npool like get_rand_list (.cu:56-59).  Writes the
+ * gathered problem's H (AoS, (n,9)); algo 0 = ACA, 1 = SKS. */
+int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
+                        const uint32_t* idx, float* H, int64_t n, int algo, int flags,
+                        void* stream);
+
+/* Device-to-device streaming copy (float4) used by bench.py as the measured
+ * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */
+int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);
+
+/* Library build/version string (static storage). */
+const char* hg_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SKS_HOMOGRAPHY_H */

@@ -1,0 +1,299 @@
+/*
+ * hg_oracle.c -- CPU restatement of the reference's 4-point homography path.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in the product (sks-homography_amd/) links,
+ * loads or calls this file.  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may use it, and only as the checker.
+ *
+ * What it restates (reference paths relative to /root/reference):
+ *   aca_one    <- sks::runKernel_ACA / runKernel_ACA_double
+ *                 "C++ Codes/modules/ACA_SKS.cpp:24-102" and ":104-179"
+ *   sks_one    <- sks::runKernel_SKS / runKernel_SKS_double
+ *                 "C++ Codes/modules/ACA_SKS.cpp:189-303" and ":305-418"
+ *   normalize  <- the common tail "ACA_SKS.cpp:94-98" (reciprocal of H[8], eight
+ *                 multiplies, H[8] := 1)
+ *   rect_one   <- TensorACA_rect "PyTorch Codes/Modules_Runtime_Test.py:286-309"
+ *                 (spec "Matlab Codes/ACA_rect.m:22-38"), evaluated the way ATen's
+ *                 CPU kernels evaluate it (cross product with one fused multiply-add
+ *                 per component, left-to-right 3-term sum, every other op rounded).
+ *
+ * Parity is PINNED: tests/test_oracle_golden.py checks every function here
+ * against tests/golden/*.npz, which tools/make_golden.py produced by running the
+ * reference's own C++ (compiled from /root/reference, oracle/Makefile) and the
+ * reference's own PyTorch statements (executed from /root/reference).
+ *
+ * Numerics contract (why this file must be compiled with -ffp-contract=off and
+ * without -march=native / -mfma): every float operation is rounded on its own, in
+ * the reference's association order.  The reference's `0.5 * x` and `1.0 / x`
+ * (double literals inside the float SKS) are reproduced as float operations; the
+ * double rounding of +,-,*,/ through binary64 is innocuous for binary32 operands
+ * (53 >= 2*24 + 2), so both forms give the same bits.
+ */
+#include <math.h>
+#include <stdint.h>
+#include <string.h>
+
+#define HG_NORMALIZE 1
+
+/* ---------------------------------------------------------------- ACA ------ */
+/* Affine-core-affine: H = H_A2^-1 * H_C * H_A1.  Points are ordered M, N, P, Q
+ * (s[0..1] = M, s[2..3] = N, s[4..5] = P, s[6..7] = Q). */
+#define DEFINE_ACA(NAME, T)                                                        \
+    static void NAME(const T* s, const T* t, T* h) {                               \
+        /* source plane: edges from M and the two area terms (ACA_SKS.cpp:28-32) */ \
+        T enx = s[2] - s[0], epx = s[4] - s[0], eqx = s[6] - s[0];                 \
+        T eny = s[3] - s[1], epy = s[5] - s[1], eqy = s[7] - s[1];                 \
+        T area1 = enx * epy - eny * epx;                                           \
+        T u1x = epy * eqx - epx * eqy;                                             \
+        T u1y = enx * eqy - eny * eqx;                                             \
+        /* target plane (ACA_SKS.cpp:38-42) */                                     \
+        T fnx = t[2] - t[0], fpx = t[4] - t[0], fqx = t[6] - t[0];                 \
+        T fny = t[3] - t[1], fpy = t[5] - t[1], fqy = t[7] - t[1];                 \
+        T area2 = fnx * fpy - fny * fpx;                                           \
+        T u2x = fpy * fqx - fpx * fqy;                                             \
+        T u2y = fnx * fqy - fny * fqx;                                             \
+        /* core transform diagonal + last row (ACA_SKS.cpp:49-54) */               \
+        T k1 = area1 - u1x - u1y;                                                  \
+        T c11 = u1y * u2x * k1;                                                    \
+        T c22 = u1x * u2y * k1;                                                    \
+        T c33 = u1x * u1y * (area2 - u2x - u2y);                                   \
+        T c31 = c11 - c33;                                                         \
+        T c32 = c22 - c33;                                                         \
+        /* H1 = H_A2^-1 * H_C, upper-left 2x2 (ACA_SKS.cpp:61-66) */                \
+        T mx = t[0] * c33;                                                         \
+        T my = t[1] * c33;                                                         \
+        T g11 = t[2] * c11 - mx;                                                   \
+        T g12 = t[4] * c22 - mx;                                                   \
+        T g21 = t[3] * c11 - my;                                                   \
+        T g22 = t[5] * c22 - my;                                                   \
+        /* H = H1 * H_A1: two columns, then the translation column (:74-82) */      \
+        h[0] = g11 * epy - g12 * eny;                                              \
+        h[1] = g12 * enx - g11 * epx;                                              \
+        h[3] = g21 * epy - g22 * eny;                                              \
+        h[4] = g22 * enx - g21 * epx;                                              \
+        h[6] = c31 * epy - c32 * eny;                                              \
+        h[7] = c32 * enx - c31 * epx;                                              \
+        h[2] = mx * area1 - h[0] * s[0] - h[1] * s[1];                             \
+        h[5] = my * area1 - h[3] * s[0] - h[4] * s[1];                             \
+        h[8] = c33 * area1 - h[6] * s[0] - h[7] * s[1];                            \
+    }
+
+/* ---------------------------------------------------------------- SKS ------ */
+/* Similarity-kernel-similarity: H = H_S2^-1 * H_K * H_S1 (ACA_SKS.cpp:189-293). */
+#define DEFINE_SKS(NAME, T)                                                        \
+    static void NAME(const T* s, const T* t, T* h) {                               \
+        const T half = (T)0.5, one = (T)1;                                         \
+        /* similarity anchored on M,N of each plane (ACA_SKS.cpp:192-206) */       \
+        T ax = half * (s[0] + s[2]), ay = half * (s[1] + s[3]);                    \
+        T vx = ax - s[0], vy = s[1] - ay;                                          \
+        T fs1 = vx * vx + vy * vy;                                                 \
+        T bx = half * (t[0] + t[2]), by = half * (t[1] + t[3]);                    \
+        T wx = bx - t[0], wy = t[1] - by;                                          \
+        T fs2 = wx * wx + wy * wy;                                                 \
+        /* P and Q of the source plane in the similarity frame (:217-232) */       \
+        T dpx = s[4] - ax, dpy = s[5] - ay;                                        \
+        T sp_x = vx * dpx - vy * dpy;                                              \
+        T sp_y = vy * dpx + vx * dpy;                                              \
+        T inv_sp = one / sp_y;                                                     \
+        T kp_x = inv_sp * sp_x;                                                    \
+        T kp_y = inv_sp * fs1;                                                     \
+        T dqx = s[6] - ax, dqy = s[7] - ay;                                        \
+        T sq_x = vx * dqx - vy * dqy;                                              \
+        T sq_y = vy * dqx + vx * dqy;                                              \
+        T z1x = sp_y * sq_x - sp_x * sq_y;                                         \
+        T z1y = (sp_y - sq_y) * fs1;                                               \
+        T z1w = sp_y * sq_y;                                                       \
+        /* same for the target plane (:238-253) */                                 \
+        T drx = t[4] - bx, dry = t[5] - by;                                        \
+        T tp_x = wx * drx - wy * dry;                                              \
+        T tp_y = wy * drx + wx * dry;                                              \
+        T inv_tp = one / tp_y;                                                     \
+        T lp_x = inv_tp * tp_x;                                                    \
+        T lp_y = inv_tp * fs2;                                                     \
+        T dsx = t[6] - bx, dsy = t[7] - by;                                        \
+        T tq_x = wx * dsx - wy * dsy;                                              \
+        T tq_y = wy * dsx + wx * dsy;                                              \
+        T z2x = tp_y * tq_x - tp_x * tq_y;                                         \
+        T z2y = (tp_y - tq_y) * fs2;                                               \
+        T z2w = tp_y * tq_y;                                                       \
+        /* kernel parameters a,b,u,v (:263-270) */                                 \
+        T na = z1x * z2x - z1y * z2y;                                              \
+        T nb = z1x * z2y - z1y * z2x;                                              \
+        T den = z1x * z1x - z1y * z1y;                                             \
+        T sc = z1w / (den * z2w);                                                  \
+        T ka = na * sc;                                                            \
+        T kb = nb * sc;                                                            \
+        T ku = lp_x - ka * kp_x - kb * kp_y;                                       \
+        T kv = lp_y - ka * kp_y - kb * kp_x;                                       \
+        /* L = H_S2^-1 * H_K (:276-278) */                                         \
+        T L0 = kb * bx + ka * wx;                                                  \
+        T L1 = wy + bx * kv + ku * wx;                                             \
+        T L2 = ka * bx + kb * wx;                                                  \
+        T L3 = kb * by - ka * wy;                                                  \
+        T L4 = wx + by * kv - ku * wy;                                             \
+        T L5 = ka * by - kb * wy;                                                  \
+        /* translation part of H_S1 (:281-282) */                                  \
+        T s13 = vy * ay - vx * ax;                                                 \
+        T s23 = -vy * ax - vx * ay;                                                \
+        /* H = L * H_S1 (:285-293) */                                              \
+        h[0] = L0 * vx + L1 * vy;                                                  \
+        h[1] = L1 * vx - L0 * vy;                                                  \
+        h[2] = L2 * fs1 + L0 * s13 + L1 * s23;                                     \
+        h[3] = L3 * vx + L4 * vy;                                                  \
+        h[4] = L4 * vx - L3 * vy;                                                  \
+        h[5] = L5 * fs1 + L3 * s13 + L4 * s23;                                     \
+        h[6] = kb * vx + kv * vy;                                                  \
+        h[7] = kv * vx - kb * vy;                                                  \
+        h[8] = ka * fs1 + kb * s13 + kv * s23;                                     \
+    }
+
+/* Last-element normalisation shared by all four reference solvers (:94-98). */
+#define DEFINE_NORMALIZE(NAME, T)                                                  \
+    static void NAME(T* h) {                                                       \
+        T r = (T)1 / h[8];                                                         \
+        for (int i = 0; i < 8; ++i) h[i] = h[i] * r;                               \
+        h[8] = (T)1;                                                               \
+    }
+
+DEFINE_ACA(aca_one_f32, float)
+DEFINE_ACA(aca_one_f64, double)
+DEFINE_SKS(sks_one_f32, float)
+DEFINE_SKS(sks_one_f64, double)
+DEFINE_NORMALIZE(normalize_f32, float)
+DEFINE_NORMALIZE(normalize_f64, double)
+
+/* ------------------------------------------------------- batch drivers ----- */
+/* layout 0 = AoS: src/tar (n,8), H (n,9).  layout 1 = SoA: src/tar (8,n), H (9,n)
+ * (the reference GPU layout, GPU_Runtime Test.cu:87-95 / :141-149). */
+#define DEFINE_BATCH(NAME, T, ONE, NORM)                                           \
+    int NAME(const T* src, const T* tar, T* H, int64_t n, int layout, int flags) { \
+        for (int64_t i = 0; i < n; ++i) {                                          \
+            T s[8], t[8], h[9];                                                    \
+            for (int k = 0; k < 8; ++k) {                                          \
+                s[k] = layout ? src[(int64_t)k * n + i] : src[i * 8 + k];          \
+                t[k] = layout ? tar[(int64_t)k * n + i] : tar[i * 8 + k];          \
+            }                                                                      \
+            ONE(s, t, h);                                                          \
+            if (flags & HG_NORMALIZE) NORM(h);                                     \
+            for (int k = 0; k < 9; ++k) {                                          \
+                if (layout) H[(int64_t)k * n + i] = h[k];                          \
+                else H[i * 9 + k] = h[k];                                          \
+            }                                                                      \
+        }                                                                          \
+        return 0;                                                                  \
+    }
+
+DEFINE_BATCH(oracle_aca_f32, float, aca_one_f32, normalize_f32)
+DEFINE_BATCH(oracle_aca_f64, double, aca_one_f64, normalize_f64)
+DEFINE_BATCH(oracle_sks_f32, float, sks_one_f32, normalize_f32)
+DEFINE_BATCH(oracle_sks_f64, double, sks_one_f64, normalize_f64)
+
+/* ------------------------------------------------------ TensorACA rect ----- */
+/* src, tar: (B,3,4) row-major, rows = x, y, w; columns = M, N, P, Q.
+ * H: (B,3,3).  scale, div are batch-uniform (Modules_Runtime_Test.py:33-35).
+ * ATen CPU evaluation (pinned by tests/golden/tensor_aca_rect.npz):
+ *   d[r][j]  = tar[r][j+1] - tar[r][0]
+ *   c        = cross(d[1], d[0]), component i = fma(a_j, b_k, -(a_k * b_j))
+ *   S        = (c0 + c1) + c2
+ *   b[r]     = S * tar[r][0]
+ *   H[r][0]  = tar[r][1] * c0 - b[r]
+ *   H[r][1]  = div * (tar[r][2] * c1 - b[r])
+ *   H[r][2]  = (scale * b[r] - src[0][0] * H[r][0]) - src[1][0] * H[r][1]   */
+int oracle_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
+                               float scale, float div) {
+    for (int64_t i = 0; i < B; ++i) {
+        const float* s = src + i * 12;
+        const float* t = tar + i * 12;
+        float* h = H + i * 9;
+        float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4]; /* d[1] */
+        float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0]; /* d[0] */
+        float c0 = fmaf(ay, bz, -(az * by));
+        float c1 = fmaf(az, bx, -(ax * bz));
+        float c2 = fmaf(ax, by, -(ay * bx));
+        float S = (c0 + c1) + c2;
+        float mx = s[0], my = s[4];
+        for (int r = 0; r < 3; ++r) {
+            float br = S * t[4 * r + 0];
+            float h0 = t[4 * r + 1] * c0 - br;
+            float h1 = div * (t[4 * r + 2] * c1 - br);
+            float sb = scale * br;
+            float m0 = mx * h0;
+            float m1 = my * h1;
+            h[3 * r + 0] = h0;
+            h[3 * r + 1] = h1;
+            h[3 * r + 2] = (sb - m0) - m1;
+        }
+    }
+    return 0;
+}
+
+/* ---------------------------------------------- synthetic input stream ----- */
+/* Counter-based uniform generator shared (bit for bit) with the product's
+ * hg_fill_uniform_f32 so full-size GPU batches can be regenerated on the host:
+ * value(i) = lo + (hi - lo) * (top24(splitmix64(seed * K + i)) * 2^-24).      */
+static uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+int oracle_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset,
+                            float lo, float hi) {
+    const float span = hi - lo;
+    const uint64_t base = seed * 0xD1B54A32D192ED03ull;
+    for (int64_t i = 0; i < count; ++i) {
+        uint64_t r = mix64(base + offset + (uint64_t)i);
+        float u = (float)(uint32_t)(r >> 40) * 5.9604644775390625e-08f; /* 2^-24 */
+        float su = span * u;
+        out[i] = lo + su;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------ CPU baseline timing ------ */
+/* Times the restatement over a batch with `threads` POSIX threads, `reps` passes.
+ * algo: 0 = ACA, 1 = SKS.  AoS f32, normalised (the C++ API semantics).
+ * Returns elapsed wall seconds (CLOCK_MONOTONIC). */
+#include <pthread.h>
+#include <time.h>
+
+typedef struct {
+    int algo;
+    const float *src, *tar;
+    float* H;
+    int64_t lo, hi;
+    int reps;
+} hg_slice_t;
+
+static void* slice_worker(void* arg) {
+    hg_slice_t* w = (hg_slice_t*)arg;
+    for (int r = 0; r < w->reps; ++r) {
+        for (int64_t i = w->lo; i < w->hi; ++i) {
+            float* h = w->H + i * 9;
+            if (w->algo == 0) aca_one_f32(w->src + i * 8, w->tar + i * 8, h);
+            else sks_one_f32(w->src + i * 8, w->tar + i * 8, h);
+            normalize_f32(h);
+        }
+    }
+    return 0;
+}
+
+double oracle_time_f32(int algo, const float* src, const float* tar, float* H, int64_t n,
+                       int threads, int reps) {
+    if (threads < 1) threads = 1;
+    if (threads > 256) threads = 256;
+    pthread_t tid[256];
+    hg_slice_t sl[256];
+    struct timespec t0, t1;
+    clock_gettime(CLOCK_MONOTONIC, &t0);
+    for (int k = 0; k < threads; ++k) {
+        sl[k].algo = algo; sl[k].src = src; sl[k].tar = tar; sl[k].H = H; sl[k].reps = reps;
+        sl[k].lo = n * k / threads;
+        sl[k].hi = n * (k + 1) / threads;
+        pthread_create(&tid[k], 0, slice_worker, &sl[k]);
+    }
+    for (int k = 0; k < threads; ++k) pthread_join(tid[k], 0);
+    clock_gettime(CLOCK_MONOTONIC, &t1);
+    return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
+}

@@ -1,0 +1,145 @@
+"""ctypes front-end for the CPU checkers built by oracle/build.sh.
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and
+bench.py's cpu_baseline leg, never by the product package.
+
+* ``Oracle``    -- our C restatement (oracle/hg_oracle.c), parity pinned against
+                   tests/golden/ (which came from the reference itself).
+* ``RefOracle`` -- the reference's own ACA_SKS.cpp compiled by oracle/build.sh
+                   (oracle/_ref/libsks_ref.so); present wherever it was built.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ORACLE_SO = os.path.join(HERE, "_build", "libhg_oracle.so")
+REF_SO = os.path.join(HERE, "_ref", "libsks_ref.so")
+
+_f32p = ctypes.POINTER(ctypes.c_float)
+_f64p = ctypes.POINTER(ctypes.c_double)
+_i64 = ctypes.c_int64
+
+ALGOS = {"aca": 0, "sks": 1}
+
+
+def _ptr(a: np.ndarray, ctype):
+    assert a.flags["C_CONTIGUOUS"], "oracle buffers must be C-contiguous"
+    return a.ctypes.data_as(ctype)
+
+
+class Oracle:
+    """C restatement of sks::runKernel_{ACA,SKS}[_double] and TensorACA_rect."""
+
+    def __init__(self, path: str = ORACLE_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing: run oracle/build.sh")
+        lib = ctypes.CDLL(path)
+        for name, fp in (("oracle_aca_f32", _f32p), ("oracle_sks_f32", _f32p),
+                         ("oracle_aca_f64", _f64p), ("oracle_sks_f64", _f64p)):
+            fn = getattr(lib, name)
+            fn.argtypes = [fp, fp, fp, _i64, ctypes.c_int, ctypes.c_int]
+            fn.restype = ctypes.c_int
+        lib.oracle_tensor_aca_rect_f32.argtypes = [_f32p, _f32p, _f32p, _i64,
+                                                   ctypes.c_float, ctypes.c_float]
+        lib.oracle_tensor_aca_rect_f32.restype = ctypes.c_int
+        lib.oracle_fill_uniform_f32.argtypes = [_f32p, _i64, ctypes.c_uint64, ctypes.c_uint64,
+                                                ctypes.c_float, ctypes.c_float]
+        lib.oracle_fill_uniform_f32.restype = ctypes.c_int
+        lib.oracle_time_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64,
+                                        ctypes.c_int, ctypes.c_int]
+        lib.oracle_time_f32.restype = ctypes.c_double
+        self.lib = lib
+
+    def solve(self, algo: str, src: np.ndarray, tar: np.ndarray, normalize: bool = True,
+              layout: str = "aos") -> np.ndarray:
+        """Batch solve.  AoS: src/tar (n,8) -> H (n,9); SoA: (8,n) -> (9,n)."""
+        dt = src.dtype
+        assert dt in (np.float32, np.float64) and tar.dtype == dt
+        soa = layout == "soa"
+        src = np.ascontiguousarray(src)
+        tar = np.ascontiguousarray(tar)
+        n = src.shape[1] if soa else src.shape[0]
+        H = np.empty((9, n) if soa else (n, 9), dtype=dt)
+        suffix = "f32" if dt == np.float32 else "f64"
+        fp = _f32p if dt == np.float32 else _f64p
+        fn = getattr(self.lib, f"oracle_{algo}_{suffix}")
+        fn(_ptr(src, fp), _ptr(tar, fp), _ptr(H, fp), n, 1 if soa else 0, 1 if normalize else 0)
+        return H
+
+    def tensor_aca_rect(self, src: np.ndarray, tar: np.ndarray, scale: float,
+                        div: float) -> np.ndarray:
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tar = np.ascontiguousarray(tar, dtype=np.float32)
+        B = tar.shape[0]
+        H = np.empty((B, 3, 3), dtype=np.float32)
+        self.lib.oracle_tensor_aca_rect_f32(_ptr(src, _f32p), _ptr(tar, _f32p), _ptr(H, _f32p),
+                                            B, float(np.float32(scale)), float(np.float32(div)))
+        return H
+
+    def fill_uniform(self, count: int, seed: int, offset: int = 0, lo: float = 0.0,
+                     hi: float = 1024.0) -> np.ndarray:
+        out = np.empty(count, dtype=np.float32)
+        self.lib.oracle_fill_uniform_f32(_ptr(out, _f32p), count, seed, offset, lo, hi)
+        return out
+
+    def time_batch(self, algo: str, src, tar, H, threads: int, reps: int) -> float:
+        return self.lib.oracle_time_f32(ALGOS[algo], _ptr(src, _f32p), _ptr(tar, _f32p),
+                                        _ptr(H, _f32p), src.shape[0], threads, reps)
+
+
+class RefOracle:
+    """The reference's own solver bodies (oracle/_ref/libsks_ref.so)."""
+
+    def __init__(self, path: str = REF_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing (reference not built here)")
+        lib = ctypes.CDLL(path)
+        lib.ref_batch_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64]
+        lib.ref_batch_f64.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, _i64]
+        lib.ref_time_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64, ctypes.c_int,
+                                     ctypes.c_int]
+        lib.ref_time_f32.restype = ctypes.c_double
+        lib.ref_time_repeat_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64]
+        lib.ref_time_repeat_f32.restype = ctypes.c_double
+        self.lib = lib
+
+    @staticmethod
+    def available(path: str = REF_SO) -> bool:
+        return os.path.exists(path)
+
+    def solve(self, algo: str, src: np.ndarray, tar: np.ndarray) -> np.ndarray:
+        src = np.ascontiguousarray(src)
+        tar = np.ascontiguousarray(tar)
+        n = src.shape[0]
+        H = np.empty((n, 9), dtype=src.dtype)
+        if src.dtype == np.float32:
+            self.lib.ref_batch_f32(ALGOS[algo], _ptr(src, _f32p), _ptr(tar, _f32p),
+                                   _ptr(H, _f32p), n)
+        else:
+            self.lib.ref_batch_f64(ALGOS[algo], _ptr(src, _f64p), _ptr(tar, _f64p),
+                                   _ptr(H, _f64p), n)
+        return H
+
+    def time_batch(self, algo: str, src, tar, H, threads: int, reps: int) -> float:
+        return self.lib.ref_time_f32(ALGOS[algo], _ptr(src, _f32p), _ptr(tar, _f32p),
+                                     _ptr(H, _f32p), src.shape[0], threads, reps)
+
+    def time_repeat(self, algo: str, src8, tar8, iters: int) -> float:
+        H9 = np.empty(9, dtype=np.float32)
+        return self.lib.ref_time_repeat_f32(ALGOS[algo], _ptr(src8, _f32p), _ptr(tar8, _f32p),
+                                            _ptr(H9, _f32p), iters)
+
+
+def same_bits(a: np.ndarray, b: np.ndarray) -> np.ndarray:
+    """Elementwise bit equality with every NaN equal to every NaN (payloads differ
+    between x86 and CDNA: x86 propagates an operand's payload, the GPU may return
+    the canonical quiet NaN)."""
+    a = np.asarray(a)
+    b = np.asarray(b)
+    ui = np.uint32 if a.dtype == np.float32 else np.uint64
+    eq = a.view(ui) == b.view(ui)
+    return eq | (np.isnan(a) & np.isnan(b))

@@ -1,0 +1,30 @@
+"""sks-homography_amd -- MI355X-native batched 4-point homography (ACA / SKS / TensorACA).
+
+Import as ``importlib.import_module("sks-homography_amd")`` (the directory name
+carries a hyphen); ``load()`` below also aliases it as ``sks_homography_amd``.
+
+Layers:
+  include/sks_homography.h   C ABI (device pointers, hipStream_t, hipError_t codes)
+  include/sks_aca_sks.hpp    the reference's sks::runKernel_* C++ interface
+  csrc/                      HIP kernels for gfx950 + the C ABI + the sks:: API
+  ops.py                     torch-facing wrappers, torch.ops.sks_amd.*
+  reference_api.py           TensorACA_rect / ACA_vanilla / getInput / adjust mirrors
+  shard.py                   per-GPU block sharding, optional RCCL gather
+"""
+from __future__ import annotations
+
+from . import _lib
+from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib, version
+from .ops import aca, fill_uniform, sample_solve, sks, solve, stream_copy, tensor_aca_rect
+from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
+from .shard import gather_blocks, shard_range
+
+BYTES_PER_PROBLEM = {"f32": 64 + 36, "f64": 128 + 72}   # algorithmic HBM bytes per H
+RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H
+
+__all__ = [
+    "aca", "sks", "solve", "tensor_aca_rect", "fill_uniform", "sample_solve", "stream_copy",
+    "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
+    "gather_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
+    "HG_FLAG_NORMALIZE", "BYTES_PER_PROBLEM", "RECT_BYTES_PER_PROBLEM",
+]

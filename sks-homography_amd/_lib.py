@@ -1,0 +1,78 @@
+"""ctypes binding of the C ABI declared in include/sks_homography.h.
+
+The product path is the HIP library only: if lib/libsks_homography_amd.so is
+missing or fails to load, every entry point raises -- there is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_amd.so")
+
+HG_LAYOUT_AOS = 0
+HG_LAYOUT_SOA = 1
+HG_FLAG_NORMALIZE = 1
+
+_vp = ctypes.c_void_p
+_i64 = ctypes.c_int64
+_int = ctypes.c_int
+
+# name -> (argtypes, restype); mirrors include/sks_homography.h one for one.
+SIGNATURES = {
+    "hg_aca_f32": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_aca_f64": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_sks_f32": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_sks_f64": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_tensor_aca_rect_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
+    "hg_tensor_aca_rect_f32_hostscalar": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
+                                           _vp], _int),
+    "hg_fill_uniform_f32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
+                             ctypes.c_float, _vp], _int),
+    "hg_sample_solve_f32": ([_vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_stream_copy": ([_vp, _vp, _i64, _vp], _int),
+    "hg_version": ([], ctypes.c_char_p),
+}
+
+_lock = threading.Lock()
+_lib = None
+
+
+class HipError(RuntimeError):
+    """A C-ABI entry point returned a non-zero hipError_t."""
+
+    def __init__(self, fn: str, code: int):
+        super().__init__(f"{fn} failed with hipError_t {code}")
+        self.code = code
+
+
+def lib() -> ctypes.CDLL:
+    """Load (once) and return the HIP library; raise loudly if it is absent."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise ImportError(
+                    f"{LIB_PATH} not built: run `python -c 'import __graft_entry__ as g; g.build()'`"
+                    " (the MI355X kernels have no CPU fallback)")
+            handle = ctypes.CDLL(LIB_PATH)
+            for name, (argtypes, restype) in SIGNATURES.items():
+                fn = getattr(handle, name)
+                fn.argtypes = argtypes
+                fn.restype = restype
+            _lib = handle
+    return _lib
+
+
+def call(name: str, *args) -> None:
+    rc = getattr(lib(), name)(*args)
+    if rc != 0:
+        raise HipError(name, rc)
+
+
+def version() -> str:
+    return lib().hg_version().decode()

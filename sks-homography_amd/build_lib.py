@@ -1,0 +1,73 @@
+"""Builds the product library sks-homography_amd/lib/libsks_homography_amd.so.
+
+hipcc, gfx950 only.  Numerics flags are part of the contract, not tuning:
+  -ffp-contract=off   every product/sum rounded on its own (bit parity with the
+                      reference's x86 SSE build); hg_solvers.hpp also pins this
+                      with `#pragma clang fp contract(off)`.
+  no -ffast-math      IEEE division (v_div_scale/fmas/fixup), NaN/Inf preserved.
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+BUILD = os.path.join(HERE, "build")
+LIB_DIR = os.path.join(HERE, "lib")
+LIB = os.path.join(LIB_DIR, "libsks_homography_amd.so")
+ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
+
+SOURCES = ["hg_kernels.hip", "hg_sks_api.cpp"]
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
+          f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
+
+
+def hipcc() -> str:
+    for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found: the MI355X library cannot be built")
+
+
+def _stale(out: str, deps: list[str]) -> bool:
+    if not os.path.exists(out):
+        return True
+    t = os.path.getmtime(out)
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(verbose: bool = False, force: bool = False) -> str:
+    os.makedirs(BUILD, exist_ok=True)
+    os.makedirs(LIB_DIR, exist_ok=True)
+    cc = hipcc()
+    headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
+    headers += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
+    objs = []
+    for src in SOURCES:
+        path = os.path.join(CSRC, src)
+        obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
+        objs.append(obj)
+        if not force and not _stale(obj, [path] + headers):
+            continue
+        cmd = [cc, *COMMON, "-c", path, "-o", obj]
+        if src.endswith(".hip"):
+            cmd[1:1] = [f"--offload-arch={ARCH}"]
+        else:
+            cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    if force or _stale(LIB, objs):
+        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(verbose=True, force="--force" in sys.argv))

@@ -1,0 +1,433 @@
+// hg_kernels.hip -- batched ACA / SKS / TensorACA kernels for MI355X (gfx950).
+//
+// Data path (AoS, the headline): one lane per problem, P problems per lane.
+//   load   : each lane reads its problem's 32-B src row and 32-B tar row as two
+//            16-B global loads each (a wave covers 2 KiB contiguous per operand and
+//            row-slot; the pair of loads consumes every byte of each 128-B line),
+//   compute: the closed form in VGPRs (hg_solvers.hpp),
+//   store  : H rows are 36 B -- not 16-B aligned per lane -- so each wave stages
+//            its 64*P rows in LDS (stride 9 dwords: conflict-free ds_write_b32) and
+//            writes the wave's contiguous 64*P*36-B slab back as 16-B stores, every
+//            lane storing consecutive 16-B chunks (fully coalesced).
+// Bytes per problem (f32): 64 read + 36 written = 100 B; ~1 FLOP/B, so the bound is
+// HBM bandwidth, not VALU.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hg_solvers.hpp"
+#include "sks_homography.h"
+
+namespace hg {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// Read 8 T's (one point row of a problem) with 16-B loads.
+template <typename T, bool NT>
+__device__ __forceinline__ void load_row8(const T* p, T (&v)[8]) {
+    constexpr int kChunks = 8 * sizeof(T) / 16;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        u32x4 w = ld16<NT>(reinterpret_cast<const char*>(p) + 16 * c);
+        __builtin_memcpy(reinterpret_cast<char*>(v) + 16 * c, &w, 16);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// AoS vector kernel: src/tar (n,8), H (n,9); all three 16-B aligned.
+// Wave w of block b owns problems [base, base + 64*P), base = (4b + w) * 64 * P;
+// lane l solves base + j*64 + l for j < P.
+template <int ALGO, bool NORM, typename T, int P, bool NT>
+__global__ __launch_bounds__(kBlock) void solve_aos_vec(const T* __restrict__ src,
+                                                        const T* __restrict__ tar,
+                                                        T* __restrict__ H, int64_t n) {
+    constexpr int kTile = kWave * P;                   // problems per wave
+    constexpr int kEl16 = 16 / sizeof(T);              // T per 16-B chunk
+    constexpr int kChunksPerLane = 9 * P / kEl16;      // 16-B output chunks per lane
+    static_assert((9 * P) % kEl16 == 0, "P must make the wave's H slab whole 16-B chunks");
+    __shared__ __attribute__((aligned(16))) T stage[kWavesPerBlock][kTile * 9];
+
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= n) return;
+    const bool full = base + kTile <= n;
+
+    T h[P][9];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        T s[8], t[8];
+        if (full || p < n) {
+            load_row8<T, NT>(src + p * 8, s);
+            load_row8<T, NT>(tar + p * 8, t);
+        } else {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) s[k] = t[k] = T(0);
+        }
+        solve<ALGO, NORM>(s, t, h[j]);
+    }
+
+    if (full) {
+        T* st = stage[wave];
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) st[(j * kWave + lane) * 9 + k] = h[j][k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        char* out = reinterpret_cast<char*>(H + base * 9);
+        const char* sb = reinterpret_cast<const char*>(st);
+#pragma unroll
+        for (int c = 0; c < kChunksPerLane; ++c) {
+            const int chunk = c * kWave + lane;
+            u32x4 w = *reinterpret_cast<const u32x4*>(sb + 16 * chunk);
+            st16<NT>(out + 16 * chunk, w);
+        }
+    } else {
+        // ragged last wave: plain per-lane stores of the valid rows
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            if (p < n) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Generic kernel: any alignment, AoS or SoA (the reference GPU layout,
+// GPU_Runtime Test.cu:87-95 / :141-149).  One problem per lane, grid-stride.
+// SoA accesses are naturally coalesced (lane-consecutive addresses per component).
+template <int ALGO, bool NORM, typename T, bool SOA>
+__global__ __launch_bounds__(kBlock) void solve_generic(const T* __restrict__ src,
+                                                        const T* __restrict__ tar,
+                                                        T* __restrict__ H, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += stride) {
+        T s[8], t[8], h[9];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s[k] = SOA ? src[(int64_t)k * n + p] : src[p * 8 + k];
+            t[k] = SOA ? tar[(int64_t)k * n + p] : tar[p * 8 + k];
+        }
+        solve<ALGO, NORM>(s, t, h);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            if (SOA) H[(int64_t)k * n + p] = h[k];
+            else H[p * 9 + k] = h[k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TensorACA rect: src/tar (B,3,4) f32, H (B,3,3) f32, unnormalised.
+// Each lane reads its 48-B tar record as three 16-B loads and two dwords of src
+// (M's x and y, offsets 0 and 16 of the 48-B src record).  Output staged like the
+// AoS kernel.  VEC requires tar, src, H 16-B aligned.
+template <int P, bool VEC, bool SCALAR_ARGS>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float scale_v, float div_v) {
+    constexpr int kTile = kWave * P;
+    constexpr int kChunksPerLane = 9 * P / 4;
+    static_assert((9 * P) % 4 == 0, "");
+    __shared__ __attribute__((aligned(16))) float stage[kWavesPerBlock][kTile * 9];
+
+    const float scale = SCALAR_ARGS ? scale_v : scale_p[0];
+    const float div = SCALAR_ARGS ? div_v : div_p[0];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= B) return;
+    const bool full = VEC && base + kTile <= B;
+
+    float h[P][9];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        float tr[12];
+        float mx = 0.f, my = 0.f;
+        if (p < B) {
+            if constexpr (VEC) {
+#pragma unroll
+                for (int c = 0; c < 3; ++c) {
+                    u32x4 w = ld16<true>(tar + p * 12 + 4 * c);
+                    __builtin_memcpy(tr + 4 * c, &w, 16);
+                }
+            } else {
+#pragma unroll
+                for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+            }
+            mx = src[p * 12 + 0];
+            my = src[p * 12 + 4];
+        } else {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) tr[k] = 0.f;
+        }
+        tensor_aca_rect_solve(tr, mx, my, scale, div, h[j]);
+    }
+
+    if (full) {
+        float* st = stage[wave];
+#pragma unroll
+        for (int j = 0; j < P; ++j)
+#pragma unroll
+            for (int k = 0; k < 9; ++k) st[(j * kWave + lane) * 9 + k] = h[j][k];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        char* out = reinterpret_cast<char*>(H + base * 9);
+        const char* sb = reinterpret_cast<const char*>(st);
+#pragma unroll
+        for (int c = 0; c < kChunksPerLane; ++c) {
+            const int chunk = c * kWave + lane;
+            st16<true>(out + 16 * chunk, *reinterpret_cast<const u32x4*>(sb + 16 * chunk));
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            if (p < B) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Fused sampler + solver: gather 4 correspondences by index from a pool (the
+// reference's get_rand_list, GPU_Runtime Test.cu:52-78) and solve in registers,
+// so each problem reads 16 B of indices instead of 64 B of coordinates.
+template <int ALGO, bool NORM>
+__global__ __launch_bounds__(kBlock) void sample_solve_kernel(
+    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
+    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += stride) {
+        const uint4 r = idx[p];
+        const uint32_t id[4] = {r.x % npool, r.y % npool, r.z % npool, r.w % npool};
+        float s[8], t[8], h[9];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
+            s[2 * k] = a.x; s[2 * k + 1] = a.y;
+            t[2 * k] = b.x; t[2 * k + 1] = b.y;
+        }
+        solve<ALGO, NORM>(s, t, h);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[k];
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Counter-based uniform generator (bit-identical to oracle_fill_uniform_f32).
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(kBlock) void fill_uniform_kernel(float* __restrict__ out,
+                                                              int64_t count, uint64_t seed,
+                                                              uint64_t offset, float lo,
+                                                              float hi) {
+    const float span = hi - lo;
+    const uint64_t base = seed * 0xD1B54A32D192ED03ull + offset;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride) {
+        const uint64_t r = mix64(base + (uint64_t)i);
+        const float u = (float)(uint32_t)(r >> 40) * 5.9604644775390625e-08f;
+        const float su = span * u;
+        out[i] = lo + su;
+    }
+}
+
+// Streaming copy, 16 B per lane per iteration (bandwidth yardstick).
+__global__ __launch_bounds__(kBlock) void stream_copy_kernel(const u32x4* __restrict__ src,
+                                                             u32x4* __restrict__ dst,
+                                                             int64_t n16) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < n16; i += stride)
+        __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
+}
+
+}  // namespace hg
+
+// ===========================================================================
+// Host launchers
+// ===========================================================================
+namespace hg {
+
+constexpr int kErrInvalid = (int)hipErrorInvalidValue;
+
+inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
+
+inline unsigned generic_grid(int64_t n) {
+    // Enough blocks to fill 256 CUs several times over, grid-stride beyond that.
+    const int64_t want = ceil_div(n, kBlock);
+    return (unsigned)(want < 8192 ? (want > 0 ? want : 1) : 8192);
+}
+
+inline int launch_status() { return (int)hipGetLastError(); }
+
+template <int ALGO, bool NORM, typename T>
+int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipStream_t s) {
+    if (layout == HG_LAYOUT_SOA) {
+        solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
+    } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {
+        constexpr int P = sizeof(T) == 4 ? 4 : 2;
+        const int64_t per_block = (int64_t)kBlock * P;
+        const int64_t blocks = ceil_div(n, per_block);
+        if (blocks > 0x7fffffffLL) return kErrInvalid;
+        solve_aos_vec<ALGO, NORM, T, P, true><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
+    } else {
+        solve_generic<ALGO, NORM, T, false><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
+    }
+    return launch_status();
+}
+
+template <int ALGO, typename T>
+int dispatch(const T* src, const T* tar, T* H, int64_t n, int layout, int flags, void* stream) {
+    if (n < 0) return kErrInvalid;
+    if (layout != HG_LAYOUT_AOS && layout != HG_LAYOUT_SOA) return kErrInvalid;
+    if (flags & ~HG_FLAG_NORMALIZE) return kErrInvalid;
+    if (n == 0) return 0;
+    if (!src || !tar || !H) return kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (flags & HG_FLAG_NORMALIZE) return launch_solver<ALGO, true>(src, tar, H, n, layout, s);
+    return launch_solver<ALGO, false>(src, tar, H, n, layout, s);
+}
+
+template <bool SCALAR>
+int launch_rect(const float* src, const float* tar, float* H, int64_t B, const float* sp,
+                const float* dp, float sv, float dv, void* stream) {
+    if (B < 0) return kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !H || (!SCALAR && (!sp || !dp))) return kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    constexpr int P = 4;
+    const int64_t blocks = ceil_div(B, (int64_t)kBlock * P);
+    if (blocks > 0x7fffffffLL) return kErrInvalid;
+    if (aligned16(src) && aligned16(tar) && aligned16(H))
+        tensor_aca_rect_kernel<P, true, SCALAR>
+            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    else
+        tensor_aca_rect_kernel<P, false, SCALAR>
+            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    return launch_status();
+}
+
+}  // namespace hg
+
+// ===========================================================================
+// C ABI (include/sks_homography.h)
+// ===========================================================================
+extern "C" {
+
+int hg_aca_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
+               void* stream) {
+    return hg::dispatch<hg::kACA>(src, tar, H, n, layout, flags, stream);
+}
+
+int hg_aca_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream) {
+    return hg::dispatch<hg::kACA>(src, tar, H, n, layout, flags, stream);
+}
+
+int hg_sks_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
+               void* stream) {
+    return hg::dispatch<hg::kSKS>(src, tar, H, n, layout, flags, stream);
+}
+
+int hg_sks_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream) {
+    return hg::dispatch<hg::kSKS>(src, tar, H, n, layout, flags, stream);
+}
+
+int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
+                           const float* scale, const float* div, void* stream) {
+    return hg::launch_rect<false>(src, tar, H, B, scale, div, 0.f, 0.f, stream);
+}
+
+int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float* H, int64_t B,
+                                      float scale, float div, void* stream) {
+    return hg::launch_rect<true>(src, tar, H, B, nullptr, nullptr, scale, div, stream);
+}
+
+int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
+                        float hi, void* stream) {
+    if (count < 0) return hg::kErrInvalid;
+    if (count == 0) return 0;
+    if (!out) return hg::kErrInvalid;
+    hg::fill_uniform_kernel<<<hg::generic_grid(count), hg::kBlock, 0,
+                              reinterpret_cast<hipStream_t>(stream)>>>(out, count, seed, offset,
+                                                                       lo, hi);
+    return hg::launch_status();
+}
+
+int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
+                        const uint32_t* idx, float* H, int64_t n, int algo, int flags,
+                        void* stream) {
+    if (n < 0 || npool == 0 || (algo != 0 && algo != 1) || (flags & ~HG_FLAG_NORMALIZE))
+        return hg::kErrInvalid;
+    if (n == 0) return 0;
+    if (!pool_src || !pool_tar || !idx || !H) return hg::kErrInvalid;
+    if (!hg::aligned16(idx) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
+        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const auto* ix = reinterpret_cast<const uint4*>(idx);
+    const unsigned g = hg::generic_grid(n);
+    const bool norm = flags & HG_FLAG_NORMALIZE;
+    if (algo == 0) {
+        if (norm) hg::sample_solve_kernel<hg::kACA, true><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
+        else hg::sample_solve_kernel<hg::kACA, false><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
+    } else {
+        if (norm) hg::sample_solve_kernel<hg::kSKS, true><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
+        else hg::sample_solve_kernel<hg::kSKS, false><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
+    }
+    return hg::launch_status();
+}
+
+int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
+    if (bytes < 0 || (bytes & 15)) return hg::kErrInvalid;
+    if (bytes == 0) return 0;
+    if (!src || !dst || !hg::aligned16(src) || !hg::aligned16(dst)) return hg::kErrInvalid;
+    const int64_t n16 = bytes / 16;
+    const int64_t want = hg::ceil_div(n16, hg::kBlock * 4);
+    const unsigned g = (unsigned)(want < 16384 ? (want > 0 ? want : 1) : 16384);
+    hg::stream_copy_kernel<<<g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        reinterpret_cast<const hg::u32x4*>(src), reinterpret_cast<hg::u32x4*>(dst), n16);
+    return hg::launch_status();
+}
+
+const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+// hg_solvers.hpp -- per-lane closed-form 4-point solvers (device code, gfx950).
+//
+// One lane owns one problem; every intermediate lives in VGPRs (no LDS, no MFMA:
+// ~100-170 scalar FLOPs per problem is not a contraction).  The association order
+// of every expression is the reference's, and this header is compiled with FP
+// contraction OFF (pragma below + -ffp-contract=off), so each product and sum is
+// rounded on its own exactly as the reference's x86 SSE build rounds it.  That is
+// what makes the GPU output bit-identical to sks::runKernel_* on the CPU.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#pragma clang fp contract(off)
+
+namespace hg {
+
+// ACA: H = H_A2^-1 * H_C * H_A1 (C++ Codes/modules/ACA_SKS.cpp:24-82, 85 FLOPs).
+// s, t = {Mx,My,Nx,Ny,Px,Py,Qx,Qy} of the source / target quad.
+template <typename T>
+__device__ __forceinline__ void aca_solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
+    // source-plane affine frame at M (ACA_SKS.cpp:28-32)
+    const T sn_x = s[2] - s[0], sp_x = s[4] - s[0], sq_x = s[6] - s[0];
+    const T sn_y = s[3] - s[1], sp_y = s[5] - s[1], sq_y = s[7] - s[1];
+    const T det_s = sn_x * sp_y - sn_y * sp_x;
+    const T qs_x = sp_y * sq_x - sp_x * sq_y;
+    const T qs_y = sn_x * sq_y - sn_y * sq_x;
+    // target-plane affine frame at M (:38-42)
+    const T tn_x = t[2] - t[0], tp_x = t[4] - t[0], tq_x = t[6] - t[0];
+    const T tn_y = t[3] - t[1], tp_y = t[5] - t[1], tq_y = t[7] - t[1];
+    const T det_t = tn_x * tp_y - tn_y * tp_x;
+    const T qt_x = tp_y * tq_x - tp_x * tq_y;
+    const T qt_y = tn_x * tq_y - tn_y * tq_x;
+    // core H_C (:49-54)
+    const T r = det_s - qs_x - qs_y;
+    const T c11 = qs_y * qt_x * r;
+    const T c22 = qs_x * qt_y * r;
+    const T c33 = qs_x * qs_y * (det_t - qt_x - qt_y);
+    const T c31 = c11 - c33;
+    const T c32 = c22 - c33;
+    // H_A2^-1 * H_C, upper 2x2 (:61-66)
+    const T m0 = t[0] * c33;
+    const T m1 = t[1] * c33;
+    const T a11 = t[2] * c11 - m0;
+    const T a12 = t[4] * c22 - m0;
+    const T a21 = t[3] * c11 - m1;
+    const T a22 = t[5] * c22 - m1;
+    // times H_A1 (:74-82)
+    h[0] = a11 * sp_y - a12 * sn_y;
+    h[1] = a12 * sn_x - a11 * sp_x;
+    h[3] = a21 * sp_y - a22 * sn_y;
+    h[4] = a22 * sn_x - a21 * sp_x;
+    h[6] = c31 * sp_y - c32 * sn_y;
+    h[7] = c32 * sn_x - c31 * sp_x;
+    h[2] = m0 * det_s - h[0] * s[0] - h[1] * s[1];
+    h[5] = m1 * det_s - h[3] * s[0] - h[4] * s[1];
+    h[8] = c33 * det_s - h[6] * s[0] - h[7] * s[1];
+}
+
+// SKS: H = H_S2^-1 * H_K * H_S1 (ACA_SKS.cpp:189-293, 157 FLOPs, three IEEE
+// divisions).  The reference's double literals (`0.5 *`, `1.0 /`) round to the
+// same binary32 result as the binary32 operation used here.
+template <typename T>
+__device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
+    const T half = T(0.5), one = T(1);
+    // similarities from the M-N anchor pair (:192-206)
+    const T o1x = half * (s[0] + s[2]), o1y = half * (s[1] + s[3]);
+    const T e1x = o1x - s[0], e1y = s[1] - o1y;
+    const T f1 = e1x * e1x + e1y * e1y;
+    const T o2x = half * (t[0] + t[2]), o2y = half * (t[1] + t[3]);
+    const T e2x = o2x - t[0], e2y = t[1] - o2y;
+    const T f2 = e2x * e2x + e2y * e2y;
+    // source P, Q in the canonical frame (:217-232)
+    const T d3x = s[4] - o1x, d3y = s[5] - o1y;
+    const T g3x = e1x * d3x - e1y * d3y;
+    const T g3y = e1y * d3x + e1x * d3y;
+    const T i3 = one / g3y;
+    const T k5x = i3 * g3x;
+    const T k5y = i3 * f1;
+    const T d5x = s[6] - o1x, d5y = s[7] - o1y;
+    const T g5x = e1x * d5x - e1y * d5y;
+    const T g5y = e1y * d5x + e1x * d5y;
+    const T z7x = g3y * g5x - g3x * g5y;
+    const T z7y = (g3y - g5y) * f1;
+    const T z7w = g3y * g5y;
+    // target P, Q (:238-253)
+    const T d4x = t[4] - o2x, d4y = t[5] - o2y;
+    const T g4x = e2x * d4x - e2y * d4y;
+    const T g4y = e2y * d4x + e2x * d4y;
+    const T i4 = one / g4y;
+    const T k6x = i4 * g4x;
+    const T k6y = i4 * f2;
+    const T d6x = t[6] - o2x, d6y = t[7] - o2y;
+    const T g6x = e2x * d6x - e2y * d6y;
+    const T g6y = e2y * d6x + e2x * d6y;
+    const T z8x = g4y * g6x - g4x * g6y;
+    const T z8y = (g4y - g6y) * f2;
+    const T z8w = g4y * g6y;
+    // kernel H_K parameters (:263-270)
+    const T n1 = z7x * z8x - z7y * z8y;
+    const T n2 = z7x * z8y - z7y * z8x;
+    const T dd = z7x * z7x - z7y * z7y;
+    const T sc = z7w / (dd * z8w);
+    const T ka = n1 * sc;
+    const T kb = n2 * sc;
+    const T ku = k6x - ka * k5x - kb * k5y;
+    const T kv = k6y - ka * k5y - kb * k5x;
+    // H_L = H_S2^-1 * H_K, first two rows (:276-278)
+    const T l0 = kb * o2x + ka * e2x;
+    const T l1 = e2y + o2x * kv + ku * e2x;
+    const T l2 = ka * o2x + kb * e2x;
+    const T l3 = kb * o2y - ka * e2y;
+    const T l4 = e2x + o2y * kv - ku * e2y;
+    const T l5 = ka * o2y - kb * e2y;
+    // H_S1 translation (:281-282)
+    const T s13 = e1y * o1y - e1x * o1x;
+    const T s23 = -e1y * o1x - e1x * o1y;
+    // H = H_L * H_S1 (:285-293)
+    h[0] = l0 * e1x + l1 * e1y;
+    h[1] = l1 * e1x - l0 * e1y;
+    h[2] = l2 * f1 + l0 * s13 + l1 * s23;
+    h[3] = l3 * e1x + l4 * e1y;
+    h[4] = l4 * e1x - l3 * e1y;
+    h[5] = l5 * f1 + l3 * s13 + l4 * s23;
+    h[6] = kb * e1x + kv * e1y;
+    h[7] = kv * e1x - kb * e1y;
+    h[8] = ka * f1 + kb * s13 + kv * s23;
+}
+
+// Last-element normalisation (ACA_SKS.cpp:94-98): one IEEE reciprocal-by-division,
+// eight multiplies, H[8] := 1.
+template <typename T>
+__device__ __forceinline__ void normalize_h(T (&h)[9]) {
+    const T r = T(1) / h[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) h[i] = h[i] * r;
+    h[8] = T(1);
+}
+
+enum Algo : int { kACA = 0, kSKS = 1 };
+
+template <int ALGO, bool NORM, typename T>
+__device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
+    if constexpr (ALGO == kACA) aca_solve(s, t, h);
+    else sks_solve(s, t, h);
+    if constexpr (NORM) normalize_h(h);
+}
+
+// TensorACA rectangle -> quad (PyTorch Codes/Modules_Runtime_Test.py:294-302),
+// evaluated as ATen evaluates it: the cross product contracts one product per
+// component into an FMA, the 3-term sum runs left to right, every other op rounds
+// on its own.  tr = (3,4) target tensor rows {x, y, w} x cols {M, N, P, Q}.
+__device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], float mx, float my,
+                                                      float scale, float div, float (&h)[9]) {
+    const float ax = tr[5] - tr[4], ay = tr[6] - tr[4], az = tr[7] - tr[4];  // d[1]: MN, MP, MQ (y)
+    const float bx = tr[1] - tr[0], by = tr[2] - tr[0], bz = tr[3] - tr[0];  // d[0]: MN, MP, MQ (x)
+    const float c0 = __builtin_fmaf(ay, bz, -(az * by));
+    const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
+    const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
+    const float sum = (c0 + c1) + c2;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float b = sum * tr[4 * r];
+        const float h0 = tr[4 * r + 1] * c0 - b;
+        const float h1 = div * (tr[4 * r + 2] * c1 - b);
+        h[3 * r + 0] = h0;
+        h[3 * r + 1] = h1;
+        h[3 * r + 2] = (scale * b - mx * h0) - my * h1;
+    }
+}
+
+}  // namespace hg

@@ -1,0 +1,199 @@
+"""Torch-facing entry points over the C ABI (device memory, torch's current stream).
+
+PyTorch is plumbing here: tensors own the HBM buffers and name the stream; every
+computation is one of the library's HIP kernels.  CPU tensors are rejected -- the
+product has no CPU path.
+
+Also registers the ops with torch.library as ``torch.ops.sks_amd.{aca, sks,
+tensor_aca_rect}`` (the op contract of SURVEY.md section 8(b)).
+"""
+from __future__ import annotations
+
+from typing import Optional, Union
+
+import torch
+
+from . import _lib
+from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA
+
+_DTYPES = {torch.float32: "f32", torch.float64: "f64"}
+
+
+def _require_device(*tensors: torch.Tensor) -> torch.device:
+    dev = tensors[0].device
+    for t in tensors:
+        if t.device.type != "cuda":
+            raise ValueError("sks_homography_amd kernels run on the GPU only; got a "
+                             f"{t.device} tensor (no CPU fallback by design)")
+        if t.device != dev:
+            raise ValueError(f"tensors on different devices: {dev} vs {t.device}")
+    return dev
+
+
+def _stream(dev: torch.device) -> int:
+    return torch.cuda.current_stream(dev).cuda_stream
+
+
+def _as_problems(x: torch.Tensor, layout: str) -> torch.Tensor:
+    """AoS accepts (n,8) or (n,4,2) (the ACA_vanilla layout, .py:312); SoA (8,n)."""
+    if layout == "aos":
+        if x.dim() == 3 and x.shape[1:] == (4, 2):
+            x = x.reshape(x.shape[0], 8)
+        if x.dim() != 2 or x.shape[1] != 8:
+            raise ValueError(f"AoS problems must be (n,8) or (n,4,2), got {tuple(x.shape)}")
+    elif layout == "soa":
+        if x.dim() != 2 or x.shape[0] != 8:
+            raise ValueError(f"SoA problems must be (8,n), got {tuple(x.shape)}")
+    else:
+        raise ValueError(f"layout must be 'aos' or 'soa', got {layout!r}")
+    return x.contiguous()
+
+
+def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = True,
+          layout: str = "aos", out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Batched 4-point homography, ``algo`` in {"aca", "sks"}.
+
+    AoS: src/tar (n,8) or (n,4,2) -> H (n,9); SoA: (8,n) -> (9,n).
+    ``normalize=True`` returns H/H[8] exactly as sks::runKernel_* (ACA_SKS.cpp:94-98);
+    False returns H up to scale as cal_Homo_* / ACA_vanilla do.
+    """
+    if algo not in ("aca", "sks"):
+        raise ValueError(f"algo must be 'aca' or 'sks', got {algo!r}")
+    dev = _require_device(src, tar)
+    if src.dtype not in _DTYPES or tar.dtype != src.dtype:
+        raise TypeError(f"src/tar must both be float32 or float64, got {src.dtype}/{tar.dtype}")
+    src = _as_problems(src, layout)
+    tar = _as_problems(tar, layout)
+    if src.shape != tar.shape:
+        raise ValueError(f"src {tuple(src.shape)} and tar {tuple(tar.shape)} differ")
+    n = src.shape[0] if layout == "aos" else src.shape[1]
+    shape = (n, 9) if layout == "aos" else (9, n)
+    if out is None:
+        out = torch.empty(shape, dtype=src.dtype, device=dev)
+    elif out.shape != shape or out.dtype != src.dtype or not out.is_contiguous() or out.device != dev:
+        raise ValueError(f"out must be a contiguous {shape} {src.dtype} tensor on {dev}")
+    fn = f"hg_{algo}_{_DTYPES[src.dtype]}"
+    with torch.cuda.device(dev):
+        _lib.call(fn, src.data_ptr(), tar.data_ptr(), out.data_ptr(), n,
+                  HG_LAYOUT_AOS if layout == "aos" else HG_LAYOUT_SOA,
+                  HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
+    return out
+
+
+def aca(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torch.Tensor:
+    return solve("aca", src, tar, normalize, layout, out)
+
+
+def sks(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torch.Tensor:
+    return solve("sks", src, tar, normalize, layout, out)
+
+
+Scalar = Union[float, int, torch.Tensor]
+
+
+def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Scalar,
+                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """TensorACA rectangle->quad (Modules_Runtime_Test.py:286-309), unnormalised.
+
+    src, tar: (B,3,4) float32 homogeneous (rows x, y, 1; columns M, N, P, Q).
+    scale, div: batch-uniform width and width/height -- Python numbers or one-element
+    float32 tensors (kept on device, as the reference keeps them).  Returns (B,3,3).
+    """
+    dev = _require_device(src, tar)
+    for name, t in (("src", src), ("tar", tar)):
+        if t.dtype != torch.float32 or t.dim() != 3 or t.shape[1:] != (3, 4):
+            raise ValueError(f"{name} must be a (B,3,4) float32 tensor, got "
+                             f"{tuple(t.shape)} {t.dtype}")
+    if src.shape[0] != tar.shape[0]:
+        raise ValueError("src and tar batch sizes differ")
+    src = src.contiguous()
+    tar = tar.contiguous()
+    B = tar.shape[0]
+    if out is None:
+        out = torch.empty((B, 3, 3), dtype=torch.float32, device=dev)
+    stream = _stream(dev)
+    with torch.cuda.device(dev):
+        if isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):
+            sc = torch.as_tensor(scale, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+            dv = torch.as_tensor(div, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+            _lib.call("hg_tensor_aca_rect_f32", src.data_ptr(), tar.data_ptr(), out.data_ptr(),
+                      B, sc.data_ptr(), dv.data_ptr(), stream)
+        else:
+            _lib.call("hg_tensor_aca_rect_f32_hostscalar", src.data_ptr(), tar.data_ptr(),
+                      out.data_ptr(), B, float(scale), float(div), stream)
+    return out
+
+
+def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: float = 1024.0,
+                 device: Union[str, torch.device] = "cuda", out=None) -> torch.Tensor:
+    """Counter-based U[lo,hi) float32 stream generated on the device."""
+    dev = torch.device(device)
+    if out is None:
+        out = torch.empty(count, dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("hg_fill_uniform_f32", out.data_ptr(), count, seed, offset, lo, hi, _stream(dev))
+    return out
+
+
+def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tensor,
+                 algo: str = "aca", normalize: bool = True) -> torch.Tensor:
+    """Fused hypothesis generation: gather 4 correspondences per row of ``idx``
+    ((n,4) int32/uint32, reduced modulo the pool size like get_rand_list,
+    GPU_Runtime Test.cu:56-59) from (npool,2) pools and solve.  Returns (n,9)."""
+    dev = _require_device(pool_src, pool_tar, idx)
+    if idx.dim() != 2 or idx.shape[1] != 4 or idx.dtype not in (torch.int32, torch.uint32):
+        raise ValueError("idx must be an (n,4) int32/uint32 tensor")
+    pool_src = pool_src.to(torch.float32).contiguous()
+    pool_tar = pool_tar.to(torch.float32).contiguous()
+    idx = idx.contiguous()
+    n = idx.shape[0]
+    out = torch.empty((n, 9), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("hg_sample_solve_f32", pool_src.data_ptr(), pool_tar.data_ptr(),
+                  pool_src.shape[0], idx.data_ptr(), out.data_ptr(), n,
+                  0 if algo == "aca" else 1, HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
+    return out
+
+
+def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
+    dev = _require_device(src, dst)
+    nbytes = src.numel() * src.element_size()
+    with torch.cuda.device(dev):
+        _lib.call("hg_stream_copy", src.data_ptr(), dst.data_ptr(), nbytes, _stream(dev))
+
+
+# ----------------------------------------------------------------- torch.library
+_NS = "sks_amd"
+
+
+def _register_ops() -> None:
+    if hasattr(torch.ops, _NS) and hasattr(getattr(torch.ops, _NS), "aca"):
+        return
+
+    @torch.library.custom_op(f"{_NS}::aca", mutates_args=())
+    def _aca(src: torch.Tensor, tar: torch.Tensor, normalize: bool = False) -> torch.Tensor:
+        return aca(src, tar, normalize).reshape(-1, 3, 3)
+
+    @_aca.register_fake
+    def _(src, tar, normalize=False):
+        return src.new_empty((src.shape[0], 3, 3))
+
+    @torch.library.custom_op(f"{_NS}::sks", mutates_args=())
+    def _sks(src: torch.Tensor, tar: torch.Tensor, normalize: bool = False) -> torch.Tensor:
+        return sks(src, tar, normalize).reshape(-1, 3, 3)
+
+    @_sks.register_fake
+    def _(src, tar, normalize=False):
+        return src.new_empty((src.shape[0], 3, 3))
+
+    @torch.library.custom_op(f"{_NS}::tensor_aca_rect", mutates_args=())
+    def _rect(src: torch.Tensor, tar: torch.Tensor, scale: torch.Tensor,
+              div: torch.Tensor) -> torch.Tensor:
+        return tensor_aca_rect(src, tar, scale, div)
+
+    @_rect.register_fake
+    def _(src, tar, scale, div):
+        return tar.new_empty((tar.shape[0], 3, 3))
+
+
+_register_ops()

@@ -1,0 +1,59 @@
+"""The reference's PyTorch interface for this path, served by the HIP kernels.
+
+Mirrors "PyTorch Codes/Modules_Runtime_Test.py" (names, argument meaning, tensor
+layouts).  Differences, all deliberate:
+  * the reference functions time a loop and return the mean time; these return H
+    (the value the reference computes and discards, .py:294-302 / :330-383);
+  * no `loops`/warm-up arguments (timing lives in bench.py);
+  * CPU tensors raise (the product path is GPU-only).
+The input generators reproduce the reference's draws call for call, so the same
+torch seed yields the same batch.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import ops
+
+
+def getInput(bS: int, device) -> torch.Tensor:
+    """(bS,4,2) axis-aligned 128x128 squares M,N,P,Q with integer top-left corner in
+    [10,30)^2 (Modules_Runtime_Test.py:9-16)."""
+    corner = torch.randint(low=10, high=30, size=[bS, 2], device=device).float()
+    offs = torch.tensor([[0.0, 0.0], [128.0, 0.0], [0.0, 128.0], [128.0, 128.0]], device=device)
+    return corner[:, None, :] + offs[None, :, :]
+
+
+def getTar(bs: int, src: torch.Tensor) -> torch.Tensor:
+    """Target quad = source + integer perturbation in [0,32) (.py:19-21)."""
+    jitter = torch.randint(low=0, high=32, size=[bs, 4, 2], device=src.device).float()
+    return src + jitter
+
+
+def adjust(device, bs: int):
+    """Builds (src, tar, src_h, tar_h, scale, div) like .py:24-37: src/tar (bs,4,2),
+    homogeneous (bs,3,4) copies, and the batch-uniform rectangle width `scale` and
+    width/height ratio `div` read from sample 0 as (1,)-shaped tensors."""
+    src = getInput(bs, device)
+    tar = getTar(bs, src)
+    ones = torch.ones((bs, 1, 4), device=src.device)
+    src_h = torch.cat((src.transpose(1, 2), ones), dim=1)
+    tar_h = torch.cat((tar.transpose(1, 2), ones), dim=1)
+    scale = src_h[0, 0, 1:2] - src_h[0, 0, 0:1]
+    div = scale / (src_h[0, 1, 2:3] - src_h[0, 1, 0:1])
+    return src, tar, src_h, tar_h, scale, div
+
+
+def TensorACA_rect(bs: int, src: torch.Tensor, tar: torch.Tensor, scale, div) -> torch.Tensor:
+    """TensorACA for a source rectangle (.py:286-309): src/tar (bs,3,4) homogeneous,
+    returns the unnormalised (bs,3,3) H."""
+    if src.shape[0] != bs or tar.shape[0] != bs:
+        raise ValueError(f"batch size {bs} does not match tensors {tuple(src.shape)}")
+    return ops.tensor_aca_rect(src, tar, scale, div)
+
+
+def ACA_vanilla(bs: int, src: torch.Tensor, tar: torch.Tensor) -> torch.Tensor:
+    """General-quad ACA (.py:312-388): src/tar (bs,4,2), returns unnormalised (bs,3,3)."""
+    if src.shape[0] != bs or tar.shape[0] != bs:
+        raise ValueError(f"batch size {bs} does not match tensors {tuple(src.shape)}")
+    return ops.aca(src, tar, normalize=False).reshape(bs, 3, 3)

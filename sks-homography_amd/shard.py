@@ -1,0 +1,56 @@
+"""Batch sharding across the GPUs of one node (one process per GPU).
+
+Problems are independent, so a batch of N splits into
+contiguous rank-major blocks and every rank solves its own block with no data-path
+collective.  Inputs are generated on each rank from the counter-based stream
+(offset = the block's first element), so no scatter is needed either.  The only
+collective is the optional gather of all H blocks to one rank over RCCL
+(torch.distributed "nccl" == RCCL on ROCm), which is what a caller that wants every
+result in one place pays for -- reported separately by bench.py.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Tuple
+
+import torch
+
+
+def shard_range(n_total: int, world: int, rank: int) -> Tuple[int, int]:
+    """[lo, hi) of rank's contiguous block; sizes differ by at most one problem."""
+    if world < 1 or not 0 <= rank < world or n_total < 0:
+        raise ValueError(f"bad shard request n={n_total} world={world} rank={rank}")
+    base, extra = divmod(n_total, world)
+    lo = rank * base + min(rank, extra)
+    hi = lo + base + (1 if rank < extra else 0)
+    return lo, hi
+
+
+def gather_blocks(block: torch.Tensor, n_total: int, world: int, rank: int, dst: int = 0,
+                  group=None) -> Optional[torch.Tensor]:
+    """Gathers each rank's (n_r, 9) H block into one (n_total, 9) tensor on ``dst``.
+
+    Uses paired send/recv (a gather, not an all-gather: rank ``dst``'s ingress is the
+    bound, ~7 xGMI links).  Returns the full tensor on ``dst``, None elsewhere.
+    """
+    import torch.distributed as dist
+
+    if world == 1:
+        return block
+    if rank == dst:
+        full = torch.empty((n_total,) + tuple(block.shape[1:]), dtype=block.dtype,
+                           device=block.device)
+        ops: List = []
+        for r in range(world):
+            lo, hi = shard_range(n_total, world, r)
+            if r == dst:
+                full[lo:hi].copy_(block)
+            elif hi > lo:
+                ops.append(dist.P2POp(dist.irecv, full[lo:hi], r, group))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        return full
+    lo, hi = shard_range(n_total, world, rank)
+    if hi > lo:
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, block.contiguous(), dst, group)]):
+            w.wait()
+    return None

@@ -1,0 +1,282 @@
+"""GPU parity: every HIP path against the oracle / reference fixtures, bit for bit.
+
+Bar: bit-exact (NaN == NaN regardless of payload) for ACA, SKS and TensorACA in
+f32 and f64, every layout, normalised or not.  All calls go through the C ABI.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _bits(orc, got, want, what):
+    got = got.detach().cpu().numpy() if isinstance(got, torch.Tensor) else got
+    ok = orc.same_bits(got, want)
+    assert ok.all(), (f"{what}: {int((~ok).sum())}/{ok.size} differ; first "
+                      f"{np.argwhere(~ok)[:3].tolist()} got {got.ravel()[np.flatnonzero(~ok)[:3]]} "
+                      f"want {np.asarray(want).ravel()[np.flatnonzero(~ok)[:3]]}")
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+# ----------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize("algo", ["aca", "sks"])
+@pytest.mark.parametrize("fixture,sk,tk,hk", [
+    ("cpp_uniform.npz", "src_f32", "tar_f32", "{a}_f32"),
+    ("cpp_uniform.npz", "src_f64", "tar_f64", "{a}_f64"),
+    ("cpp_wall.npz", "src", "tar", "{a}"),
+    ("cpp_edge.npz", "src", "tar", "{a}"),
+    ("cpp_edge.npz", "src_f64", "tar_f64", "{a}_f64"),
+    ("kat_veri4pts.npz", "src_f32", "tar_f32", "{a}_f32"),
+    ("kat_veri4pts.npz", "src", "tar", "{a}_f64"),
+])
+def test_golden_reference_cpp(orc, pkg, dev, algo, fixture, sk, tk, hk):
+    g = load_golden(fixture)
+    src, tar = _t(g[sk], dev), _t(g[tk], dev)
+    H = pkg.solve(algo, src, tar, normalize=True)
+    _bits(orc, H, g[hk.format(a=algo)], f"{fixture}:{algo}")
+    # SoA (reference GPU layout) must give the same bits
+    Hs = pkg.solve(algo, src.T.contiguous(), tar.T.contiguous(), normalize=True, layout="soa")
+    _bits(orc, Hs.T, g[hk.format(a=algo)], f"{fixture}:{algo}:soa")
+
+
+def test_golden_aca_vanilla(orc, pkg, dev):
+    g = load_golden("torch_tensor_aca.npz")
+    for tag in ("int", "f"):
+        B = g[f"{tag}_src"].shape[0]
+        H = pkg.ACA_vanilla(B, _t(g[f"{tag}_src"], dev), _t(g[f"{tag}_tar"], dev))
+        _bits(orc, H, g[f"{tag}_vanilla"], f"ACA_vanilla {tag}")
+
+
+@pytest.mark.parametrize("key", ["int_rect", "f_rect", "f_rect_div125"])
+@pytest.mark.parametrize("scalar_kind", ["device", "host"])
+def test_golden_tensor_aca_rect(orc, pkg, dev, key, scalar_kind):
+    g = load_golden("torch_tensor_aca.npz")
+    tag = key.split("_")[0]
+    if key == "int_rect":
+        scale, div = g["int_scale"], g["int_div"]
+    elif key == "f_rect":
+        scale, div = np.array([128.0], np.float32), np.array([1.0], np.float32)
+    else:
+        scale, div = np.array([50.0], np.float32), np.array([1.25], np.float32)
+    if scalar_kind == "device":
+        scale, div = _t(scale, dev), _t(div, dev)
+    else:
+        scale, div = float(scale[0]), float(div[0])
+    src, tar = _t(g[f"{tag}_src_h"], dev), _t(g[f"{tag}_tar_h"], dev)
+    H = pkg.TensorACA_rect(src.shape[0], src, tar, scale, div)
+    _bits(orc, H, g[key], key)
+
+
+# ------------------------------------------------------- seeded random batches
+SIZES = [1, 2, 63, 64, 65, 255, 256, 257, 1023, 1024, 1025, 4095, 4096, 4097, 100_003]
+
+
+@pytest.mark.parametrize("n", SIZES)
+def test_ragged_sizes_vs_oracle(orc, oracle, pkg, dev, n):
+    src = pkg.fill_uniform(n * 8, 3, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 3, n * 8, device=dev).view(n, 8)
+    s, t = src.cpu().numpy(), tar.cpu().numpy()
+    for algo in ("aca", "sks"):
+        for norm in (True, False):
+            H = pkg.solve(algo, src, tar, normalize=norm)
+            _bits(orc, H, oracle.solve(algo, s, t, normalize=norm), f"{algo} n={n} norm={norm}")
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_random_1m_all_variants(orc, oracle, pkg, dev, dtype, layout):
+    n = 1_000_003
+    rng = np.random.default_rng(42)
+    s = rng.uniform(-2048, 2048, (n, 8)).astype(dtype == torch.float32 and np.float32 or np.float64)
+    t = rng.uniform(-2048, 2048, (n, 8)).astype(s.dtype)
+    src, tar = _t(s, dev), _t(t, dev)
+    if layout == "soa":
+        src, tar = src.T.contiguous(), tar.T.contiguous()
+    for algo in ("aca", "sks"):
+        for norm in (True, False):
+            H = pkg.solve(algo, src, tar, normalize=norm, layout=layout)
+            if layout == "soa":
+                H = H.T
+            _bits(orc, H, oracle.solve(algo, s, t, normalize=norm), f"{algo} {dtype} {layout}")
+
+
+def test_unaligned_pointers_take_generic_path(orc, oracle, pkg, dev):
+    n = 5000
+    s = oracle.fill_uniform(n * 8 + 1, 9, 0)[1:].reshape(n, 8)
+    t = oracle.fill_uniform(n * 8 + 1, 9, 99)[1:].reshape(n, 8)
+    big_s = torch.zeros(n * 8 + 1, device=dev)
+    big_t = torch.zeros(n * 8 + 1, device=dev)
+    big_s[1:] = _t(s.ravel(), dev)
+    big_t[1:] = _t(t.ravel(), dev)
+    src, tar = big_s[1:].view(n, 8), big_t[1:].view(n, 8)   # 4-byte aligned only
+    out_big = torch.zeros(n * 9 + 1, device=dev)
+    out = out_big[1:].view(n, 9)
+    for algo in ("aca", "sks"):
+        pkg.solve(algo, src, tar, normalize=True, out=out)
+        _bits(orc, out, oracle.solve(algo, s, t), f"{algo} unaligned")
+
+
+def test_rect_unaligned_and_ragged(orc, oracle, pkg, dev):
+    for B in (1, 255, 256, 1025, 3001):
+        torch.manual_seed(B)
+        _, _, sh, th, sc, dv = pkg.adjust(dev, B)
+        th = th + torch.rand_like(th) * 0.5          # non-integer
+        th[:, 2, :] = 1.0
+        want = oracle.tensor_aca_rect(sh.cpu().numpy(), th.cpu().numpy(), 128.0, 1.0)
+        _bits(orc, pkg.tensor_aca_rect(sh, th, sc, dv), want, f"rect B={B}")
+        # unaligned views
+        bt = torch.zeros(B * 12 + 1, device=dev)
+        bt[1:] = th.reshape(-1)
+        bs = torch.zeros(B * 12 + 1, device=dev)
+        bs[1:] = sh.reshape(-1)
+        ho = torch.zeros(B * 9 + 1, device=dev)
+        H = pkg.tensor_aca_rect(bs[1:].view(B, 3, 4), bt[1:].view(B, 3, 4), 128.0, 1.0,
+                                out=ho[1:].view(B, 3, 3))
+        _bits(orc, H, want, f"rect unaligned B={B}")
+
+
+def test_rect_large_batch_vs_oracle(orc, oracle, pkg, dev):
+    B = 1 << 20
+    torch.manual_seed(1)
+    _, _, sh, th, sc, dv = pkg.adjust(dev, B)
+    th = th + torch.rand_like(th)
+    th[:, 2, :] = 1.0
+    want = oracle.tensor_aca_rect(sh.cpu().numpy(), th.cpu().numpy(), 128.0, 1.0)
+    _bits(orc, pkg.tensor_aca_rect(sh, th, sc, dv), want, "rect 1M")
+
+
+def test_rect_close_to_torch_composed_on_gpu(pkg, dev):
+    """Against the reference's own ATen composition run on THIS GPU (ROCm kernels
+    may contract differently from ATen-CPU, so the bar is a tolerance: 1e-5 of the
+    row norm; the bit-exact bar is against the CPU-pinned fixtures above)."""
+    import bench
+    torch.manual_seed(0)
+    _, _, sh, th, sc, dv = pkg.adjust(dev, 65536)
+    ours = pkg.TensorACA_rect(65536, sh, th, sc, dv).double()
+    theirs = bench.torch_tensor_aca_rect(sh, th, sc, dv).double()
+    err = (ours - theirs).norm(dim=2) / theirs.norm(dim=2)
+    assert err.max().item() < 1e-5
+
+
+# -------------------------------------------------------------- other entries
+def test_fill_uniform_matches_host_stream(oracle, pkg, dev):
+    for off in (0, 12345, (1 << 33) + 7):
+        a = pkg.fill_uniform(100_001, 11, off, device=dev).cpu().numpy()
+        np.testing.assert_array_equal(a, oracle.fill_uniform(100_001, 11, off))
+
+
+def test_fused_sampler_vs_oracle(orc, oracle, pkg, dev):
+    g = load_golden("cpp_wall.npz")
+    ps, pt, idx = _t(g["pool_src"], dev), _t(g["pool_tar"], dev), _t(g["idx"].astype(np.int32), dev)
+    for algo in ("aca", "sks"):
+        H = pkg.sample_solve(ps, pt, idx, algo=algo)
+        _bits(orc, H, g[algo], f"sample_solve {algo}")
+    # modulo reduction like get_rand_list (.cu:56-59)
+    big = idx + 2540 * 3
+    _bits(orc, pkg.sample_solve(ps, pt, big, "aca"), g["aca"], "sample_solve modulo")
+
+
+def test_stream_copy(pkg, dev):
+    a = torch.randn(1 << 22, device=dev)
+    b = torch.empty_like(a)
+    pkg.stream_copy(a, b)
+    assert torch.equal(a, b)
+
+
+def test_torch_library_ops(orc, oracle, pkg, dev):
+    g = load_golden("cpp_uniform.npz")
+    src, tar = _t(g["src_f32"], dev), _t(g["tar_f32"], dev)
+    H = torch.ops.sks_amd.aca(src, tar, True)
+    _bits(orc, H.reshape(-1, 9), g["aca_f32"], "torch.ops.sks_amd.aca")
+    H = torch.ops.sks_amd.sks(src, tar, True)
+    _bits(orc, H.reshape(-1, 9), g["sks_f32"], "torch.ops.sks_amd.sks")
+    t = load_golden("torch_tensor_aca.npz")
+    H = torch.ops.sks_amd.tensor_aca_rect(_t(t["int_src_h"], dev), _t(t["int_tar_h"], dev),
+                                          _t(t["int_scale"], dev), _t(t["int_div"], dev))
+    _bits(orc, H, t["int_rect"], "torch.ops.sks_amd.tensor_aca_rect")
+
+
+def test_stream_and_graph_capture(orc, oracle, pkg, dev):
+    """Launches honour torch's current stream and are capturable in a HIP graph."""
+    n = 300_000
+    src = pkg.fill_uniform(n * 8, 5, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 5, n * 8, device=dev).view(n, 8)
+    H = torch.empty(n, 9, device=dev)
+    s = torch.cuda.Stream(dev)
+    s.wait_stream(torch.cuda.current_stream(dev))
+    with torch.cuda.stream(s):
+        pkg.aca(src, tar, out=H)
+    torch.cuda.current_stream(dev).wait_stream(s)
+    want = oracle.solve("aca", src.cpu().numpy(), tar.cpu().numpy())
+    _bits(orc, H, want, "side stream")
+    H.zero_()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.stream(s):
+        with torch.cuda.graph(graph, stream=s):
+            pkg.aca(src, tar, out=H)
+    graph.replay()
+    torch.cuda.synchronize(dev)
+    _bits(orc, H, want, "graph replay")
+
+
+# ------------------------------------------------------- the sks:: C++ API
+def _sks_api(pkg):
+    lib = pkg.lib()
+    fns = {}
+    for name, mangled, ct in (
+            ("aca", "_ZN3sks13runKernel_ACAEPfS0_S0_", ctypes.c_float),
+            ("sks", "_ZN3sks13runKernel_SKSEPfS0_S0_", ctypes.c_float),
+            ("aca64", "_ZN3sks20runKernel_ACA_doubleEPdS0_S0_", ctypes.c_double),
+            ("sks64", "_ZN3sks20runKernel_SKS_doubleEPdS0_S0_", ctypes.c_double)):
+        f = getattr(lib, mangled)
+        f.restype = ctypes.c_int
+        fns[name] = (f, ct)
+    return fns
+
+
+def test_cpp_api_single_problem_host_and_device(orc, pkg, dev):
+    g = load_golden("cpp_uniform.npz")
+    fns = _sks_api(pkg)
+    torch.cuda.synchronize(dev)
+    for key, algo, sfx in (("aca", "aca", "f32"), ("sks", "sks", "f32"), ("aca64", "aca", "f64"),
+                           ("sks64", "sks", "f64")):
+        f, ct = fns[key]
+        for i in range(0, 1024, 97):
+            s = np.ascontiguousarray(g[f"src_{sfx}"][i])
+            t = np.ascontiguousarray(g[f"tar_{sfx}"][i])
+            h = np.zeros(9, s.dtype)
+            P = ctypes.POINTER(ct)
+            rc = f(s.ctypes.data_as(P), t.ctypes.data_as(P), h.ctypes.data_as(P))
+            assert rc == 0
+            _bits(orc, h, g[f"{algo}_{sfx}"][i], f"sks::{key} host ptrs #{i}")
+        # device pointers
+        ds, dt = _t(g[f"src_{sfx}"][5], dev), _t(g[f"tar_{sfx}"][5], dev)
+        dh = torch.zeros(9, dtype=ds.dtype, device=dev)
+        assert f(ctypes.c_void_p(ds.data_ptr()), ctypes.c_void_p(dt.data_ptr()),
+                 ctypes.c_void_p(dh.data_ptr())) == 0
+        _bits(orc, dh, g[f"{algo}_{sfx}"][5], f"sks::{key} device ptrs")
+
+
+# --------------------------------------------------------------- full size
+@pytest.mark.slow
+def test_full_size_10m_bit_exact(orc, oracle, pkg, dev):
+    """BASELINE configs[1]/[2] at full size: ACA and SKS over the bench's own 10 M
+    inputs, every element compared with the oracle."""
+    n = 10_000_000
+    src = pkg.fill_uniform(n * 8, 11, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 11, n * 8, device=dev).view(n, 8)
+    s = oracle.fill_uniform(n * 8, 11, 0).reshape(n, 8)
+    t = oracle.fill_uniform(n * 8, 11, n * 8).reshape(n, 8)
+    np.testing.assert_array_equal(src[:1000].cpu().numpy(), s[:1000])
+    for algo in ("aca", "sks"):
+        H = pkg.solve(algo, src, tar, normalize=True).cpu().numpy()
+        _bits(orc, H, oracle.solve(algo, s, t), f"{algo} 10M")
+        del H

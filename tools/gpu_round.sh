@@ -1,0 +1,49 @@
+#!/usr/bin/env bash
+# One GPU-box session: smoke -> pytest -m gpu -> bench -> rocprofv3 kernel trace.
+# Every GPU step has its own time limit; a crash / abort / timeout ends the script
+# (a plain test failure, exit 1, does not).  Usage (from the repo root):
+#   gpurun -- bash tools/gpu_round.sh [tag] [steps...]
+set -u
+TAG="${1:-r01}"
+shift || true
+STEPS="${*:-smoke tests bench prof}"
+OUT=gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+
+fatal() {  # exit codes that mean the GPU run did not end normally
+    case "$1" in 0|1|2|3|4|5) return 1 ;; *) return 0 ;; esac
+}
+
+run() {  # run <name> <seconds> <cmd...>
+    local name="$1" secs="$2"; shift 2
+    echo "=== $name: $*" | tee -a "$OUT/steps.log"
+    timeout -k 10 "$secs" "$@" > "$OUT/$name.log" 2>&1
+    local rc=$?
+    echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
+    tail -n 5 "$OUT/$name.log"
+    if fatal "$rc"; then echo "FATAL rc=$rc in $name: stopping"; exit "$rc"; fi
+    return 0
+}
+
+rocm-smi --showproductname > "$OUT/rocm_smi.txt" 2>&1 || true
+lscpu > "$OUT/lscpu.txt" 2>&1 || true
+for step in $STEPS; do
+    case "$step" in
+        smoke) run smoke 300 python __graft_entry__.py smoke ;;
+        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        bench) run bench 600 python bench.py ;;
+        prof)
+            run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/prof_$TAG" -o run -- python3 bench.py --no-cpu ;;
+        pmc)
+            # HBM traffic: separate passes, FETCH_SIZE and WRITE_SIZE can't share one
+            run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+                -d "$OUT/pmc_fetch_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2
+            run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+                -d "$OUT/pmc_write_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
+        kbench) run kbench 600 python tools/kbench.py ;;
+        *) echo "unknown step $step" ;;
+    esac
+done
+echo "done"

@@ -1,0 +1,276 @@
+"""Generates the golden fixtures under tests/golden/ FROM THE REFERENCE ITSELF.
+
+Runs only in the build container (it reads /root/reference; nothing on the GPU box
+needs it).  Run with PYTHONDONTWRITEBYTECODE=1 (it also sets
+sys.dont_write_bytecode) so nothing is written under /root/reference.
+
+Sources of expected outputs:
+  * C++  -- the reference's own "C++ Codes/modules/ACA_SKS.cpp", compiled by
+            oracle/build.sh into oracle/_ref/libsks_ref.so (normalised H, f32 & f64).
+  * PyTorch -- the reference's own statements of TensorACA_rect and ACA_vanilla
+            ("PyTorch Codes/Modules_Runtime_Test.py:294-302, :330-383") and of its
+            input generators (:9-37), executed verbatim on CPU torch.  The module is
+            not imported (its top level imports torchgeometry, absent here): the
+            script parses the file and executes those functions' own statements,
+            dropping only the timing lines of the loop bodies (torch.cuda.synchronize,
+            perf_counter, time_list).
+  * Matlab -- veri_4Pts.m's camera model restated in numpy (no Octave here): the
+            known-answer H_real for the KAT quad (veri_4Pts.m:9-53) and rectangle
+            (:82-93).
+Inputs include the reference's own correspondence file
+("C++ Codes/Runtime Test/CPU_Runtime Test/orig_pts_wall.txt").
+
+Every fixture stores inputs and expected outputs as raw float32/float64 arrays.
+"""
+from __future__ import annotations
+
+import ast
+import os
+import sys
+
+sys.dont_write_bytecode = True
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REF = os.environ.get("SKS_REFERENCE_ROOT", "/root/reference")
+PY_REF = os.path.join(REF, "PyTorch Codes", "Modules_Runtime_Test.py")
+WALL = os.path.join(REF, "C++ Codes", "Runtime Test", "CPU_Runtime Test", "orig_pts_wall.txt")
+OUT = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, os.path.join(ROOT, "oracle"))
+from oracle import RefOracle  # noqa: E402
+
+
+# ------------------------------------------------------------ python reference
+def _ref_functions():
+    tree = ast.parse(open(PY_REF).read(), PY_REF)
+    return {n.name: n for n in tree.body if isinstance(n, ast.FunctionDef)}
+
+
+_TIMING_TOKENS = ("torch.cuda.synchronize", "perf_counter", "time_list")
+
+
+def _loop_body(fn: ast.FunctionDef, src_text: str) -> ast.Module:
+    """The statements of the function's timing loop, minus the timing statements."""
+    loops = [n for n in fn.body if isinstance(n, ast.For)]
+    assert len(loops) == 1, fn.name
+    keep = [s for s in loops[0].body
+            if not any(tok in ast.get_source_segment(src_text, s) for tok in _TIMING_TOKENS)]
+    return ast.Module(body=keep, type_ignores=[])
+
+
+def run_ref_statements(name: str, **env):
+    text = open(PY_REF).read()
+    fns = _ref_functions()
+    mod = _loop_body(fns[name], text)
+    ns = {"torch": torch, **env}
+    exec(compile(mod, f"{PY_REF}:{name}", "exec"), ns)
+    return ns
+
+
+def ref_generators():
+    fns = _ref_functions()
+    mod = ast.Module(body=[fns["getInput"], fns["getTar"], fns["adjust"]], type_ignores=[])
+    ns = {"torch": torch}
+    exec(compile(mod, f"{PY_REF}:generators", "exec"), ns)
+    return ns
+
+
+# ----------------------------------------------------------------- data helpers
+def read_wall():
+    with open(WALL) as f:
+        count = int(f.readline().split()[0])
+        rows = [list(map(float, f.readline().split()[:4])) for _ in range(count)]
+    a = np.asarray(rows, dtype=np.float32)
+    return a[:, 0:2], a[:, 2:4]
+
+
+def wall_problems(n, seed):
+    ps, pt = read_wall()
+    rng = np.random.default_rng(seed)
+    idx = rng.integers(0, ps.shape[0], size=(n, 4))
+    return ps[idx].reshape(n, 8), pt[idx].reshape(n, 8), idx.astype(np.uint32)
+
+
+def edge_problems():
+    """Degenerate and extreme quads (duplicates, collinear triples, zero/huge/
+    negative/subnormal coordinates, NaN/Inf inputs, integer grids)."""
+    rng = np.random.default_rng(7)
+    base_s = np.array([0, 0, 200, 0, 50, 139, 181, 93], np.float32)
+    base_t = np.array([10, 12, 220, 5, 40, 160, 190, 110], np.float32)
+    cases = []
+
+    def add(s, t):
+        cases.append((np.asarray(s, np.float32), np.asarray(t, np.float32)))
+
+    add(base_s, base_t)
+    add(base_s, base_s)                                     # identity
+    add(np.zeros(8), np.zeros(8))                           # everything coincident
+    s = base_s.copy(); s[2:4] = s[0:2]; add(s, base_t)      # M == N
+    s = base_s.copy(); s[6:8] = s[4:6]; add(s, base_t)      # P == Q
+    t = base_t.copy(); t[4:6] = t[0:2]; add(base_s, t)      # target M == P
+    add([0, 0, 1, 1, 2, 2, 3, 7], base_t)                   # collinear M, N, P
+    add(base_s, [0, 0, 10, 0, 20, 0, 5, 9])                 # collinear target M, N, P
+    add([0, 0, 1, 0, 0, 1, 1, 1], [0, 0, 1, 0, 0, 1, 1, 1])  # unit square
+    add([0, 0, 1, 0, 0, 1, 1, 1], [0, 0, 2, 0, 0, 2, 2, 2])
+    add(-base_s, base_t)                                    # negative coordinates
+    add(base_s * 1e6, base_t * 1e6)                         # huge
+    add(base_s * 1e18, base_t * 1e18)                       # overflow territory
+    add(base_s * 1e-20, base_t * 1e-20)                     # underflow / subnormal
+    add(base_s * np.float32(1e-39), base_t)                 # subnormal source
+    s = base_s.copy(); s[3] = np.nan; add(s, base_t)        # NaN input
+    t = base_t.copy(); t[0] = np.inf; add(base_s, t)        # Inf input
+    add([0, 0, 0, 0, 0, 0, 0, 0], base_t)                   # zero-area source
+    for k in range(16):                                     # integer grids
+        g = rng.integers(-64, 64, size=8).astype(np.float32)
+        h = rng.integers(-64, 64, size=8).astype(np.float32)
+        add(g, h)
+    for k in range(16):                                     # tiny perturbations of a square
+        sq = np.array([0, 0, 1, 0, 0, 1, 1, 1], np.float32) * 100
+        add(sq + rng.normal(0, 1e-3, 8).astype(np.float32), sq)
+    for k in range(14):                                     # wide dynamic range
+        add(rng.uniform(-1, 1, 8).astype(np.float32) * np.float32(10.0 ** rng.integers(-8, 8)),
+            rng.uniform(-1, 1, 8).astype(np.float32) * np.float32(10.0 ** rng.integers(-8, 8)))
+    src = np.stack([c[0] for c in cases])
+    tar = np.stack([c[1] for c in cases])
+    return src, tar
+
+
+# --------------------------------------------------------------- Matlab KAT
+def veri_4pts():
+    """Camera model of veri_4Pts.m:28-53 (K, R = Rx*Ry*Rz, T) restated in numpy."""
+    fu = fv = 900.0
+    u0, v0 = 500.0, 400.0
+    K = np.array([[fu, 0, u0], [0, fv, v0], [0, 0, 1.0]])
+    rx = -np.pi / 8 * np.sqrt(5)
+    ry = -np.pi / 8 * np.sqrt(5)
+    rz = -np.pi / 16 * np.sqrt(5)
+    Rx = np.array([[1, 0, 0], [0, np.cos(rx), -np.sin(rx)], [0, np.sin(rx), np.cos(rx)]])
+    Ry = np.array([[np.cos(ry), 0, np.sin(ry)], [0, 1, 0], [-np.sin(ry), 0, np.cos(ry)]])
+    Rz = np.array([[np.cos(rz), -np.sin(rz), 0], [np.sin(rz), np.cos(rz), 0], [0, 0, 1]])
+    R = Rx @ Ry @ Rz
+    T = np.array([-10.5, -12.5, 525.0])
+    H_real = K @ np.column_stack([R[:, 0], R[:, 1], T])
+    src = np.array([[0, 0], [200, 0], [50, 139], [181, 93]], dtype=np.float64)   # :9-12
+
+    def project(pts):
+        ph = H_real @ np.vstack([pts.T, np.ones(len(pts))])
+        return (ph[:2] / ph[2]).T
+
+    tar = project(src)
+    # rectangle case (:82-93): width 50, height 40, M = (36, 81), order M N P Q
+    w, h, mx, my = 50.0, 40.0, 36.0, 81.0
+    rect = np.array([[mx, my], [mx + w, my], [mx, my + h], [mx + w, my + h]])
+    rect_tar = project(rect)
+    return H_real, src, tar, rect, rect_tar, (w, h, mx, my)
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    ref = RefOracle()
+    manifest = []
+
+    # 1. uniform random quads (f32 + f64) -- C++ reference, normalised
+    rng = np.random.default_rng(2025)
+    n = 1024
+    s32 = rng.uniform(0, 1024, (n, 8)).astype(np.float32)
+    t32 = rng.uniform(0, 1024, (n, 8)).astype(np.float32)
+    s64 = rng.uniform(-512, 512, (n, 8))
+    t64 = rng.uniform(-512, 512, (n, 8))
+    np.savez(os.path.join(OUT, "cpp_uniform.npz"), src_f32=s32, tar_f32=t32,
+             aca_f32=ref.solve("aca", s32, t32), sks_f32=ref.solve("sks", s32, t32),
+             src_f64=s64, tar_f64=t64, aca_f64=ref.solve("aca", s64, t64),
+             sks_f64=ref.solve("sks", s64, t64))
+    manifest.append("cpp_uniform.npz: 1024 U[0,1024) f32 + 1024 U[-512,512) f64 quads; "
+                    "sks::runKernel_{ACA,SKS}[_double] outputs (reference C++)")
+
+    # 2. the reference's own correspondence file, random 4-subsets
+    ws, wt, widx = wall_problems(1024, 11)
+    ps, pt = read_wall()
+    np.savez(os.path.join(OUT, "cpp_wall.npz"), src=ws, tar=wt, idx=widx, pool_src=ps,
+             pool_tar=pt, aca=ref.solve("aca", ws, wt), sks=ref.solve("sks", ws, wt))
+    manifest.append("cpp_wall.npz: 1024 4-subsets of orig_pts_wall.txt (reference data file), "
+                    "pool + indices kept for the fused sampler; reference C++ outputs")
+
+    # 3. edge cases, f32 and f64
+    es, et = edge_problems()
+    np.savez(os.path.join(OUT, "cpp_edge.npz"), src=es, tar=et,
+             aca=ref.solve("aca", es, et), sks=ref.solve("sks", es, et),
+             src_f64=es.astype(np.float64), tar_f64=et.astype(np.float64),
+             aca_f64=ref.solve("aca", es.astype(np.float64), et.astype(np.float64)),
+             sks_f64=ref.solve("sks", es.astype(np.float64), et.astype(np.float64)))
+    manifest.append(f"cpp_edge.npz: {len(es)} degenerate/extreme quads (duplicates, collinear, "
+                    "zero/huge/subnormal/NaN/Inf, integer grids); reference C++ outputs")
+
+    # 4. Matlab KAT
+    H_real, ks, kt, rect, rect_tar, (w, h, mx, my) = veri_4pts()
+    ks32, kt32 = ks.reshape(1, 8).astype(np.float32), kt.reshape(1, 8).astype(np.float32)
+    np.savez(os.path.join(OUT, "kat_veri4pts.npz"), H_real=H_real,
+             H_real_norm=H_real / H_real[2, 2], src=ks.reshape(1, 8), tar=kt.reshape(1, 8),
+             src_f32=ks32, tar_f32=kt32, aca_f32=ref.solve("aca", ks32, kt32),
+             sks_f32=ref.solve("sks", ks32, kt32),
+             aca_f64=ref.solve("aca", ks.reshape(1, 8), kt.reshape(1, 8)),
+             sks_f64=ref.solve("sks", ks.reshape(1, 8), kt.reshape(1, 8)),
+             rect_src=rect, rect_tar=rect_tar, rect_whm=np.array([w, h, mx, my]))
+    manifest.append("kat_veri4pts.npz: veri_4Pts.m camera-model KAT (H_real, projected quad and "
+                    "rectangle) + reference C++ outputs on it")
+
+    # 5. PyTorch reference: TensorACA_rect and ACA_vanilla statements, CPU torch
+    gen = ref_generators()
+    torch.manual_seed(0)
+    B = 256
+    src, tar, src_h, tar_h, scale, div = gen["adjust"]("cpu", B)
+    ns = run_ref_statements("TensorACA_rect", bs=B, src=src_h, tar=tar_h, scale=scale, div=div)
+    H_rect_int = ns["H"].numpy().copy()
+    ns = run_ref_statements("ACA_vanilla", bs=B, src=src, tar=tar)
+    H_van_int = ns["H"].numpy().copy()
+    # non-integer inputs (exercises every rounding of the formulation)
+    g = torch.Generator().manual_seed(5)
+    src2 = torch.rand((B, 4, 2), generator=g) * 128 + torch.tensor([[0, 0], [128, 0], [0, 128],
+                                                                    [128, 128.0]])
+    tar2 = src2 + torch.rand((B, 4, 2), generator=g) * 32
+    ones = torch.ones((B, 1, 4))
+    src2_h = torch.cat((src2.transpose(1, 2), ones), dim=1)
+    tar2_h = torch.cat((tar2.transpose(1, 2), ones), dim=1)
+    sc2 = torch.tensor([128.0])
+    dv2 = torch.tensor([1.0])
+    # rectangle with a non-square aspect, like veri_4Pts's 50x40 (div = 1.25)
+    sc3 = torch.tensor([50.0])
+    dv3 = torch.tensor([1.25])
+    H_rect_f = run_ref_statements("TensorACA_rect", bs=B, src=src2_h, tar=tar2_h, scale=sc2,
+                                  div=dv2)["H"].numpy().copy()
+    H_rect_f3 = run_ref_statements("TensorACA_rect", bs=B, src=src2_h, tar=tar2_h, scale=sc3,
+                                   div=dv3)["H"].numpy().copy()
+    H_van_f = run_ref_statements("ACA_vanilla", bs=B, src=src2, tar=tar2)["H"].numpy().copy()
+    np.savez(os.path.join(OUT, "torch_tensor_aca.npz"),
+             int_src=src.numpy(), int_tar=tar.numpy(), int_src_h=src_h.numpy(),
+             int_tar_h=tar_h.numpy(), int_scale=scale.numpy(), int_div=div.numpy(),
+             int_rect=H_rect_int, int_vanilla=H_van_int,
+             f_src=src2.numpy(), f_tar=tar2.numpy(), f_src_h=src2_h.numpy(),
+             f_tar_h=tar2_h.numpy(), f_rect=H_rect_f, f_rect_div125=H_rect_f3,
+             f_vanilla=H_van_f)
+    manifest.append("torch_tensor_aca.npz: TensorACA_rect / ACA_vanilla statements of the "
+                    "reference executed on CPU torch %s (ATen CPU capability %s): 256 "
+                    "adjust() batches (seed 0) + 256 non-integer batches (scale 128/div 1 and "
+                    "scale 50/div 1.25)" % (torch.__version__,
+                                            torch.backends.cpu.get_cpu_capability()))
+
+    # 6. the reference input generator itself (seed 0, B=8)
+    torch.manual_seed(0)
+    out = gen["adjust"]("cpu", 8)
+    np.savez(os.path.join(OUT, "torch_generator.npz"),
+             **{k: v.numpy() for k, v in zip(["src", "tar", "src_h", "tar_h", "scale", "div"],
+                                            out)})
+    manifest.append("torch_generator.npz: reference adjust('cpu', 8) after torch.manual_seed(0)")
+
+    with open(os.path.join(OUT, "MANIFEST.txt"), "w") as f:
+        f.write("Golden fixtures, generated by tools/make_golden.py from the reference itself.\n")
+        f.write("torch %s, numpy %s\n\n" % (torch.__version__, np.__version__))
+        for m in manifest:
+            f.write("- " + m + "\n")
+    print("\n".join(manifest))
+
+
+if __name__ == "__main__":
+    main()
