@@ -153,6 +153,37 @@ def torch_tensor_aca_rect(src, tar, scale, div):
     return H
 
 
+TABLE8_US = {"aca": 245.0, "sks": 436.0}  # imgs/GPU-runtime.png, N = 1M, FP64 SoA
+
+
+def reference_layout(d: Dist, pkg):
+    """Like-for-like with the reference GPU harness (cal_Homo_ACA/SKS,
+    GPU_Runtime Test.cu:81-240, timed as cal_ACA does at :1166-1206): FP64, SoA
+    (8,N)/(9,N), unnormalised, N = 1M and 10M, mean per-launch time over ~1 s of
+    back-to-back launches.  Table 8's numbers are from an unnamed CUDA GPU."""
+    out = {}
+    for n in (1_000_000, 10_000_000):
+        src = pkg.fill_uniform(n * 8, SEED, 0, device=d.dev).view(8, n).double()
+        tar = pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(8, n).double()
+        H = torch.empty((9, n), dtype=torch.float64, device=d.dev)
+        for algo in ("aca", "sks"):
+            f = lambda: pkg.solve(algo, src, tar, normalize=False, layout="soa", out=H)  # noqa
+            for _ in range(10):
+                f()
+            _, ms1 = timed_region(d, f, 10)
+            loops = max(10, min(5000, int(1000.0 / max(ms1, 1e-3))))  # ~1 s, like .cu:1188
+            _, ms = timed_region(d, f, loops)
+            rec = {"us_per_launch": round(ms * 1e3, 2), "launches": loops,
+                   "achieved_gbps": round(n * 200 / (ms * 1e-3) / 1e9, 1),
+                   "G_homographies_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
+            if n == 1_000_000:
+                rec["table8_us"] = TABLE8_US[algo]
+                rec["speedup_vs_table8"] = round(TABLE8_US[algo] / (ms * 1e3), 2)
+            out[f"{algo}_f64_soa_n{n}"] = rec
+        del src, tar, H
+    return out
+
+
 def main():
     args = parse()
     d = Dist()
@@ -197,7 +228,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "hg::solve_aos_vec<ACA,NORM,f32,P=4>",
+            "kernel": "hg::solve_aos<ACA,NORM,f32,P=2,nt|lds-dma> (hg_aos.hpp)",
             "algorithmic_bytes_per_launch": n * bpp,
             "launch_ms": round(ms_launch, 5),
         },
@@ -254,6 +285,7 @@ def main():
             "large_frac": round(big * rb / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         }
         del bs_h, bt_h, Hb
+        line["reference_layout"] = reference_layout(d, pkg)
 
     if args.gather and d.world > 1:
         d.barrier()

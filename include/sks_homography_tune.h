@@ -1,0 +1,26 @@
+/*
+ * sks_homography_tune.h -- kernel-variant launcher used by tools/kbench.py to pick
+ * the shipped AoS memory schedule.  Not part of the drop-in boundary
+ * (include/sks_homography.h); every variant produces the same bits.
+ */
+#ifndef SKS_HOMOGRAPHY_TUNE_H
+#define SKS_HOMOGRAPHY_TUNE_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int hg_tune_num_variants(void);
+const char* hg_tune_variant_name(int variant);
+/* AoS f32, normalised; algo 0 = ACA, 1 = SKS; per_cu = blocks per CU for persistent
+ * variants (ignored otherwise). */
+int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, float* H,
+                    int64_t n, int per_cu, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif

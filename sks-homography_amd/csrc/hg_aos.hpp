@@ -1,0 +1,227 @@
+// hg_aos.hpp -- the AoS streaming solver kernel (the headline path) and its
+// memory helpers.  One template covers the shipped configuration and the variants
+// tools/kbench.py sweeps (hg_tune.hip); see DESIGN.md "Kernel variants".
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hg_solvers.hpp"
+
+namespace hg {
+
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kWave = 64;
+constexpr int kBlock = 256;
+constexpr int kWavesPerBlock = kBlock / kWave;
+
+// AoS kernel option bits (template parameter FL)
+enum : int {
+    kNtLoad = 1,     // non-temporal (streaming) global loads
+    kNtStore = 2,    // non-temporal global stores
+    kLdsLoad = 4,    // stage inputs through LDS: each load instruction reads 1 KiB contiguous
+    kDirectSt = 8,   // store H rows per lane (9 x 4-B stores) instead of LDS-staged 16-B stores
+    kPersist = 16,   // persistent grid: blocks loop over tiles
+    kLdsDma = 32,    // with kLdsLoad: global_load_lds_dwordx4 (LDS-DMA, no VGPR staging)
+};
+
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+typedef __attribute__((address_space(1))) const void* gbl_ptr_t;
+
+template <bool NT>
+__device__ __forceinline__ u32x4 ld16(const void* p) {
+    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
+    else return *reinterpret_cast<const u32x4*>(p);
+}
+
+template <bool NT>
+__device__ __forceinline__ void st16(void* p, u32x4 v) {
+    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
+    else *reinterpret_cast<u32x4*>(p) = v;
+}
+
+// Read 8 T's (one problem's point row) with 16-B loads.
+template <typename T, bool NT>
+__device__ __forceinline__ void load_row8(const T* p, T (&v)[8]) {
+    constexpr int kChunks = 8 * sizeof(T) / 16;
+#pragma unroll
+    for (int c = 0; c < kChunks; ++c) {
+        u32x4 w = ld16<NT>(reinterpret_cast<const char*>(p) + 16 * c);
+        __builtin_memcpy(reinterpret_cast<char*>(v) + 16 * c, &w, 16);
+    }
+}
+
+__device__ __forceinline__ void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Copies NS contiguous slabs of kBytes each (a multiple of 1 KiB) from global
+// memory into this wave's LDS, every wave-instruction moving 1 KiB (64 lanes x 16 B);
+// all loads of all slabs are issued before the single wait.  DMA: global_load_lds
+// _dwordx4 (no VGPR round trip); else global_load_dwordx4 + ds_write_b128.
+// Ends with the slabs visible to every lane of the wave.
+template <int kBytes, int NS, bool DMA, bool NT>
+__device__ __forceinline__ void slabs_to_lds(const char* const (&g)[NS], char* const (&l)[NS],
+                                             int lane) {
+    static_assert(kBytes % (16 * kWave) == 0, "slab must be whole 1 KiB pieces");
+    constexpr int kPieces = kBytes / (16 * kWave);
+    if constexpr (DMA) {
+#pragma unroll
+        for (int c = 0; c < kPieces; ++c)
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g[s] + 16 * (c * kWave + lane)),
+                                                 (lds_ptr_t)(l[s] + 16 * c * kWave), 16, 0,
+                                                 NT ? 2 : 0);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+        u32x4 v[NS][kPieces];
+#pragma unroll
+        for (int c = 0; c < kPieces; ++c)
+#pragma unroll
+            for (int s = 0; s < NS; ++s) v[s][c] = ld16<NT>(g[s] + 16 * (c * kWave + lane));
+#pragma unroll
+        for (int c = 0; c < kPieces; ++c)
+#pragma unroll
+            for (int s = 0; s < NS; ++s)
+                *reinterpret_cast<u32x4*>(l[s] + 16 * (c * kWave + lane)) = v[s][c];
+    }
+    wave_lds_sync();
+}
+
+// Writes a wave's 64*P rows of 9 T (36/72-B rows, not 16-B aligned per lane) to
+// the contiguous slab `out`: rows are staged in LDS at a 9-element stride (odd dword
+// stride: conflict-free ds_write_b32), then every lane stores consecutive 16-B chunks.
+template <typename T, int P, bool NT>
+__device__ __forceinline__ void store_rows9_staged(char* __restrict__ out, const T (&h)[P][9],
+                                                   char* lds, int lane) {
+    T* st = reinterpret_cast<T*>(lds);
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) st[(j * kWave + lane) * 9 + k] = h[j][k];
+    wave_lds_sync();
+    constexpr int kChunks = kWave * P * 9 * (int)sizeof(T) / 16;  // 144*P*sizeof(T)/4
+    constexpr int kIters = (kChunks + kWave - 1) / kWave;
+#pragma unroll
+    for (int c = 0; c < kIters; ++c) {
+        const int chunk = c * kWave + lane;
+        if (kChunks % kWave == 0 || chunk < kChunks)
+            st16<NT>(out + 16 * chunk, *reinterpret_cast<const u32x4*>(lds + 16 * chunk));
+    }
+    wave_lds_sync();  // the caller may rewrite the staging bytes next
+}
+
+template <typename T, int P, int FL>
+struct AosSmem {
+    static constexpr int kTile = kWave * P;                     // problems per wave
+    static constexpr int kOutBytes = kTile * 9 * (int)sizeof(T);
+    static constexpr int kInBytes = (FL & kLdsLoad) ? 2 * kTile * 8 * (int)sizeof(T) : 0;
+    static constexpr int kBytes = (FL & kDirectSt) && !(FL & kLdsLoad) ? 16
+                                  : (kInBytes > kOutBytes ? kInBytes : kOutBytes);
+};
+
+// One wave solves problems [base, base + 64*P): lane l owns base + j*64 + l.
+template <int ALGO, bool NORM, typename T, int P, int FL>
+__device__ __forceinline__ void aos_wave_tile(const T* __restrict__ src, const T* __restrict__ tar,
+                                              T* __restrict__ H, int64_t n, int64_t base,
+                                              char* lds, int lane) {
+    constexpr bool NTL = FL & kNtLoad, NTS = FL & kNtStore;
+    constexpr int kTile = kWave * P;
+    const bool full = base + kTile <= n;
+
+    T h[P][9];
+    if ((FL & kLdsLoad) && full) {
+        // each instruction: 64 lanes x 16 B contiguous; slab = kTile rows of 8 T
+        constexpr int kSlab = kTile * 8 * (int)sizeof(T);   // bytes per operand
+        const char* gs = reinterpret_cast<const char*>(src + base * 8);
+        const char* gt = reinterpret_cast<const char*>(tar + base * 8);
+        const char* const gsrc[2] = {gs, gt};
+        char* const lsrc[2] = {lds, lds + kSlab};
+        slabs_to_lds<kSlab, 2, (FL & kLdsDma) != 0, NTL>(gsrc, lsrc, lane);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int row = j * kWave + lane;
+            T s[8], t[8];
+            __builtin_memcpy(s, lds + row * 8 * sizeof(T), 8 * sizeof(T));
+            __builtin_memcpy(t, lds + kSlab + row * 8 * sizeof(T), 8 * sizeof(T));
+            solve<ALGO, NORM>(s, t, h[j]);
+        }
+        wave_lds_sync();  // the output staging below reuses these bytes
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            T s[8], t[8];
+            if (full || p < n) {
+                load_row8<T, NTL>(src + p * 8, s);
+                load_row8<T, NTL>(tar + p * 8, t);
+            } else {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) s[k] = t[k] = T(0);
+            }
+            solve<ALGO, NORM>(s, t, h[j]);
+        }
+    }
+
+    bool staged = false;
+    if constexpr (!(FL & kDirectSt)) {
+      if (full) {
+        staged = true;
+        store_rows9_staged<T, P, NTS>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+      }
+    }
+    if (!staged) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            if (full || p < n) {
+#pragma unroll
+                for (int k = 0; k < 9; ++k) {
+                    if constexpr (NTS) __builtin_nontemporal_store(h[j][k], H + p * 9 + k);
+                    else H[p * 9 + k] = h[j][k];
+                }
+            }
+        }
+    }
+}
+
+// AoS vector kernel: src/tar (n,8), H (n,9); all three 16-B aligned.
+// Block b's wave w owns tile (4b + w) (or loops over tiles with kPersist).
+template <int ALGO, bool NORM, typename T, int P, int FL>
+__global__ __launch_bounds__(kBlock) void solve_aos(const T* __restrict__ src,
+                                                    const T* __restrict__ tar,
+                                                    T* __restrict__ H, int64_t n) {
+    using S = AosSmem<T, P, FL>;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][S::kBytes];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t tiles = (n + S::kTile - 1) / S::kTile;
+    if constexpr (FL & kPersist) {
+        for (int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave; t < tiles;
+             t += (int64_t)gridDim.x * kWavesPerBlock)
+            aos_wave_tile<ALGO, NORM, T, P, FL>(src, tar, H, n, t * S::kTile, smem[wave], lane);
+    } else {
+        const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+        if (t < tiles)
+            aos_wave_tile<ALGO, NORM, T, P, FL>(src, tar, H, n, t * S::kTile, smem[wave], lane);
+    }
+}
+
+// Grid for solve_aos: one block per 4 tiles, or a persistent grid of `per_cu`
+// blocks on each of the 256 CUs.
+template <typename T, int P, int FL>
+inline int64_t aos_grid(int64_t n, int per_cu = 8) {
+    const int64_t tile = (int64_t)kWave * P;
+    const int64_t blocks = ((n + tile - 1) / tile + kWavesPerBlock - 1) / kWavesPerBlock;
+    if constexpr (FL & kPersist) {
+        const int64_t cap = 256LL * per_cu;
+        return blocks < cap ? blocks : cap;
+    }
+    return blocks;
+}
+
+}  // namespace hg

@@ -1,118 +1,27 @@
-// hg_kernels.hip -- batched ACA / SKS / TensorACA kernels for MI355X (gfx950).
+// hg_kernels.hip -- batched ACA / SKS / TensorACA kernels for MI355X (gfx950) and
+// the C ABI (include/sks_homography.h).
 //
-// Data path (AoS, the headline): one lane per problem, P problems per lane.
-//   load   : each lane reads its problem's 32-B src row and 32-B tar row as two
-//            16-B global loads each (a wave covers 2 KiB contiguous per operand and
-//            row-slot; the pair of loads consumes every byte of each 128-B line),
-//   compute: the closed form in VGPRs (hg_solvers.hpp),
-//   store  : H rows are 36 B -- not 16-B aligned per lane -- so each wave stages
-//            its 64*P rows in LDS (stride 9 dwords: conflict-free ds_write_b32) and
-//            writes the wave's contiguous 64*P*36-B slab back as 16-B stores, every
-//            lane storing consecutive 16-B chunks (fully coalesced).
-// Bytes per problem (f32): 64 read + 36 written = 100 B; ~1 FLOP/B, so the bound is
-// HBM bandwidth, not VALU.
+// Headline data path (AoS f32, hg_aos.hpp): a wave owns a tile of 64*P problems
+// (P = 2: 8 KiB of src + tar).
+//   load   : the tile's src and tar slabs are contiguous, so they land in the wave's
+//            LDS by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave-instruction,
+//            non-temporal), no VGPR round trip,
+//   compute: each lane reads its problems' 32-B rows from LDS and runs the closed
+//            form in VGPRs (hg_solvers.hpp; no FMA contraction, IEEE division),
+//   store  : H rows are 36 B -- not 16-B aligned per lane -- so the wave stages its
+//            rows in LDS and writes its contiguous H slab as 16-B non-temporal
+//            stores, lane-consecutive (fully coalesced).
+// Bytes per problem (f32): 64 read + 36 written = 100 B at ~1-1.7 FLOP/B: the bound
+// is HBM bandwidth, not VALU.
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
 
+#include "hg_aos.hpp"
 #include "hg_solvers.hpp"
 #include "sks_homography.h"
 
 namespace hg {
-
-typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
-
-constexpr int kWave = 64;
-constexpr int kBlock = 256;
-constexpr int kWavesPerBlock = kBlock / kWave;
-
-template <bool NT>
-__device__ __forceinline__ u32x4 ld16(const void* p) {
-    if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p));
-    else return *reinterpret_cast<const u32x4*>(p);
-}
-
-template <bool NT>
-__device__ __forceinline__ void st16(void* p, u32x4 v) {
-    if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(p));
-    else *reinterpret_cast<u32x4*>(p) = v;
-}
-
-// Read 8 T's (one point row of a problem) with 16-B loads.
-template <typename T, bool NT>
-__device__ __forceinline__ void load_row8(const T* p, T (&v)[8]) {
-    constexpr int kChunks = 8 * sizeof(T) / 16;
-#pragma unroll
-    for (int c = 0; c < kChunks; ++c) {
-        u32x4 w = ld16<NT>(reinterpret_cast<const char*>(p) + 16 * c);
-        __builtin_memcpy(reinterpret_cast<char*>(v) + 16 * c, &w, 16);
-    }
-}
-
-// ---------------------------------------------------------------------------
-// AoS vector kernel: src/tar (n,8), H (n,9); all three 16-B aligned.
-// Wave w of block b owns problems [base, base + 64*P), base = (4b + w) * 64 * P;
-// lane l solves base + j*64 + l for j < P.
-template <int ALGO, bool NORM, typename T, int P, bool NT>
-__global__ __launch_bounds__(kBlock) void solve_aos_vec(const T* __restrict__ src,
-                                                        const T* __restrict__ tar,
-                                                        T* __restrict__ H, int64_t n) {
-    constexpr int kTile = kWave * P;                   // problems per wave
-    constexpr int kEl16 = 16 / sizeof(T);              // T per 16-B chunk
-    constexpr int kChunksPerLane = 9 * P / kEl16;      // 16-B output chunks per lane
-    static_assert((9 * P) % kEl16 == 0, "P must make the wave's H slab whole 16-B chunks");
-    __shared__ __attribute__((aligned(16))) T stage[kWavesPerBlock][kTile * 9];
-
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
-    if (base >= n) return;
-    const bool full = base + kTile <= n;
-
-    T h[P][9];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int64_t p = base + j * kWave + lane;
-        T s[8], t[8];
-        if (full || p < n) {
-            load_row8<T, NT>(src + p * 8, s);
-            load_row8<T, NT>(tar + p * 8, t);
-        } else {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) s[k] = t[k] = T(0);
-        }
-        solve<ALGO, NORM>(s, t, h[j]);
-    }
-
-    if (full) {
-        T* st = stage[wave];
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) st[(j * kWave + lane) * 9 + k] = h[j][k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        char* out = reinterpret_cast<char*>(H + base * 9);
-        const char* sb = reinterpret_cast<const char*>(st);
-#pragma unroll
-        for (int c = 0; c < kChunksPerLane; ++c) {
-            const int chunk = c * kWave + lane;
-            u32x4 w = *reinterpret_cast<const u32x4*>(sb + 16 * chunk);
-            st16<NT>(out + 16 * chunk, w);
-        }
-    } else {
-        // ragged last wave: plain per-lane stores of the valid rows
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int64_t p = base + j * kWave + lane;
-            if (p < n) {
-#pragma unroll
-                for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
-            }
-        }
-    }
-}
 
 // ---------------------------------------------------------------------------
 // Generic kernel: any alignment, AoS or SoA (the reference GPU layout,
@@ -141,18 +50,21 @@ __global__ __launch_bounds__(kBlock) void solve_generic(const T* __restrict__ sr
 
 // ---------------------------------------------------------------------------
 // TensorACA rect: src/tar (B,3,4) f32, H (B,3,3) f32, unnormalised.
-// Each lane reads its 48-B tar record as three 16-B loads and two dwords of src
-// (M's x and y, offsets 0 and 16 of the 48-B src record).  Output staged like the
-// AoS kernel.  VEC requires tar, src, H 16-B aligned.
+// A wave owns 64*P problems.  Full tiles (VEC: 16-B aligned tensors): the wave's
+// contiguous tar slab (64*P*48 B) lands in LDS by LDS-DMA, each lane then reads its
+// 48-B record with three ds_read_b128; M's x and y come from src with two dword
+// loads per lane (offsets 0 and 16 of the 48-B src record) issued before the DMA
+// wait.  H is written through the LDS-staged 16-B store.  Ragged/unaligned tiles
+// use per-lane loads and stores.
 template <int P, bool VEC, bool SCALAR_ARGS>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
     float scale_v, float div_v) {
     constexpr int kTile = kWave * P;
-    constexpr int kChunksPerLane = 9 * P / 4;
-    static_assert((9 * P) % 4 == 0, "");
-    __shared__ __attribute__((aligned(16))) float stage[kWavesPerBlock][kTile * 9];
+    constexpr int kSlab = kTile * 48;
+    constexpr int kLds = kSlab > kTile * 36 ? kSlab : kTile * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][VEC ? kLds : 16];
 
     const float scale = SCALAR_ARGS ? scale_v : scale_p[0];
     const float div = SCALAR_ARGS ? div_v : div_p[0];
@@ -161,57 +73,81 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
     const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
     if (base >= B) return;
     const bool full = VEC && base + kTile <= B;
+    char* lds = smem[wave];
 
     float h[P][9];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int64_t p = base + j * kWave + lane;
-        float tr[12];
-        float mx = 0.f, my = 0.f;
-        if (p < B) {
-            if constexpr (VEC) {
-#pragma unroll
-                for (int c = 0; c < 3; ++c) {
-                    u32x4 w = ld16<true>(tar + p * 12 + 4 * c);
-                    __builtin_memcpy(tr + 4 * c, &w, 16);
-                }
-            } else {
-#pragma unroll
-                for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
-            }
-            mx = src[p * 12 + 0];
-            my = src[p * 12 + 4];
-        } else {
-#pragma unroll
-            for (int k = 0; k < 12; ++k) tr[k] = 0.f;
-        }
-        tensor_aca_rect_solve(tr, mx, my, scale, div, h[j]);
-    }
-
     if (full) {
-        float* st = stage[wave];
-#pragma unroll
-        for (int j = 0; j < P; ++j)
-#pragma unroll
-            for (int k = 0; k < 9; ++k) st[(j * kWave + lane) * 9 + k] = h[j][k];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        char* out = reinterpret_cast<char*>(H + base * 9);
-        const char* sb = reinterpret_cast<const char*>(st);
-#pragma unroll
-        for (int c = 0; c < kChunksPerLane; ++c) {
-            const int chunk = c * kWave + lane;
-            st16<true>(out + 16 * chunk, *reinterpret_cast<const u32x4*>(sb + 16 * chunk));
-        }
-    } else {
+        float mx[P], my[P];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int64_t p = base + j * kWave + lane;
-            if (p < B) {
+            mx[j] = __builtin_nontemporal_load(src + p * 12 + 0);
+            my[j] = __builtin_nontemporal_load(src + p * 12 + 4);
+        }
+        const char* const g[1] = {reinterpret_cast<const char*>(tar + base * 12)};
+        char* const l[1] = {lds};
+        slabs_to_lds<kSlab, 1, true, true>(g, l, lane);
 #pragma unroll
-                for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
-            }
+        for (int j = 0; j < P; ++j) {
+            float tr[12];
+            __builtin_memcpy(tr, lds + (j * kWave + lane) * 48, 48);
+            tensor_aca_rect_solve(tr, mx[j], my[j], scale, div, h[j]);
+        }
+        wave_lds_sync();
+        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        if (p < B) {
+            float tr[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+            tensor_aca_rect_solve(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// SoA vector kernel (the reference GPU layout, GPU_Runtime Test.cu:87-95 and
+// :141-149): lane owns V = 16/sizeof(T) consecutive problems and moves each of the
+// 8 + 8 input and 9 output components as one 16-B access (rows are 16-B aligned
+// when n % V == 0 and the bases are 16-B aligned).  Grid-stride.
+template <int ALGO, bool NORM, typename T>
+__global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ src,
+                                                        const T* __restrict__ tar,
+                                                        T* __restrict__ H, int64_t n) {
+    constexpr int V = 16 / sizeof(T);
+    const int64_t groups = n / V;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < groups; q += stride) {
+        T s[8][V], t[8][V];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            u32x4 a = ld16<true>(src + (int64_t)k * n + q * V);
+            u32x4 b = ld16<true>(tar + (int64_t)k * n + q * V);
+            __builtin_memcpy(s[k], &a, 16);
+            __builtin_memcpy(t[k], &b, 16);
+        }
+        T h[V][9];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            T sv[8], tv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { sv[k] = s[k][v]; tv[k] = t[k][v]; }
+            solve<ALGO, NORM>(sv, tv, h[v]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            T o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) o[v] = h[v][k];
+            u32x4 w;
+            __builtin_memcpy(&w, o, 16);
+            st16<true>(H + (int64_t)k * n + q * V, w);
         }
     }
 }
@@ -283,6 +219,14 @@ namespace hg {
 
 constexpr int kErrInvalid = (int)hipErrorInvalidValue;
 
+// Shipped AoS configuration (chosen by tools/kbench.py sweeps, profiles/r01/):
+// P problems per lane (2 f32 / 1 f64: an 8 KiB wave tile either way), inputs by
+// LDS-DMA with the non-temporal policy, LDS-staged non-temporal 16-B H stores.
+template <typename T>
+constexpr int kAosP = sizeof(T) == 4 ? 2 : 1;
+constexpr int kAosFlags = kNtLoad | kNtStore | kLdsLoad | kLdsDma;
+constexpr int kRectP = 2;
+
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
@@ -298,13 +242,16 @@ inline int launch_status() { return (int)hipGetLastError(); }
 template <int ALGO, bool NORM, typename T>
 int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipStream_t s) {
     if (layout == HG_LAYOUT_SOA) {
-        solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
+        constexpr int V = 16 / sizeof(T);
+        if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H))
+            solve_soa_vec<ALGO, NORM, T><<<generic_grid(n / V), kBlock, 0, s>>>(src, tar, H, n);
+        else
+            solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {
-        constexpr int P = sizeof(T) == 4 ? 4 : 2;
-        const int64_t per_block = (int64_t)kBlock * P;
-        const int64_t blocks = ceil_div(n, per_block);
+        constexpr int P = kAosP<T>;
+        const int64_t blocks = aos_grid<T, P, kAosFlags>(n);
         if (blocks > 0x7fffffffLL) return kErrInvalid;
-        solve_aos_vec<ALGO, NORM, T, P, true><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
+        solve_aos<ALGO, NORM, T, P, kAosFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
     } else {
         solve_generic<ALGO, NORM, T, false><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     }
@@ -330,7 +277,7 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
     if (B == 0) return 0;
     if (!src || !tar || !H || (!SCALAR && (!sp || !dp))) return kErrInvalid;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    constexpr int P = 4;
+    constexpr int P = kRectP;
     const int64_t blocks = ceil_div(B, (int64_t)kBlock * P);
     if (blocks > 0x7fffffffLL) return kErrInvalid;
     if (aligned16(src) && aligned16(tar) && aligned16(H))

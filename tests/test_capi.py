@@ -1,0 +1,117 @@
+"""The C-ABI library loads (no GPU needed) and exports every symbol include/*.h
+declares; argument validation happens before any HIP call.  CPU only."""
+import ctypes
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from conftest import ROOT
+
+INCLUDE = os.path.join(ROOT, "include")
+
+
+def _c_decls():
+    text = open(os.path.join(INCLUDE, "sks_homography.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(hg_\w+)\s*\(", text)))
+
+
+def test_header_declares_expected_entry_points():
+    decls = _c_decls()
+    for name in ("hg_aca_f32", "hg_aca_f64", "hg_sks_f32", "hg_sks_f64",
+                 "hg_tensor_aca_rect_f32", "hg_fill_uniform_f32", "hg_version"):
+        assert name in decls
+
+
+def test_library_exports_every_c_symbol(pkg):
+    lib = pkg.lib()
+    for name in _c_decls():
+        assert hasattr(lib, name), f"{name} declared in sks_homography.h but not exported"
+    assert set(_c_decls()) == set(pkg._lib.SIGNATURES), "ctypes table out of sync with header"
+
+
+def test_cpp_api_links_against_library(pkg):
+    """Every declaration of include/sks_aca_sks.hpp (the reference's sks:: interface)
+    resolves when a C++ program is linked against the library."""
+    prog = r"""
+    #include "sks_aca_sks.hpp"
+    #include <cstdio>
+    int main(int argc, char**) {
+        void* f[] = {(void*)&sks::runKernel_ACA, (void*)&sks::runKernel_ACA_double,
+                     (void*)&sks::runKernel_SKS, (void*)&sks::runKernel_SKS_double,
+                     (void*)&sks::runKernel_ACA_batch, (void*)&sks::runKernel_ACA_double_batch,
+                     (void*)&sks::runKernel_SKS_batch, (void*)&sks::runKernel_SKS_double_batch,
+                     (void*)&hg_aca_f32, (void*)&hg_sks_f64, (void*)&hg_version};
+        if (argc > 5) std::printf("%p", f[0]);
+        // argument validation returns before touching the GPU
+        return sks::runKernel_ACA_batch(nullptr, nullptr, nullptr, -1) == 1 ? 0 : 3;
+    }
+    """
+    libdir = os.path.dirname(pkg._lib.LIB_PATH)
+    with tempfile.TemporaryDirectory() as d:
+        cpp = os.path.join(d, "t.cpp")
+        exe = os.path.join(d, "t")
+        open(cpp, "w").write(prog)
+        subprocess.run(["g++", "-std=c++17", f"-I{INCLUDE}", cpp, f"-L{libdir}",
+                        "-lsks_homography_amd", f"-Wl,-rpath,{libdir}", "-o", exe], check=True)
+        assert subprocess.run([exe]).returncode == 0
+
+
+@pytest.mark.parametrize("fn", ["hg_aca_f32", "hg_aca_f64", "hg_sks_f32", "hg_sks_f64"])
+def test_argument_validation_without_gpu(pkg, fn):
+    lib = pkg.lib()
+    f = getattr(lib, fn)
+    INVALID = 1  # hipErrorInvalidValue
+    assert f(None, None, None, -1, 0, 0, None) == INVALID      # n < 0
+    assert f(None, None, None, 0, 0, 0, None) == 0             # empty batch: no-op
+    assert f(None, None, None, 5, 0, 0, None) == INVALID       # NULL with n > 0
+    assert f(None, None, None, 5, 7, 0, None) == INVALID       # unknown layout
+    assert f(None, None, None, 5, 0, 6, None) == INVALID       # unknown flag bits
+    assert f(None, None, None, 0, 2, 0, None) == INVALID       # layout checked first
+
+
+def test_other_entry_validation(pkg):
+    lib = pkg.lib()
+    assert lib.hg_tensor_aca_rect_f32(None, None, None, -1, None, None, None) == 1
+    assert lib.hg_tensor_aca_rect_f32(None, None, None, 0, None, None, None) == 0
+    assert lib.hg_tensor_aca_rect_f32(None, None, None, 4, None, None, None) == 1
+    assert lib.hg_tensor_aca_rect_f32_hostscalar(None, None, None, 4, 1.0, 1.0, None) == 1
+    assert lib.hg_fill_uniform_f32(None, -3, 0, 0, 0.0, 1.0, None) == 1
+    assert lib.hg_fill_uniform_f32(None, 0, 0, 0, 0.0, 1.0, None) == 0
+    assert lib.hg_sample_solve_f32(None, None, 0, None, None, 4, 0, 0, None) == 1  # npool 0
+    assert lib.hg_sample_solve_f32(None, None, 5, None, None, 4, 9, 0, None) == 1  # algo
+    assert lib.hg_stream_copy(None, None, 17, None) == 1                          # not x16
+    assert lib.hg_stream_copy(None, None, 0, None) == 0
+    assert pkg.version().startswith("sks-homography-amd")
+
+
+def test_product_rejects_cpu_tensors(pkg):
+    """No CPU fallback: host tensors are refused loudly."""
+    import torch
+    x = torch.zeros(4, 8)
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.aca(x, x)
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.tensor_aca_rect(torch.zeros(2, 3, 4), torch.zeros(2, 3, 4), 1.0, 1.0)
+
+
+def test_missing_library_fails_loudly(pkg, monkeypatch):
+    monkeypatch.setattr(pkg._lib, "_lib", None)
+    monkeypatch.setattr(pkg._lib, "LIB_PATH", "/nonexistent/libsks_homography_amd.so")
+    with pytest.raises(ImportError, match="no CPU fallback"):
+        pkg._lib.lib()
+
+
+def test_product_never_imports_oracle():
+    """The product package must not reach the checker."""
+    pkg_dir = os.path.join(ROOT, "sks-homography_amd")
+    forbidden = re.compile(r"import\s+oracle|from\s+oracle|load_oracle|libhg_oracle|libsks_ref|"
+                           r"oracle_\w+\(|ref_batch_f")
+    for dirpath, _, files in os.walk(pkg_dir):
+        for f in files:
+            if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")):
+                text = open(os.path.join(dirpath, f)).read()
+                assert not forbidden.search(text), f"{f} reaches the oracle"

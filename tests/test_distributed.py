@@ -1,0 +1,71 @@
+"""Multi-GPU path on CPU: sharding arithmetic and the gather, world_size 2 over gloo."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import ROOT
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (10, 1), (10, 3), (80_000_000, 8), (7, 8),
+                                     (10_000_001, 4)])
+def test_shard_range_partitions(pkg, n, world):
+    spans = [pkg.shard_range(n, world, r) for r in range(world)]
+    assert spans[0][0] == 0 and spans[-1][1] == n
+    for (a, b), (c, _) in zip(spans, spans[1:]):
+        assert b == c
+    sizes = [b - a for a, b in spans]
+    assert max(sizes) - min(sizes) <= 1
+
+
+def test_shard_range_rejects_bad(pkg):
+    for args in ((10, 0, 0), (10, 2, 2), (-1, 1, 0)):
+        with pytest.raises(ValueError):
+            pkg.shard_range(*args)
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, n_total, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pkg = ge.load_package()
+    lo, hi = pkg.shard_range(n_total, world, rank)
+    # stand-in for the rank's H block: a deterministic function of the global index
+    block = torch.arange(lo, hi, dtype=torch.float32).repeat_interleave(9).view(-1, 9)
+    full = pkg.gather_blocks(block, n_total, world, rank, dst=0)
+    # max-over-ranks timing reduction used by bench.py
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    if rank == 0:
+        want = torch.arange(n_total, dtype=torch.float32).repeat_interleave(9).view(-1, 9)
+        q.put((bool(torch.equal(full, want)), float(t.item())))
+    else:
+        q.put((full is None, float(t.item())))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world,n_total", [(2, 1001), (3, 10)])
+def test_gather_blocks_gloo(world, n_total):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, n_total, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for ok, _ in res)
+    assert all(m == float(world) for _, m in res)

@@ -1,0 +1,81 @@
+"""HBM traffic per launch from rocprofv3 PMC passes (FETCH_SIZE, WRITE_SIZE).
+
+Usage: python tools/pmc_traffic.py <fetch_dir> <write_dir> [out.json]
+
+Corrections (MI355X_MICROARCH.md "HBM" + cdna_hip_programming.md section 7):
+  * both counters are in KiB -> x1024;
+  * on gfx950 FETCH_SIZE reports half the bytes of a wide coalesced streaming read
+    -> x2.  Verified here on hg::stream_copy_kernel, whose byte count is known
+    exactly: the x2-corrected fetch must equal the bytes copied (check printed and
+    stored as "calibration");
+  * WRITE_SIZE reads exact for 16-B-per-lane streaming stores.
+Counters were collected in separate passes (FETCH_SIZE and WRITE_SIZE cannot share
+one), with no tracing domains, as the guide prescribes.
+"""
+from __future__ import annotations
+
+import collections
+import csv
+import glob
+import json
+import os
+import statistics
+import sys
+
+KEYS = {
+    # key: (kernel-name prefix, algorithmic bytes per launch or None, grid filter)
+    "aca_f32_aos_norm": ("void hg::solve_aos<0, true, float", 10_000_000 * 100),
+    "sks_f32_aos_norm": ("void hg::solve_aos<1, true, float", 10_000_000 * 100),
+    "stream_copy": ("hg::stream_copy_kernel", None),
+    "tensor_aca_rect": ("void hg::tensor_aca_rect_kernel", None),
+}
+
+
+def load(d):
+    path = glob.glob(os.path.join(d, "*counter_collection.csv"))[0]
+    per = collections.defaultdict(list)
+    for r in csv.DictReader(open(path)):
+        per[(r["Kernel_Name"], int(r["Grid_Size"]))].append(float(r["Counter_Value"]))
+    return per
+
+
+def main():
+    fetch, write = load(sys.argv[1]), load(sys.argv[2])
+    out_path = sys.argv[3] if len(sys.argv) > 3 else None
+    res = {}
+    for key, (prefix, algo_bytes) in KEYS.items():
+        groups = sorted({g for (k, g) in fetch if k.startswith(prefix)})
+        for g in groups:
+            f = [v for (k, gg), vs in fetch.items() if k.startswith(prefix) and gg == g for v in vs]
+            w = [v for (k, gg), vs in write.items() if k.startswith(prefix) and gg == g for v in vs]
+            if not f or not w:
+                continue
+            fb = statistics.median(f) * 1024 * 2
+            wb = statistics.median(w) * 1024
+            name = key if len(groups) == 1 else f"{key}@grid{g}"
+            res[name] = {"fetch_bytes": fb, "write_bytes": wb, "hbm_bytes": fb + wb,
+                         "fetch_kib_raw": statistics.median(f), "write_kib_raw": statistics.median(w),
+                         "launches": len(f), "grid": g}
+            if algo_bytes:
+                res[name]["algorithmic_bytes"] = algo_bytes
+                res[name]["traffic_over_algorithmic"] = round((fb + wb) / algo_bytes, 4)
+    # calibration on the copy kernel: bytes copied == bytes written (exact counter)
+    cp = next((v for k, v in res.items() if k.startswith("stream_copy")), None)
+    if cp:
+        cp["calibration"] = {"fetch_x2_over_written": round(cp["fetch_bytes"] / cp["write_bytes"], 4)}
+    # flat per-launch numbers bench.py reads
+    flat = {k: round(v["hbm_bytes"]) for k, v in res.items() if k in ("aca_f32_aos_norm",
+                                                                      "sks_f32_aos_norm")}
+    doc = dict(flat)
+    doc["detail"] = res
+    doc["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, csv; "
+                     "bytes = KiB*1024, FETCH x2 (gfx950 wide-read correction, calibrated on "
+                     "stream_copy); median over launches of `python3 bench.py --no-cpu --steps 20`")
+    print(json.dumps(doc, indent=1))
+    if out_path:
+        with open(out_path, "w") as fh:
+            json.dump(doc, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
