@@ -36,6 +36,21 @@ def test_oracle_vs_reference_cpp_edge(orc, oracle, algo):
                  f"{algo} edge f64")
 
 
+@pytest.mark.parametrize("dtype", [np.float32, np.float64])
+def test_oracle_vs_compiled_reference_random(orc, oracle, dtype):
+    """Where the reference was compiled (oracle/_ref, built from /root/reference),
+    the restatement must equal it on fresh random quads too."""
+    if not orc.RefOracle.available():
+        pytest.skip("oracle/_ref not built here")
+    ref = orc.RefOracle()
+    rng = np.random.default_rng(123)
+    n = 200_000
+    s = rng.uniform(-3000, 3000, (n, 8)).astype(dtype)
+    t = rng.uniform(-3000, 3000, (n, 8)).astype(dtype)
+    for algo in ("aca", "sks"):
+        _assert_bits(orc, oracle.solve(algo, s, t), ref.solve(algo, s, t), f"{algo} {dtype}")
+
+
 def test_oracle_soa_equals_aos(orc, oracle):
     g = load_golden("cpp_uniform.npz")
     for algo in ("aca", "sks"):
