@@ -19,6 +19,10 @@ const char* hg_tune_variant_name(int variant);
 int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, float* H,
                     int64_t n, int per_cu, void* stream);
 
+/* Streaming-copy yardstick variants: 0 = 4x16 B/lane nt, 1 = 8x16 B/lane nt,
+ * 2 = 4x16 B/lane plain, 3 = LDS-DMA 8 KiB per wave (bytes % 32 KiB == 0). */
+int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -25,7 +25,7 @@ int launch_variant(int algo, const float* s, const float* t, float* H, int64_t n
 }
 
 const Variant kVariants[] = {
-    {"P4 nt-ld nt-st stage (shipped)", launch_variant<4, kNtLoad | kNtStore>},
+    {"P4 nt-ld nt-st stage (first version)", launch_variant<4, kNtLoad | kNtStore>},
     {"P4 plain", launch_variant<4, 0>},
     {"P4 nt-ld", launch_variant<4, kNtLoad>},
     {"P4 nt-st", launch_variant<4, kNtStore>},
@@ -47,11 +47,69 @@ const Variant kVariants[] = {
     {"P4 nt-ld lds-load plain-st", launch_variant<4, kNtLoad | kLdsLoad>},
     {"P2 nt stage", launch_variant<2, kNtLoad | kNtStore>},
     {"P2 nt lds-dma persist", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kPersist>},
+    {"P1 nt lds-dma", launch_variant<1, kNtLoad | kNtStore | kLdsLoad | kLdsDma>},
+    {"P2 lds-dma nt-ld plain-st", launch_variant<2, kNtLoad | kLdsLoad | kLdsDma>},
+    {"P3 nt lds-dma", launch_variant<3, kNtLoad | kNtStore | kLdsLoad | kLdsDma>},
 };
+
+// Streaming-copy variants for the bandwidth yardstick.
+template <int U, bool NT>
+__global__ __launch_bounds__(kBlock) void copy_unrolled(const u32x4* __restrict__ src,
+                                                        u32x4* __restrict__ dst, int64_t n16) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) v[u] = ld16<NT>(src + i);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) st16<NT>(dst + i, v[u]);
+    }
+}
+
+// LDS-DMA copy: each wave moves 8 KiB through LDS per iteration.
+__global__ __launch_bounds__(kBlock) void copy_dma(const char* __restrict__ src,
+                                                   char* __restrict__ dst, int64_t bytes) {
+    constexpr int kSlab = 8192;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kSlab];
+    const int lane = threadIdx.x & 63, wave = threadIdx.x / 64;
+    const int64_t slab = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    if ((slab + 1) * kSlab > bytes) return;
+    const char* const g[1] = {src + slab * kSlab};
+    char* const l[1] = {smem[wave]};
+    slabs_to_lds<kSlab, 1, true, true>(g, l, lane);
+#pragma unroll
+    for (int c = 0; c < kSlab / 1024; ++c)
+        st16<true>(dst + slab * kSlab + 16 * (c * 64 + lane),
+                   *reinterpret_cast<const u32x4*>(smem[wave] + 16 * (c * 64 + lane)));
+}
 
 }  // namespace
 
 extern "C" {
+
+// variant 0: U=4 nt, 1: U=8 nt, 2: U=4 plain, 3: LDS-DMA (bytes % 32 KiB == 0)
+int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* stream) {
+    if (bytes <= 0 || (bytes & 15)) return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n16 = bytes / 16;
+    const auto* s = reinterpret_cast<const u32x4*>(src);
+    auto* d = reinterpret_cast<u32x4*>(dst);
+    switch (variant) {
+        case 0: copy_unrolled<4, true><<<(unsigned)((n16 + 1023) / 1024), kBlock, 0, st>>>(s, d, n16); break;
+        case 1: copy_unrolled<8, true><<<(unsigned)((n16 + 2047) / 2048), kBlock, 0, st>>>(s, d, n16); break;
+        case 2: copy_unrolled<4, false><<<(unsigned)((n16 + 1023) / 1024), kBlock, 0, st>>>(s, d, n16); break;
+        case 3:
+            if (bytes % 32768) return (int)hipErrorInvalidValue;
+            copy_dma<<<(unsigned)(bytes / 32768), kBlock, 0, st>>>((const char*)src, (char*)dst, bytes);
+            break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
 
 int hg_tune_num_variants(void) { return (int)(sizeof(kVariants) / sizeof(kVariants[0])); }
 

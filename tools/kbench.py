@@ -40,7 +40,11 @@ def main():
     sp = stream.cuda_stream
     nv = lib.hg_tune_num_variants()
     cases = []
+    only = os.environ.get("KB_VARIANTS")
+    keep = set(int(x) for x in only.split(",")) if only else set(range(nv))
     for v in range(nv):
+        if v not in keep:
+            continue
         name = lib.hg_tune_variant_name(v).decode()
         per = [8] if "persist" not in name else [2, 4, 8, 16]
         for pc in per:
@@ -81,6 +85,29 @@ def main():
         e1.record(stream)
         e1.synchronize()
         copy_t.append(e0.elapsed_time(e1) / iters)
+    # copy-yardstick variants (hg_tune_copy), same byte count, interleaved
+    lib.hg_tune_copy.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                 ctypes.c_void_p]
+    lib.hg_tune_copy.restype = ctypes.c_int
+    nbc = nb // 32768 * 32768
+    ctimes = {v: [] for v in range(4)}
+    for v in range(4):
+        assert lib.hg_tune_copy(v, a.data_ptr(), b.data_ptr(), nbc, sp) == 0
+    torch.cuda.synchronize()
+    for r in range(rounds):
+        for v in range(4):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(iters):
+                lib.hg_tune_copy(v, a.data_ptr(), b.data_ptr(), nbc, sp)
+            e1.record(stream)
+            e1.synchronize()
+            ctimes[v].append(e0.elapsed_time(e1) / iters)
+    copy_variants = {}
+    for v, name in enumerate(["U4 nt", "U8 nt", "U4 plain", "LDS-DMA 8K/wave"]):
+        med = statistics.median(ctimes[v])
+        copy_variants[name] = round(2 * nbc / (med * 1e-3) / 1e9, 1)
+        print(f"copy variant {name}: {copy_variants[name]} GB/s")
     out = []
     cmed = statistics.median(copy_t)
     print(f"copy yardstick: {2 * nb / (cmed * 1e-3) / 1e9:.1f} GB/s ({cmed * 1e3:.1f} us)")
@@ -96,7 +123,8 @@ def main():
         print(json.dumps(rec))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
     with open(os.path.join(ROOT, "gpurun_out", "kbench.json"), "w") as f:
-        json.dump({"n": n, "copy_gbps": 2 * nb / (cmed * 1e-3) / 1e9, "cases": out}, f, indent=1)
+        json.dump({"n": n, "copy_gbps": 2 * nb / (cmed * 1e-3) / 1e9,
+                   "copy_variants_gbps": copy_variants, "cases": out}, f, indent=1)
 
 
 if __name__ == "__main__":
