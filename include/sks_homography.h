@@ -73,6 +73,16 @@ int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t
 int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float* H, int64_t B,
                                       float scale, float div, void* stream);
 
+/* Backward of hg_tensor_aca_rect_f32 (the gradients ATen autograd gives the
+ * reference's composed TensorACA_rect, Modules_Runtime_Test.py:294-302).  grad_H:
+ * (B,3,3) dL/dH.  Writes grad_tar (B,3,4); grad_src (B,3,4, only [0][0] and [1][0]
+ * non-zero) when non-NULL; grad_scale_div (B,2) per-problem partials of dL/dscale and
+ * dL/ddiv when non-NULL (the caller sums them).  scale, div: device pointers. */
+int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
+                                    int64_t B, const float* scale, const float* div,
+                                    float* grad_src, float* grad_tar, float* grad_scale_div,
+                                    void* stream);
+
 /* Synthetic input stream: out[i] = lo + (hi - lo) * u(i), u(i) = top 24 bits of
  * splitmix64(seed * 0xD1B54A32D192ED03 + offset + i) * 2^-24.  Counter based, so a
  * rank can generate its own shard (offset = first element) and a host can

@@ -297,3 +297,63 @@ double oracle_time_f32(int algo, const float* src, const float* tar, float* H, i
     clock_gettime(CLOCK_MONOTONIC, &t1);
     return (double)(t1.tv_sec - t0.tv_sec) + 1e-9 * (double)(t1.tv_nsec - t0.tv_nsec);
 }
+
+/* ------------------------------------------------- TensorACA backward ------ */
+/* dL/dtar, dL/dsrc (M's x, y), dL/dscale, dL/ddiv for TensorACA_rect given
+ * dL/dH -- the gradient ATen autograd produces for .py:294-302,
+ * restated in the product kernel's fixed evaluation order (every op rounded on its
+ * own except the forward's cross-product FMAs).  gsd: (B,2) per-problem partials. */
+int oracle_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* gH,
+                                        int64_t B, float scale, float div, float* gsrc,
+                                        float* gtar, float* gsd) {
+    for (int64_t i = 0; i < B; ++i) {
+        const float* t = tar + i * 12;
+        const float* g = gH + i * 9;
+        float* gt = gtar + i * 12;
+        const float mx = src[i * 12 + 0], my = src[i * 12 + 4];
+        float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4];
+        float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0];
+        float c0 = fmaf(ay, bz, -(az * by));
+        float c1 = fmaf(az, bx, -(ax * bz));
+        float c2 = fmaf(ax, by, -(ay * bx));
+        float S = (c0 + c1) + c2;
+        float gc0 = 0.f, gc1 = 0.f, gS = 0.f, gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
+        for (int r = 0; r < 3; ++r) {
+            float br = S * t[4 * r];
+            float h0 = t[4 * r + 1] * c0 - br;
+            float x = t[4 * r + 2] * c1 - br;
+            float h1 = div * x;
+            float g2 = g[3 * r + 2];
+            float gh0 = g[3 * r + 0] - mx * g2;
+            float gh1 = g[3 * r + 1] - my * g2;
+            gmx = gmx - g2 * h0;
+            gmy = gmy - g2 * h1;
+            gsc = gsc + g2 * br;
+            float gx = div * gh1;
+            gdv = gdv + gh1 * x;
+            float gb = (scale * g2 - gh0) - gx;
+            gt[4 * r + 0] = gb * S;
+            gt[4 * r + 1] = gh0 * c0;
+            gt[4 * r + 2] = gx * c1;
+            gt[4 * r + 3] = 0.f;
+            gc0 = gc0 + gh0 * t[4 * r + 1];
+            gc1 = gc1 + gx * t[4 * r + 2];
+            gS = gS + gb * t[4 * r];
+        }
+        gc0 = gc0 + gS;
+        gc1 = gc1 + gS;
+        float gc2 = gS;
+        float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
+        float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
+        gt[5] = gt[5] + gax; gt[6] = gt[6] + gay; gt[7] = gt[7] + gaz;
+        gt[4] = gt[4] - ((gax + gay) + gaz);
+        gt[1] = gt[1] + gbx; gt[2] = gt[2] + gby; gt[3] = gt[3] + gbz;
+        gt[0] = gt[0] - ((gbx + gby) + gbz);
+        for (int k = 0; k < 12; ++k) gsrc[i * 12 + k] = 0.f;
+        gsrc[i * 12 + 0] = gmx;
+        gsrc[i * 12 + 4] = gmy;
+        gsd[i * 2 + 0] = gsc;
+        gsd[i * 2 + 1] = gdv;
+    }
+    return 0;
+}

@@ -49,6 +49,10 @@ class Oracle:
         lib.oracle_fill_uniform_f32.argtypes = [_f32p, _i64, ctypes.c_uint64, ctypes.c_uint64,
                                                 ctypes.c_float, ctypes.c_float]
         lib.oracle_fill_uniform_f32.restype = ctypes.c_int
+        lib.oracle_tensor_aca_rect_backward_f32.argtypes = [_f32p, _f32p, _f32p, _i64,
+                                                            ctypes.c_float, ctypes.c_float,
+                                                            _f32p, _f32p, _f32p]
+        lib.oracle_tensor_aca_rect_backward_f32.restype = ctypes.c_int
         lib.oracle_time_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64,
                                         ctypes.c_int, ctypes.c_int]
         lib.oracle_time_f32.restype = ctypes.c_double
@@ -79,6 +83,20 @@ class Oracle:
         self.lib.oracle_tensor_aca_rect_f32(_ptr(src, _f32p), _ptr(tar, _f32p), _ptr(H, _f32p),
                                             B, float(np.float32(scale)), float(np.float32(div)))
         return H
+
+    def tensor_aca_rect_backward(self, src, tar, gH, scale: float, div: float):
+        """Returns (grad_src (B,3,4), grad_tar (B,3,4), per-problem (B,2) [dscale, ddiv])."""
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tar = np.ascontiguousarray(tar, dtype=np.float32)
+        gH = np.ascontiguousarray(gH, dtype=np.float32)
+        B = tar.shape[0]
+        gs = np.empty((B, 3, 4), np.float32)
+        gt = np.empty((B, 3, 4), np.float32)
+        gsd = np.empty((B, 2), np.float32)
+        self.lib.oracle_tensor_aca_rect_backward_f32(
+            _ptr(src, _f32p), _ptr(tar, _f32p), _ptr(gH, _f32p), B, float(np.float32(scale)),
+            float(np.float32(div)), _ptr(gs, _f32p), _ptr(gt, _f32p), _ptr(gsd, _f32p))
+        return gs, gt, gsd
 
     def fill_uniform(self, count: int, seed: int, offset: int = 0, lo: float = 0.0,
                      hi: float = 1024.0) -> np.ndarray:

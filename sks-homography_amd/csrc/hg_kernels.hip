@@ -112,6 +112,39 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// TensorACA rect backward: one lane per problem, grid-stride.  Writes dL/dtar
+// (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and the
+// per-problem (dL/dscale, dL/ddiv) partials (B,2) that the caller reduces.
+template <bool WANT_SRC, bool WANT_SD>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float* __restrict__ gsrc, float* __restrict__ gtar, float* __restrict__ gsd) {
+    const float scale = scale_p[0], div = div_p[0];
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float tr[12], g[9], gt[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        float gmx, gmy, gscale, gdiv;
+        tensor_aca_rect_grad(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx, gmy,
+                             gscale, gdiv);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
+        if constexpr (WANT_SRC) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
+        }
+        if constexpr (WANT_SD) {
+            gsd[p * 2 + 0] = gscale;
+            gsd[p * 2 + 1] = gdiv;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // SoA vector kernel (the reference GPU layout, GPU_Runtime Test.cu:87-95 and
 // :141-149): lane owns V = 16/sizeof(T) consecutive problems and moves each of the
 // 8 + 8 input and 9 output components as one 16-B access (rows are 16-B aligned
@@ -324,6 +357,27 @@ int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t
 int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float* H, int64_t B,
                                       float scale, float div, void* stream) {
     return hg::launch_rect<true>(src, tar, H, B, nullptr, nullptr, scale, div, stream);
+}
+
+int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
+                                    int64_t B, const float* scale, const float* div,
+                                    float* grad_src, float* grad_tar, float* grad_scale_div,
+                                    void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const unsigned g = hg::generic_grid(B);
+    const bool ws = grad_src != nullptr, wd = grad_scale_div != nullptr;
+#define HG_RECT_BWD(A, Bf)                                                                    \
+    hg::tensor_aca_rect_backward_kernel<A, Bf><<<g, hg::kBlock, 0, s>>>(                      \
+        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
+    if (ws && wd) HG_RECT_BWD(true, true);
+    else if (ws) HG_RECT_BWD(true, false);
+    else if (wd) HG_RECT_BWD(false, true);
+    else HG_RECT_BWD(false, false);
+#undef HG_RECT_BWD
+    return hg::launch_status();
 }
 
 int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,

@@ -167,4 +167,60 @@ __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], flo
     }
 }
 
+// Reverse-mode derivative of tensor_aca_rect_solve (the gradients ATen autograd
+// gives the reference's composed TensorACA_rect, .py:294-302).
+// In: the forward's inputs and g = dL/dH (3x3).  Out: gt = dL/dtar (3,4), gmx/gmy =
+// dL/d src[0][0], src[1][0], gscale / gdiv = this problem's share of dL/dscale,
+// dL/ddiv.  Fixed evaluation order (restated op for op in oracle/hg_oracle.c).
+__device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,
+                                                     float scale, float div, const float (&g)[9],
+                                                     float (&gt)[12], float& gmx, float& gmy,
+                                                     float& gscale, float& gdiv) {
+    const float ax = tr[5] - tr[4], ay = tr[6] - tr[4], az = tr[7] - tr[4];
+    const float bx = tr[1] - tr[0], by = tr[2] - tr[0], bz = tr[3] - tr[0];
+    const float c0 = __builtin_fmaf(ay, bz, -(az * by));
+    const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
+    const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
+    const float sum = (c0 + c1) + c2;
+    float gc0 = 0.f, gc1 = 0.f, gs = 0.f;
+    gmx = 0.f; gmy = 0.f; gscale = 0.f; gdiv = 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        const float b = sum * tr[4 * r];
+        const float h0 = tr[4 * r + 1] * c0 - b;
+        const float x = tr[4 * r + 2] * c1 - b;
+        const float h1 = div * x;
+        const float g2 = g[3 * r + 2];
+        const float gh0 = g[3 * r + 0] - mx * g2;
+        const float gh1 = g[3 * r + 1] - my * g2;
+        gmx = gmx - g2 * h0;
+        gmy = gmy - g2 * h1;
+        gscale = gscale + g2 * b;
+        const float gx = div * gh1;
+        gdiv = gdiv + gh1 * x;
+        const float gb = (scale * g2 - gh0) - gx;
+        gt[4 * r + 0] = gb * sum;
+        gt[4 * r + 1] = gh0 * c0;
+        gt[4 * r + 2] = gx * c1;
+        gt[4 * r + 3] = 0.f;
+        gc0 = gc0 + gh0 * tr[4 * r + 1];
+        gc1 = gc1 + gx * tr[4 * r + 2];
+        gs = gs + gb * tr[4 * r];
+    }
+    gc0 = gc0 + gs;
+    gc1 = gc1 + gs;
+    const float gc2 = gs;
+    // c = a x b:  dL/da = b x gc,  dL/db = gc x a
+    const float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
+    const float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
+    gt[5] = gt[5] + gax;
+    gt[6] = gt[6] + gay;
+    gt[7] = gt[7] + gaz;
+    gt[4] = gt[4] - ((gax + gay) + gaz);
+    gt[1] = gt[1] + gbx;
+    gt[2] = gt[2] + gby;
+    gt[3] = gt[3] + gbz;
+    gt[0] = gt[0] - ((gbx + gby) + gbz);
+}
+
 }  // namespace hg

@@ -9,7 +9,7 @@ tensor_aca_rect}`` (the op contract of SURVEY.md section 8(b)).
 """
 from __future__ import annotations
 
-from typing import Optional, Union
+from typing import Optional, Tuple, Union
 
 import torch
 
@@ -124,6 +124,40 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     return out
 
 
+def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor,
+                             scale: torch.Tensor, div: torch.Tensor, need_src: bool = True,
+                             need_scale_div: bool = True):
+    """Gradients of tensor_aca_rect: (dL/dsrc (B,3,4) or empty, dL/dtar (B,3,4),
+    [dL/dscale, dL/ddiv] (2,) or empty).  The per-problem scale/div partials from the
+    kernel are summed here (deterministically, in float32)."""
+    dev = _require_device(src, tar, grad)
+    src, tar, grad = src.contiguous(), tar.contiguous(), grad.contiguous()
+    B = tar.shape[0]
+    sc = torch.as_tensor(scale, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+    dv = torch.as_tensor(div, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+    g_tar = torch.empty((B, 3, 4), dtype=torch.float32, device=dev)
+    g_src = torch.empty((B, 3, 4) if need_src else (0,), dtype=torch.float32, device=dev)
+    part = torch.empty((B, 2) if need_scale_div else (0,), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("hg_tensor_aca_rect_backward_f32", src.data_ptr(), tar.data_ptr(),
+                  grad.data_ptr(), B, sc.data_ptr(), dv.data_ptr(),
+                  g_src.data_ptr() if need_src and B else None, g_tar.data_ptr(),
+                  part.data_ptr() if need_scale_div and B else None, _stream(dev))
+    g_sd = part.sum(0) if need_scale_div else part
+    return g_src, g_tar, g_sd
+
+
+def tensor_aca_rect_autograd(src: torch.Tensor, tar: torch.Tensor, scale: Scalar,
+                             div: Scalar) -> torch.Tensor:
+    """Differentiable TensorACA (torch.ops.sks_amd.tensor_aca_rect): gradients flow to
+    tar, src (M's coordinates), and scale/div when they are tensors requiring grad."""
+    dev = _require_device(src, tar)
+    sc = scale if isinstance(scale, torch.Tensor) else torch.tensor([float(scale)], device=dev)
+    dv = div if isinstance(div, torch.Tensor) else torch.tensor([float(div)], device=dev)
+    return torch.ops.sks_amd.tensor_aca_rect(src, tar, sc.to(torch.float32),
+                                             dv.to(torch.float32))
+
+
 def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: float = 1024.0,
                  device: Union[str, torch.device] = "cuda", out=None) -> torch.Tensor:
     """Counter-based U[lo,hi) float32 stream generated on the device."""
@@ -194,6 +228,35 @@ def _register_ops() -> None:
     @_rect.register_fake
     def _(src, tar, scale, div):
         return tar.new_empty((tar.shape[0], 3, 3))
+
+    @torch.library.custom_op(f"{_NS}::tensor_aca_rect_backward", mutates_args=())
+    def _rect_bwd(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor, scale: torch.Tensor,
+                  div: torch.Tensor, need_src: bool,
+                  need_scale_div: bool) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+        return tensor_aca_rect_backward(src, tar, grad, scale, div, need_src, need_scale_div)
+
+    @_rect_bwd.register_fake
+    def _(src, tar, grad, scale, div, need_src, need_scale_div):
+        B = tar.shape[0]
+        return (tar.new_empty((B, 3, 4) if need_src else (0,)), tar.new_empty((B, 3, 4)),
+                tar.new_empty((2,) if need_scale_div else (0,)))
+
+    def _setup(ctx, inputs, output):
+        src, tar, scale, div = inputs
+        ctx.save_for_backward(src, tar, scale, div)
+
+    def _backward(ctx, grad):
+        src, tar, scale, div = ctx.saved_tensors
+        need_src = ctx.needs_input_grad[0]
+        need_sd = ctx.needs_input_grad[2] or ctx.needs_input_grad[3]
+        g_src, g_tar, g_sd = torch.ops.sks_amd.tensor_aca_rect_backward(
+            src, tar, grad.contiguous(), scale, div, need_src, need_sd)
+        g_scale = g_sd[0:1].reshape(scale.shape) if ctx.needs_input_grad[2] else None
+        g_div = g_sd[1:2].reshape(div.shape) if ctx.needs_input_grad[3] else None
+        return (g_src if need_src else None, g_tar if ctx.needs_input_grad[1] else None,
+                g_scale, g_div)
+
+    _rect.register_autograd(_backward, setup_context=_setup)
 
 
 _register_ops()

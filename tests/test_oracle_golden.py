@@ -128,3 +128,39 @@ def test_uniform_stream_known_values(oracle):
     assert a.dtype == np.float32 and (a >= 0).all() and (a < 1024).all()
     # a pinned value so the generator cannot drift silently
     assert a[:4].tolist() == pytest.approx(oracle.fill_uniform(4, 11, 0).tolist())
+
+
+def _functional_rect(src, tar, scale, div):
+    """Out-of-place statement of the reference composition (.py:296-302); the
+    reference writes H by slices in place, which autograd can differentiate w.r.t.
+    tar/scale/div but not w.r.t. src."""
+    d = tar[:, :, 1:] - tar[:, :, 0:1]
+    q = torch.cross(d[:, 1:2, :], d[:, 0:1, :], dim=2)
+    b = q.sum(2, keepdim=True) * tar[:, :, 0:1]
+    h0 = tar[:, :, 1:2] * q[:, :, 0:1] - b
+    h1 = div * (tar[:, :, 2:3] * q[:, :, 1:2] - b)
+    h2 = scale * b - src[:, 0:1, 0:1] * h0 - src[:, 1:2, 0:1] * h1
+    return torch.cat([h0, h1, h2], 2)
+
+
+@pytest.mark.parametrize("scale,div", [(128.0, 1.0), (50.0, 1.25)])
+def test_oracle_rect_backward_vs_autograd_f64(oracle, scale, div):
+    """The hand-derived TensorACA gradient against float64 autograd of
+    the reference composition."""
+    g = load_golden("torch_tensor_aca.npz")
+    sh, th = torch.from_numpy(g["f_src_h"]), torch.from_numpy(g["f_tar_h"])
+    gH = torch.randn(th.shape[0], 3, 3, generator=torch.Generator().manual_seed(1))
+    gs, gt, gsd = oracle.tensor_aca_rect_backward(sh.numpy(), th.numpy(), gH.numpy(), scale, div)
+    s64 = sh.double().requires_grad_()
+    t64 = th.double().requires_grad_()
+    sc = torch.tensor([scale], dtype=torch.float64, requires_grad=True)
+    dv = torch.tensor([div], dtype=torch.float64, requires_grad=True)
+    _functional_rect(s64, t64, sc, dv).backward(gH.double())
+
+    def rel(a, b):
+        return float(np.abs(a - b).max() / np.abs(b).max())
+
+    assert rel(gt, t64.grad.numpy()) < 1e-6
+    assert rel(gs, s64.grad.numpy()) < 1e-6
+    assert abs(gsd[:, 0].astype(np.float64).sum() / sc.grad.item() - 1) < 1e-5
+    assert abs(gsd[:, 1].astype(np.float64).sum() / dv.grad.item() - 1) < 1e-5
