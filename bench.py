@@ -275,7 +275,29 @@ def main():
         for _ in range(5):
             pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb)
         _, ms_b = timed_region(d, lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb), 50)
+        # compact form (corner + 4 offsets) on the same big batch
+        corner = bs_h[:, 0:2, 0].contiguous()
+        offs = (bt_h[:, 0:2, :] - bs_h[:, 0:2, :]).transpose(1, 2).contiguous()
+        Ho = torch.empty((big, 3, 3), device=d.dev)
+        f_off = lambda: pkg.ops.tensor_aca_offsets(corner, offs, 128.0, 128.0, out=Ho)  # noqa
+        for _ in range(5):
+            f_off()
+        _, ms_ob = timed_region(d, f_off, 50)
+        c64, o64 = corner[:args.rect_batch].contiguous(), offs[:args.rect_batch].contiguous()
+        Hs = torch.empty((args.rect_batch, 3, 3), device=d.dev)
+        f_os = lambda: pkg.ops.tensor_aca_offsets(c64, o64, 128.0, 128.0, out=Hs)  # noqa
+        for _ in range(100):
+            f_os()
+        _, ms_os = timed_region(d, f_os, 1000)
+        del corner, offs, Ho
         rb = pkg.RECT_BYTES_PER_PROBLEM
+        line["tensor_aca_offsets"] = {
+            "batch": args.rect_batch, "us_per_call": round(ms_os * 1e3, 3),
+            "large_batch": big, "large_us_per_call": round(ms_ob * 1e3, 2),
+            "large_achieved_gbps": round(big * 76 / (ms_ob * 1e-3) / 1e9, 1),
+            "large_frac": round(big * 76 / (ms_ob * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "bytes_per_problem": 76,
+        }
         line["tensor_aca_rect"] = {
             "batch": args.rect_batch, "us_per_call": round(ms_o * 1e3, 3),
             "torch_composed_us_per_call": round(ms_t * 1e3, 3),

@@ -83,6 +83,22 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
                                     void* stream);
 
+/* Compact TensorACA for deep-homography nets: the source is the
+ * axis-aligned width x height rectangle with top-left corner (B,2) -- getInput's shape,
+ * Modules_Runtime_Test.py:9-16 -- and the target is source + offsets (B,4,2), the
+ * 4-corner offsets a network predicts (getTar, .py:19-21).  Identical bits to
+ * building the (B,3,4) tensors with float adds and calling hg_tensor_aca_rect_f32
+ * with scale = width, div = width / height; moves 76 B per problem instead of 132. */
+int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,
+                              float width, float height, void* stream);
+
+/* Backward of hg_tensor_aca_offsets_f32: grad_offsets (B,4,2); grad_corner (B,2) when
+ * non-NULL. */
+int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets,
+                                       const float* grad_H, int64_t B, float width,
+                                       float height, float* grad_offsets, float* grad_corner,
+                                       void* stream);
+
 /* Synthetic input stream: out[i] = lo + (hi - lo) * u(i), u(i) = top 24 bits of
  * splitmix64(seed * 0xD1B54A32D192ED03 + offset + i) * 2^-24.  Counter based, so a
  * rank can generate its own shard (offset = first element) and a host can

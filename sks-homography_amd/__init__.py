@@ -16,7 +16,8 @@ from __future__ import annotations
 from . import _lib
 from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib, version
 from .ops import (aca, fill_uniform, sample_solve, sks, solve, stream_copy, tensor_aca_rect,
-                  tensor_aca_rect_autograd, tensor_aca_rect_backward)
+                  tensor_aca_rect_autograd, tensor_aca_rect_backward,
+                  tensor_aca_offsets, tensor_aca_offsets_backward)
 from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
 from .shard import gather_blocks, shard_range
 
@@ -25,7 +26,8 @@ RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H (SURV
 
 __all__ = [
     "aca", "sks", "solve", "tensor_aca_rect", "tensor_aca_rect_autograd",
-    "tensor_aca_rect_backward", "fill_uniform", "sample_solve", "stream_copy",
+    "tensor_aca_rect_backward", "tensor_aca_offsets", "tensor_aca_offsets_backward",
+    "fill_uniform", "sample_solve", "stream_copy",
     "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
     "gather_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
     "HG_FLAG_NORMALIZE", "BYTES_PER_PROBLEM", "RECT_BYTES_PER_PROBLEM",

@@ -30,6 +30,10 @@ SIGNATURES = {
     "hg_tensor_aca_rect_f32_hostscalar": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
                                            _vp], _int),
     "hg_tensor_aca_rect_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
+    "hg_tensor_aca_offsets_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
+                                  _int),
+    "hg_tensor_aca_offsets_backward_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
+                                           _vp, _vp, _vp], _int),
     "hg_fill_uniform_f32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
                              ctypes.c_float, _vp], _int),
     "hg_sample_solve_f32": ([_vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _int, _vp], _int),

@@ -92,6 +92,22 @@ __device__ __forceinline__ void slabs_to_lds(const char* const (&g)[NS], char* c
     wave_lds_sync();
 }
 
+// Issue-only LDS-DMA of one kBytes slab (no wait): for slabs of different sizes,
+// issue each, then call dma_wait_sync() once.
+template <int kBytes, bool NT>
+__device__ __forceinline__ void dma_slab_issue(const char* __restrict__ g, char* l, int lane) {
+    static_assert(kBytes % (16 * kWave) == 0, "slab must be whole 1 KiB pieces");
+#pragma unroll
+    for (int c = 0; c < kBytes / (16 * kWave); ++c)
+        __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + 16 * (c * kWave + lane)),
+                                         (lds_ptr_t)(l + 16 * c * kWave), 16, 0, NT ? 2 : 0);
+}
+
+__device__ __forceinline__ void dma_wait_sync() {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    wave_lds_sync();
+}
+
 // Writes a wave's 64*P rows of 9 T (36/72-B rows, not 16-B aligned per lane) to
 // the contiguous slab `out`: rows are staged in LDS at a 9-element stride (odd dword
 // stride: conflict-free ds_write_b32), then every lane stores consecutive 16-B chunks.

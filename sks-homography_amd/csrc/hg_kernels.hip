@@ -145,6 +145,90 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// Compact TensorACA: corner (B,2) + offsets (B,4,2) -> H (B,3,3) = 8 + 32 + 36 B per
+// problem instead of the (B,3,4) tensors' 48 + 48 + 36.  Full tiles: both slabs by
+// LDS-DMA (P = 2: 1 KiB of corners + 4 KiB of offsets per wave), staged 16-B H stores.
+template <int P, bool VEC>
+__global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
+    const float* __restrict__ corner, const float* __restrict__ offsets, float* __restrict__ H,
+    int64_t B, float w, float h) {
+    constexpr int kTile = kWave * P;
+    constexpr int kCorner = kTile * 8, kOff = kTile * 32;
+    constexpr int kLds = kCorner + kOff > kTile * 36 ? kCorner + kOff : kTile * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][VEC ? kLds : 16];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= B) return;
+    const float div = w / h;
+    char* lds = smem[wave];
+    float hm[P][9];
+    if (VEC && base + kTile <= B) {
+        dma_slab_issue<kCorner, true>(reinterpret_cast<const char*>(corner + base * 2), lds, lane);
+        dma_slab_issue<kOff, true>(reinterpret_cast<const char*>(offsets + base * 8),
+                                   lds + kCorner, lane);
+        dma_wait_sync();
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int row = j * kWave + lane;
+            float c[2], off[8], tr[12];
+            __builtin_memcpy(c, lds + row * 8, 8);
+            __builtin_memcpy(off, lds + kCorner + row * 32, 32);
+            rect_target_from_offsets(c[0], c[1], w, h, off, tr);
+            tensor_aca_rect_solve(tr, c[0], c[1], w, div, hm[j]);
+        }
+        wave_lds_sync();
+        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), hm, lds, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        if (p < B) {
+            float off[8], tr[12];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
+            const float mx = corner[p * 2], my = corner[p * 2 + 1];
+            rect_target_from_offsets(mx, my, w, h, off, tr);
+            tensor_aca_rect_solve(tr, mx, my, w, div, hm[j]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[p * 9 + k] = hm[j][k];
+        }
+    }
+}
+
+// Backward of the compact form: dL/doffsets (B,4,2) and optionally dL/dcorner (B,2).
+template <bool WANT_CORNER>
+__global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
+    const float* __restrict__ corner, const float* __restrict__ offsets,
+    const float* __restrict__ gH, int64_t B, float w, float h, float* __restrict__ g_off,
+    float* __restrict__ g_corner) {
+    const float div = w / h;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float off[8], tr[12], g[9], gt[12];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        const float mx = corner[p * 2], my = corner[p * 2 + 1];
+        rect_target_from_offsets(mx, my, w, h, off, tr);
+        float gmx, gmy, gsc, gdv;
+        tensor_aca_rect_grad(tr, mx, my, w, div, g, gt, gmx, gmy, gsc, gdv);
+        // tar[0][j] = x_j + off[j].x, tar[1][j] = y_j + off[j].y
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            g_off[p * 8 + 2 * j] = gt[j];
+            g_off[p * 8 + 2 * j + 1] = gt[4 + j];
+        }
+        if constexpr (WANT_CORNER) {
+            g_corner[p * 2] = gmx + (((gt[0] + gt[1]) + gt[2]) + gt[3]);
+            g_corner[p * 2 + 1] = gmy + (((gt[4] + gt[5]) + gt[6]) + gt[7]);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // SoA vector kernel (the reference GPU layout, GPU_Runtime Test.cu:87-95 and
 // :141-149): lane owns V = 16/sizeof(T) consecutive problems and moves each of the
 // 8 + 8 input and 9 output components as one 16-B access (rows are 16-B aligned
@@ -377,6 +461,42 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
     else if (wd) HG_RECT_BWD(false, true);
     else HG_RECT_BWD(false, false);
 #undef HG_RECT_BWD
+    return hg::launch_status();
+}
+
+int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,
+                              float width, float height, void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!corner || !offsets || !H) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    constexpr int P = 2;
+    const int64_t blocks = hg::ceil_div(B, (int64_t)hg::kBlock * P);
+    if (blocks > 0x7fffffffLL) return hg::kErrInvalid;
+    if (hg::aligned16(corner) && hg::aligned16(offsets) && hg::aligned16(H))
+        hg::tensor_aca_offsets_kernel<P, true><<<(unsigned)blocks, hg::kBlock, 0, s>>>(
+            corner, offsets, H, B, width, height);
+    else  // unaligned views: per-lane loads and stores
+        hg::tensor_aca_offsets_kernel<P, false><<<(unsigned)blocks, hg::kBlock, 0, s>>>(
+            corner, offsets, H, B, width, height);
+    return hg::launch_status();
+}
+
+int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets,
+                                       const float* grad_H, int64_t B, float width,
+                                       float height, float* grad_offsets, float* grad_corner,
+                                       void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!corner || !offsets || !grad_H || !grad_offsets) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const unsigned g = hg::generic_grid(B);
+    if (grad_corner)
+        hg::tensor_aca_offsets_backward_kernel<true><<<g, hg::kBlock, 0, s>>>(
+            corner, offsets, grad_H, B, width, height, grad_offsets, grad_corner);
+    else
+        hg::tensor_aca_offsets_backward_kernel<false><<<g, hg::kBlock, 0, s>>>(
+            corner, offsets, grad_H, B, width, height, grad_offsets, nullptr);
     return hg::launch_status();
 }
 

@@ -167,6 +167,26 @@ __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], flo
     }
 }
 
+// Compact deep-homography form: the source is the axis-aligned
+// w x h rectangle at corner (mx, my) -- the shape getInput builds
+// (Modules_Runtime_Test.py:9-16) -- and the network predicts the 4 corner offsets
+// (getTar, .py:19-21).  Builds the (3,4) target tensor exactly as the reference's
+// float ops do: N = M + (w,0), P = M + (0,h), Q = M + (w,h), tar = src + offset.
+__device__ __forceinline__ void rect_target_from_offsets(float mx, float my, float w, float h,
+                                                         const float (&off)[8],
+                                                         float (&tr)[12]) {
+    const float nx = mx + w, py = my + h;
+    tr[0] = mx + off[0];
+    tr[1] = nx + off[2];
+    tr[2] = mx + off[4];
+    tr[3] = nx + off[6];
+    tr[4] = my + off[1];
+    tr[5] = my + off[3];
+    tr[6] = py + off[5];
+    tr[7] = py + off[7];
+    tr[8] = tr[9] = tr[10] = tr[11] = 1.f;
+}
+
 // Reverse-mode derivative of tensor_aca_rect_solve (the gradients ATen autograd
 // gives the reference's composed TensorACA_rect, .py:294-302).
 // In: the forward's inputs and g = dL/dH (3x3).  Out: gt = dL/dtar (3,4), gmx/gmy =

@@ -147,6 +147,46 @@ def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.T
     return g_src, g_tar, g_sd
 
 
+def _check_offsets(corner: torch.Tensor, offsets: torch.Tensor) -> torch.device:
+    dev = _require_device(corner, offsets)
+    if offsets.dtype != torch.float32 or tuple(offsets.shape[1:]) not in ((4, 2), (8,)):
+        raise ValueError(f"offsets must be (B,4,2) or (B,8) float32, got {tuple(offsets.shape)}")
+    if corner.dtype != torch.float32 or tuple(corner.shape) != (offsets.shape[0], 2):
+        raise ValueError(f"corner must be (B,2) float32, got {tuple(corner.shape)}")
+    return dev
+
+
+def tensor_aca_offsets(corner: torch.Tensor, offsets: torch.Tensor, width: float, height: float,
+                       out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Compact TensorACA: source = the width x height rectangle at
+    ``corner`` (B,2), target = source + ``offsets`` (B,4,2) in M,N,P,Q order.  Same bits
+    as building the (B,3,4) tensors and calling tensor_aca_rect(scale=width,
+    div=width/height).  Returns the unnormalised (B,3,3) H."""
+    dev = _check_offsets(corner, offsets)
+    corner, offsets = corner.contiguous(), offsets.contiguous()
+    B = offsets.shape[0]
+    if out is None:
+        out = torch.empty((B, 3, 3), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("hg_tensor_aca_offsets_f32", corner.data_ptr(), offsets.data_ptr(),
+                  out.data_ptr(), B, float(width), float(height), _stream(dev))
+    return out
+
+
+def tensor_aca_offsets_backward(corner, offsets, grad, width: float, height: float,
+                                need_corner: bool = True):
+    dev = _check_offsets(corner, offsets)
+    corner, offsets, grad = corner.contiguous(), offsets.contiguous(), grad.contiguous()
+    B = offsets.shape[0]
+    g_off = torch.empty(offsets.shape, dtype=torch.float32, device=dev)
+    g_cor = torch.empty((B, 2) if need_corner else (0,), dtype=torch.float32, device=dev)
+    with torch.cuda.device(dev):
+        _lib.call("hg_tensor_aca_offsets_backward_f32", corner.data_ptr(), offsets.data_ptr(),
+                  grad.data_ptr(), B, float(width), float(height), g_off.data_ptr(),
+                  g_cor.data_ptr() if need_corner and B else None, _stream(dev))
+    return g_off, g_cor
+
+
 def tensor_aca_rect_autograd(src: torch.Tensor, tar: torch.Tensor, scale: Scalar,
                              div: Scalar) -> torch.Tensor:
     """Differentiable TensorACA (torch.ops.sks_amd.tensor_aca_rect): gradients flow to
@@ -257,6 +297,40 @@ def _register_ops() -> None:
                 g_scale, g_div)
 
     _rect.register_autograd(_backward, setup_context=_setup)
+
+    @torch.library.custom_op(f"{_NS}::tensor_aca_offsets", mutates_args=())
+    def _offs(corner: torch.Tensor, offsets: torch.Tensor, width: float,
+              height: float) -> torch.Tensor:
+        return tensor_aca_offsets(corner, offsets, width, height)
+
+    @_offs.register_fake
+    def _(corner, offsets, width, height):
+        return offsets.new_empty((offsets.shape[0], 3, 3))
+
+    @torch.library.custom_op(f"{_NS}::tensor_aca_offsets_backward", mutates_args=())
+    def _offs_bwd(corner: torch.Tensor, offsets: torch.Tensor, grad: torch.Tensor, width: float,
+                  height: float, need_corner: bool) -> Tuple[torch.Tensor, torch.Tensor]:
+        return tensor_aca_offsets_backward(corner, offsets, grad, width, height, need_corner)
+
+    @_offs_bwd.register_fake
+    def _(corner, offsets, grad, width, height, need_corner):
+        return (offsets.new_empty(offsets.shape),
+                offsets.new_empty((offsets.shape[0], 2) if need_corner else (0,)))
+
+    def _offs_setup(ctx, inputs, output):
+        corner, offsets, width, height = inputs
+        ctx.save_for_backward(corner, offsets)
+        ctx.wh = (width, height)
+
+    def _offs_backward(ctx, grad):
+        corner, offsets = ctx.saved_tensors
+        need_c = ctx.needs_input_grad[0]
+        g_off, g_cor = torch.ops.sks_amd.tensor_aca_offsets_backward(
+            corner, offsets, grad.contiguous(), ctx.wh[0], ctx.wh[1], need_c)
+        return (g_cor if need_c else None,
+                g_off if ctx.needs_input_grad[1] else None, None, None)
+
+    _offs.register_autograd(_offs_backward, setup_context=_offs_setup)
 
 
 _register_ops()

@@ -1,0 +1,81 @@
+"""Compact TensorACA (corner + 4 offsets): forward bit-exact against
+the oracle's TensorACA_rect on the equivalently-built (B,3,4) tensors; backward
+bit-exact against the oracle gradient mapped to offsets; autograd close to float64."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _build_h(corner, offsets, w, h):
+    """(B,3,4) src/tar exactly as getInput/getTar/adjust build them (float32 adds)."""
+    c = corner.astype(np.float32)
+    o = offsets.reshape(-1, 4, 2).astype(np.float32)
+    w, h = np.float32(w), np.float32(h)
+    sx = np.stack([c[:, 0], c[:, 0] + w, c[:, 0], c[:, 0] + w], 1)
+    sy = np.stack([c[:, 1], c[:, 1], c[:, 1] + h, c[:, 1] + h], 1)
+    ones = np.ones_like(sx)
+    src = np.stack([sx, sy, ones], 1)
+    tar = np.stack([sx + o[:, :, 0], sy + o[:, :, 1], ones], 1)
+    return src.astype(np.float32), tar.astype(np.float32)
+
+
+@pytest.mark.parametrize("B", [1, 127, 128, 129, 4096, 100_001])
+@pytest.mark.parametrize("wh", [(128.0, 128.0), (50.0, 40.0)])
+def test_offsets_forward_backward_vs_oracle(orc, oracle, pkg, dev, B, wh):
+    w, h = wh
+    g = torch.Generator(device=dev).manual_seed(B)
+    corner = (torch.rand(B, 2, device=dev, generator=g) * 20 + 10).floor() + 0.25
+    offsets = torch.rand(B, 4, 2, device=dev, generator=g) * 32
+    H = pkg.tensor_aca_offsets(corner, offsets, w, h)
+    src, tar = _build_h(corner.cpu().numpy(), offsets.cpu().numpy(), w, h)
+    div = float(np.float32(w) / np.float32(h))
+    want = oracle.tensor_aca_rect(src, tar, w, div)
+    ok = orc.same_bits(H.cpu().numpy(), want)
+    assert ok.all(), f"{(~ok).sum()} differ"
+    gH = torch.randn(B, 3, 3, device=dev, generator=g)
+    g_off, g_cor = pkg.tensor_aca_offsets_backward(corner, offsets, gH, w, h, True)
+    ws, wt, _ = oracle.tensor_aca_rect_backward(src, tar, gH.cpu().numpy(), w, div)
+    want_off = np.stack([wt[:, 0, :], wt[:, 1, :]], 2)  # (B,4,2)
+    assert orc.same_bits(g_off.cpu().numpy(), want_off).all()
+    want_cx = ws[:, 0, 0] + (((wt[:, 0, 0] + wt[:, 0, 1]) + wt[:, 0, 2]) + wt[:, 0, 3])
+    want_cy = ws[:, 1, 0] + (((wt[:, 1, 0] + wt[:, 1, 1]) + wt[:, 1, 2]) + wt[:, 1, 3])
+    assert orc.same_bits(g_cor.cpu().numpy(), np.stack([want_cx, want_cy], 1)).all()
+
+
+def test_offsets_unaligned_views(orc, oracle, pkg, dev):
+    B = 3001
+    corner = torch.rand(B, 2, device=dev) * 20
+    offsets = torch.rand(B, 4, 2, device=dev) * 32
+    cbig = torch.zeros(B * 2 + 1, device=dev)
+    cbig[1:] = corner.reshape(-1)
+    obig = torch.zeros(B * 8 + 1, device=dev)
+    obig[1:] = offsets.reshape(-1)
+    H = pkg.tensor_aca_offsets(cbig[1:].view(B, 2), obig[1:].view(B, 4, 2), 128.0, 128.0)
+    assert torch.equal(H, pkg.tensor_aca_offsets(corner, offsets, 128.0, 128.0))
+
+
+def test_offsets_autograd_vs_float64(pkg, dev):
+    B = 2048
+    corner = (torch.rand(B, 2, device=dev) * 20 + 10).requires_grad_()
+    offsets = (torch.rand(B, 4, 2, device=dev) * 32).requires_grad_()
+    H = torch.ops.sks_amd.tensor_aca_offsets(corner, offsets, 50.0, 40.0)
+    gH = torch.randn(B, 3, 3, device=dev)
+    H.backward(gH)
+    c64 = corner.detach().double().requires_grad_()
+    o64 = offsets.detach().double().requires_grad_()
+    w, h = 50.0, 40.0
+    sx = torch.stack([c64[:, 0], c64[:, 0] + w, c64[:, 0], c64[:, 0] + w], 1)
+    sy = torch.stack([c64[:, 1], c64[:, 1], c64[:, 1] + h, c64[:, 1] + h], 1)
+    ones = torch.ones_like(sx)
+    src = torch.stack([sx, sy, ones], 1)
+    tar = torch.stack([sx + o64[:, :, 0], sy + o64[:, :, 1], ones], 1)
+    from test_oracle_golden import _functional_rect
+    _functional_rect(src, tar, w, w / h).backward(gH.double())
+
+    def rel(a, b):
+        return ((a.double() - b).abs().max() / b.abs().max()).item()
+
+    assert rel(offsets.grad, o64.grad) < 1e-5
+    assert rel(corner.grad, c64.grad) < 1e-4
