@@ -93,6 +93,22 @@ def timed_region(d: Dist, fn, steps: int):
     return d.max(wall), e0.elapsed_time(e1) / steps
 
 
+def graph_of(d: Dist, fn, calls: int):
+    """HIP graph of `calls` back-to-back invocations (captured on a side stream)."""
+    s = torch.cuda.Stream(d.dev)
+    s.wait_stream(torch.cuda.current_stream(d.dev))
+    with torch.cuda.stream(s):
+        fn()  # warm the allocator on the capture stream
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g, stream=s):
+            for _ in range(calls):
+                fn()
+    torch.cuda.current_stream(d.dev).wait_stream(s)
+    g.replay()
+    torch.cuda.synchronize(d.dev)
+    return g
+
+
 def pmc_traffic(kernel_key: str):
     """Per-launch HBM bytes of `kernel_key` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py), or None."""
@@ -268,6 +284,11 @@ def main():
             f_torch()
         _, ms_o = timed_region(d, f_ours, 1000)
         _, ms_t = timed_region(d, f_torch, 1000)
+        g_ours = graph_of(d, f_ours, 100)
+        g_torch = graph_of(d, f_torch, 100)
+        _, ms_go = timed_region(d, g_ours.replay, 20)
+        _, ms_gt = timed_region(d, g_torch.replay, 20)
+        del g_ours, g_torch
         big = 16 * 1024 * 1024
         torch.manual_seed(0)
         _, _, bs_h, bt_h, bsc, bdv = pkg.adjust(d.dev, big)
@@ -302,6 +323,9 @@ def main():
             "batch": args.rect_batch, "us_per_call": round(ms_o * 1e3, 3),
             "torch_composed_us_per_call": round(ms_t * 1e3, 3),
             "speedup_vs_torch": round(ms_t / ms_o, 2),
+            "graph_us_per_call": round(ms_go * 1e3 / 100, 3),
+            "torch_composed_graph_us_per_call": round(ms_gt * 1e3 / 100, 3),
+            "graph_speedup_vs_torch": round(ms_gt / ms_go, 2),
             "large_batch": big, "large_us_per_call": round(ms_b * 1e3, 2),
             "large_achieved_gbps": round(big * rb / (ms_b * 1e-3) / 1e9, 1),
             "large_frac": round(big * rb / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),

@@ -18,6 +18,7 @@
 #include <cstdint>
 
 #include "hg_aos.hpp"
+#include "hg_soa.hpp"
 #include "hg_solvers.hpp"
 #include "sks_homography.h"
 
@@ -229,47 +230,6 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// SoA vector kernel (the reference GPU layout, GPU_Runtime Test.cu:87-95 and
-// :141-149): lane owns V = 16/sizeof(T) consecutive problems and moves each of the
-// 8 + 8 input and 9 output components as one 16-B access (rows are 16-B aligned
-// when n % V == 0 and the bases are 16-B aligned).  Grid-stride.
-template <int ALGO, bool NORM, typename T>
-__global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ src,
-                                                        const T* __restrict__ tar,
-                                                        T* __restrict__ H, int64_t n) {
-    constexpr int V = 16 / sizeof(T);
-    const int64_t groups = n / V;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x; q < groups; q += stride) {
-        T s[8][V], t[8][V];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-            u32x4 a = ld16<true>(src + (int64_t)k * n + q * V);
-            u32x4 b = ld16<true>(tar + (int64_t)k * n + q * V);
-            __builtin_memcpy(s[k], &a, 16);
-            __builtin_memcpy(t[k], &b, 16);
-        }
-        T h[V][9];
-#pragma unroll
-        for (int v = 0; v < V; ++v) {
-            T sv[8], tv[8];
-#pragma unroll
-            for (int k = 0; k < 8; ++k) { sv[k] = s[k][v]; tv[k] = t[k][v]; }
-            solve<ALGO, NORM>(sv, tv, h[v]);
-        }
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            T o[V];
-#pragma unroll
-            for (int v = 0; v < V; ++v) o[v] = h[v][k];
-            u32x4 w;
-            __builtin_memcpy(&w, o, 16);
-            st16<true>(H + (int64_t)k * n + q * V, w);
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Fused sampler + solver: gather 4 correspondences by index from a pool (the
 // reference's get_rand_list, GPU_Runtime Test.cu:52-78) and solve in registers,
 // so each problem reads 16 B of indices instead of 64 B of coordinates.
@@ -343,6 +303,7 @@ template <typename T>
 constexpr int kAosP = sizeof(T) == 4 ? 2 : 1;
 constexpr int kAosFlags = kNtLoad | kNtStore | kLdsLoad | kLdsDma;
 constexpr int kRectP = 2;
+constexpr int kSoaG = 1;  // 16-B groups per lane (SoA path)
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -361,7 +322,8 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
     if (layout == HG_LAYOUT_SOA) {
         constexpr int V = 16 / sizeof(T);
         if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H))
-            solve_soa_vec<ALGO, NORM, T><<<generic_grid(n / V), kBlock, 0, s>>>(src, tar, H, n);
+            solve_soa_vec<ALGO, NORM, T, kSoaG, false>
+                <<<(unsigned)soa_grid<kSoaG, false>(n / V), kBlock, 0, s>>>(src, tar, H, n);
         else
             solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {

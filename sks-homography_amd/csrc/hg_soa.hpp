@@ -1,0 +1,69 @@
+// hg_soa.hpp -- SoA streaming solver (the reference GPU layout,
+// GPU_Runtime Test.cu:87-95 / :141-149: src/tar (8,n), H (9,n)).
+//
+// A lane owns G groups of V = 16/sizeof(T) consecutive problems and moves each of a
+// group's 8 + 8 input and 9 output components as ONE 16-B access, so every
+// wave-instruction touches 1 KiB contiguous of one component row.  Needs n % V == 0
+// and 16-B aligned bases (else solve_generic runs).  Block b covers groups
+// [b*256*G, (b+1)*256*G); PERSIST loops blocks over that range grid-stride.
+#pragma once
+#include "hg_aos.hpp"
+
+namespace hg {
+
+template <int ALGO, bool NORM, typename T, int G, bool PERSIST>
+__global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ src,
+                                                        const T* __restrict__ tar,
+                                                        T* __restrict__ H, int64_t n) {
+    constexpr int V = 16 / sizeof(T);
+    const int64_t groups = n / V;
+    const int64_t chunks = (groups + (int64_t)kBlock * G - 1) / ((int64_t)kBlock * G);
+    for (int64_t c = blockIdx.x; c < chunks; c += PERSIST ? gridDim.x : chunks) {
+        const int64_t q0 = c * kBlock * G + threadIdx.x;
+        T s[G][8][V], t[G][8][V];
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int64_t q = q0 + (int64_t)g * kBlock;
+            if (q < groups) {
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    u32x4 a = ld16<true>(src + (int64_t)k * n + q * V);
+                    u32x4 b = ld16<true>(tar + (int64_t)k * n + q * V);
+                    __builtin_memcpy(s[g][k], &a, 16);
+                    __builtin_memcpy(t[g][k], &b, 16);
+                }
+            }
+        }
+#pragma unroll
+        for (int g = 0; g < G; ++g) {
+            const int64_t q = q0 + (int64_t)g * kBlock;
+            if (q >= groups) continue;
+            T h[V][9];
+#pragma unroll
+            for (int v = 0; v < V; ++v) {
+                T sv[8], tv[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) { sv[k] = s[g][k][v]; tv[k] = t[g][k][v]; }
+                solve<ALGO, NORM>(sv, tv, h[v]);
+            }
+#pragma unroll
+            for (int k = 0; k < 9; ++k) {
+                T o[V];
+#pragma unroll
+                for (int v = 0; v < V; ++v) o[v] = h[v][k];
+                u32x4 w;
+                __builtin_memcpy(&w, o, 16);
+                st16<true>(H + (int64_t)k * n + q * V, w);
+            }
+        }
+    }
+}
+
+template <int G, bool PERSIST>
+inline int64_t soa_grid(int64_t groups, int per_cu = 8) {
+    const int64_t chunks = (groups + (int64_t)kBlock * G - 1) / ((int64_t)kBlock * G);
+    if (PERSIST) return chunks < 256LL * per_cu ? chunks : 256LL * per_cu;
+    return chunks > 0 ? chunks : 1;
+}
+
+}  // namespace hg

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hg_aos.hpp"
+#include "hg_soa.hpp"
 #include "sks_homography.h"
 
 namespace {
@@ -87,9 +88,52 @@ __global__ __launch_bounds__(kBlock) void copy_dma(const char* __restrict__ src,
                    *reinterpret_cast<const u32x4*>(smem[wave] + 16 * (c * 64 + lane)));
 }
 
+template <typename T, int G, bool PERSIST>
+int launch_soa(int algo, const void* s, const void* t, void* H, int64_t n, int per_cu,
+               hipStream_t st) {
+    constexpr int V = 16 / sizeof(T);
+    if (n % V) return (int)hipErrorInvalidValue;
+    const unsigned g = (unsigned)soa_grid<G, PERSIST>(n / V, per_cu);
+    const T* a = (const T*)s;
+    const T* b = (const T*)t;
+    T* h = (T*)H;
+    if (algo == 0) solve_soa_vec<kACA, false, T, G, PERSIST><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else solve_soa_vec<kSKS, false, T, G, PERSIST><<<g, kBlock, 0, st>>>(a, b, h, n);
+    return (int)hipGetLastError();
+}
+
+struct SoaVariant {
+    const char* name;
+    int (*launch)(int, const void*, const void*, void*, int64_t, int, hipStream_t);
+};
+
+const SoaVariant kSoaVariants[] = {
+    {"f64 G1 one-shot (shipped)", launch_soa<double, 1, false>},
+    {"f64 G2 one-shot", launch_soa<double, 2, false>},
+    {"f64 G1 persist", launch_soa<double, 1, true>},
+    {"f64 G2 persist", launch_soa<double, 2, true>},
+    {"f32 G1 one-shot (shipped)", launch_soa<float, 1, false>},
+    {"f32 G2 one-shot", launch_soa<float, 2, false>},
+    {"f32 G1 persist", launch_soa<float, 1, true>},
+};
+
 }  // namespace
 
 extern "C" {
+
+int hg_tune_num_soa_variants(void) { return (int)(sizeof(kSoaVariants) / sizeof(kSoaVariants[0])); }
+
+const char* hg_tune_soa_variant_name(int v) {
+    return (v >= 0 && v < hg_tune_num_soa_variants()) ? kSoaVariants[v].name : nullptr;
+}
+
+/* SoA unnormalised (the reference GPU semantics); dtype follows the variant. */
+int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H, int64_t n,
+                int per_cu, void* stream) {
+    if (variant < 0 || variant >= hg_tune_num_soa_variants() || n <= 0) return (int)hipErrorInvalidValue;
+    return kSoaVariants[variant].launch(algo, src, tar, H, n, per_cu > 0 ? per_cu : 8,
+                                        reinterpret_cast<hipStream_t>(stream));
+}
 
 // variant 0: U=4 nt, 1: U=8 nt, 2: U=4 plain, 3: LDS-DMA (bytes % 32 KiB == 0)
 int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* stream) {

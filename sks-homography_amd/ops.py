@@ -31,7 +31,38 @@ def _require_device(*tensors: torch.Tensor) -> torch.device:
 
 
 def _stream(dev: torch.device) -> int:
-    return torch.cuda.current_stream(dev).cuda_stream
+    """Raw hipStream_t of torch's current stream on `dev` (0 = the default stream)."""
+    return torch._C._cuda_getCurrentRawStream(dev.index if dev.index is not None
+                                              else torch.cuda.current_device())
+
+
+class _NoGuard:
+    def __enter__(self):
+        return None
+
+    def __exit__(self, *exc):
+        return False
+
+
+_NO_GUARD = _NoGuard()
+
+
+def _guard(dev: torch.device):
+    """Device guard only when `dev` is not already current: a launch on the default
+    stream goes to the current device, and the guard costs microseconds per call."""
+    if dev.index is None or dev.index == torch.cuda.current_device():
+        return _NO_GUARD
+    return torch.cuda.device(dev)
+
+
+def _scalar_ptr(x, dev: torch.device):
+    """Device pointer of a batch-uniform scalar kept on the device (no copy when it
+    already is a float32 CUDA tensor there), plus the tensor that owns it."""
+    if (isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.device == dev
+            and x.numel() >= 1):
+        return x.data_ptr(), x
+    t = torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+    return t.data_ptr(), t
 
 
 def _as_problems(x: torch.Tensor, layout: str) -> torch.Tensor:
@@ -73,7 +104,7 @@ def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = Tru
     elif out.shape != shape or out.dtype != src.dtype or not out.is_contiguous() or out.device != dev:
         raise ValueError(f"out must be a contiguous {shape} {src.dtype} tensor on {dev}")
     fn = f"hg_{algo}_{_DTYPES[src.dtype]}"
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call(fn, src.data_ptr(), tar.data_ptr(), out.data_ptr(), n,
                   HG_LAYOUT_AOS if layout == "aos" else HG_LAYOUT_SOA,
                   HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
@@ -112,12 +143,12 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     if out is None:
         out = torch.empty((B, 3, 3), dtype=torch.float32, device=dev)
     stream = _stream(dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         if isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):
-            sc = torch.as_tensor(scale, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
-            dv = torch.as_tensor(div, dtype=torch.float32, device=dev).reshape(-1)[:1].contiguous()
+            sp, _sc = _scalar_ptr(scale, dev)
+            dp, _dv = _scalar_ptr(div, dev)
             _lib.call("hg_tensor_aca_rect_f32", src.data_ptr(), tar.data_ptr(), out.data_ptr(),
-                      B, sc.data_ptr(), dv.data_ptr(), stream)
+                      B, sp, dp, stream)
         else:
             _lib.call("hg_tensor_aca_rect_f32_hostscalar", src.data_ptr(), tar.data_ptr(),
                       out.data_ptr(), B, float(scale), float(div), stream)
@@ -138,7 +169,7 @@ def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.T
     g_tar = torch.empty((B, 3, 4), dtype=torch.float32, device=dev)
     g_src = torch.empty((B, 3, 4) if need_src else (0,), dtype=torch.float32, device=dev)
     part = torch.empty((B, 2) if need_scale_div else (0,), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_tensor_aca_rect_backward_f32", src.data_ptr(), tar.data_ptr(),
                   grad.data_ptr(), B, sc.data_ptr(), dv.data_ptr(),
                   g_src.data_ptr() if need_src and B else None, g_tar.data_ptr(),
@@ -167,7 +198,7 @@ def tensor_aca_offsets(corner: torch.Tensor, offsets: torch.Tensor, width: float
     B = offsets.shape[0]
     if out is None:
         out = torch.empty((B, 3, 3), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_tensor_aca_offsets_f32", corner.data_ptr(), offsets.data_ptr(),
                   out.data_ptr(), B, float(width), float(height), _stream(dev))
     return out
@@ -180,7 +211,7 @@ def tensor_aca_offsets_backward(corner, offsets, grad, width: float, height: flo
     B = offsets.shape[0]
     g_off = torch.empty(offsets.shape, dtype=torch.float32, device=dev)
     g_cor = torch.empty((B, 2) if need_corner else (0,), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_tensor_aca_offsets_backward_f32", corner.data_ptr(), offsets.data_ptr(),
                   grad.data_ptr(), B, float(width), float(height), g_off.data_ptr(),
                   g_cor.data_ptr() if need_corner and B else None, _stream(dev))
@@ -204,7 +235,7 @@ def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: fl
     dev = torch.device(device)
     if out is None:
         out = torch.empty(count, dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_fill_uniform_f32", out.data_ptr(), count, seed, offset, lo, hi, _stream(dev))
     return out
 
@@ -222,7 +253,7 @@ def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tens
     idx = idx.contiguous()
     n = idx.shape[0]
     out = torch.empty((n, 9), dtype=torch.float32, device=dev)
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_sample_solve_f32", pool_src.data_ptr(), pool_tar.data_ptr(),
                   pool_src.shape[0], idx.data_ptr(), out.data_ptr(), n,
                   0 if algo == "aca" else 1, HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
@@ -232,7 +263,7 @@ def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tens
 def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
     dev = _require_device(src, dst)
     nbytes = src.numel() * src.element_size()
-    with torch.cuda.device(dev):
+    with _guard(dev):
         _lib.call("hg_stream_copy", src.data_ptr(), dst.data_ptr(), nbytes, _stream(dev))
 
 

@@ -43,6 +43,7 @@ for step in $STEPS; do
             run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv \
                 -d "$OUT/pmc_write_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
+        kbench_soa) run kbench_soa 600 python tools/kbench_soa.py ;;
         *) echo "unknown step $step" ;;
     esac
 done
