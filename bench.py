@@ -42,30 +42,47 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-extras", action="store_true", help="ACA headline only")
     ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of H")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
 
 
 class Dist:
-    def __init__(self):
+    """One process per GPU (torch.distributed.run sets RANK/LOCAL_RANK/WORLD_SIZE).
+    Backend "nccl" (= RCCL over xGMI) by default.  --dist-backend gloo exists only to
+    rehearse the N > 1 control path on a one-GPU box (RCCL refuses two ranks on one
+    device): ranks then share cuda:(LOCAL_RANK % device_count) and reduce on the host."""
+
+    def __init__(self, backend: str = "nccl"):
         self.world = int(os.environ.get("WORLD_SIZE", "1"))
         self.rank = int(os.environ.get("RANK", "0"))
         self.local = int(os.environ.get("LOCAL_RANK", "0"))
-        self.dev = torch.device("cuda", self.local)
+        self.backend = backend
+        ndev = torch.cuda.device_count()
+        idx = self.local if backend == "nccl" else self.local % max(ndev, 1)
+        self.dev = torch.device("cuda", idx)
         torch.cuda.set_device(self.dev)
         self.pg = None
         if self.world > 1:
             import torch.distributed as dist
-            dist.init_process_group("nccl", device_id=self.dev)
+            if backend == "nccl":
+                dist.init_process_group("nccl", device_id=self.dev)
+            else:
+                dist.init_process_group(backend)
             self.pg = dist
 
     def barrier(self):
         if self.pg:
-            self.pg.barrier(device_ids=[self.local])
+            if self.backend == "nccl":
+                self.pg.barrier(device_ids=[self.dev.index])
+            else:
+                self.pg.barrier()
 
     def max(self, x: float) -> float:
         if not self.pg:
             return x
-        t = torch.tensor([x], dtype=torch.float64, device=self.dev)
+        dev = self.dev if self.backend == "nccl" else "cpu"
+        t = torch.tensor([x], dtype=torch.float64, device=dev)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
 
@@ -200,9 +217,39 @@ def reference_layout(d: Dist, pkg):
     return out
 
 
+def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
+    """1M random 4-point hypotheses over the reference's own
+    correspondence file (orig_pts_wall.txt, 2540 pairs, committed in tests/golden):
+    draw + fused gather/solve (HBM-bound: 16 B idx + 36 B H per hypothesis) and the
+    inlier scorer (VALU-bound: every hypothesis x every pair)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"]).to(d.dev)
+    pt = torch.from_numpy(g["pool_tar"]).to(d.dev)
+    idx = pkg.fill_bits(hyps * 4, SEED, 0, d.dev).view(hyps, 4)
+    H = pkg.sample_solve(ps, pt, idx)
+    f_solve = lambda: pkg.sample_solve(ps, pt, idx)  # noqa: E731
+    f_score = lambda: pkg.ransac_score(H, ps, pt, thresh)  # noqa: E731
+    for _ in range(3):
+        f_solve()
+        f_score()
+    _, ms_solve = timed_region(d, f_solve, 20)
+    _, ms_score = timed_region(d, f_score, 5)
+    counts = pkg.ransac_score(H, ps, pt, thresh)
+    pairs = hyps * ps.shape[0]
+    return {
+        "hypotheses": hyps, "pool": int(ps.shape[0]), "thresh_px": thresh,
+        "sample_solve_us": round(ms_solve * 1e3, 2),
+        "sample_solve_G_hyp_per_s": round(hyps / (ms_solve * 1e-3) / 1e9, 2),
+        "sample_solve_gbps": round(hyps * 52 / (ms_solve * 1e-3) / 1e9, 1),
+        "score_ms": round(ms_score, 3),
+        "score_G_pairs_per_s": round(pairs / (ms_score * 1e-3) / 1e9, 1),
+        "best_inliers": int(counts.max().item()),
+    }
+
+
 def main():
     args = parse()
-    d = Dist()
+    d = Dist(args.dist_backend)
     pkg = ge.load_package()
     n = args.n
     n_total = n * d.world
@@ -332,6 +379,7 @@ def main():
         }
         del bs_h, bt_h, Hb
         line["reference_layout"] = reference_layout(d, pkg)
+        line["ransac"] = ransac_section(d, pkg)
 
     if args.gather and d.world > 1:
         d.barrier()

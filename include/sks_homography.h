@@ -107,13 +107,27 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
 int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
                         float hi, void* stream);
 
+/* Counter-based 32-bit draws: out[i] = high 32 bits of
+ * splitmix64(seed * 0xA0761D6478BD642F + offset + i).  The RANSAC sampler's index
+ * source (the reference draws with cuRAND MRG32K3A, GPU_Runtime Test.cu:1443-1446). */
+int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset,
+                     void* stream);
+
 /* Fused RANSAC-style hypothesis generator + solver (GPU_Runtime Test.cu:52-78 fused
- * with :81-151).  pool_src/pool_tar: (npool,2) correspondences; idx: (n,4) uint32
- * indices, each reduced modulo npool like get_rand_list (.cu:56-59).  Writes the
- * gathered problem's H (AoS, (n,9)); algo 0 = ACA, 1 = SKS. */
+ * with :81-151).  pool_src/pool_tar: (npool,2) correspondences (8-B aligned); idx:
+ * (n,4) uint32 indices (16-B aligned), each reduced modulo npool like get_rand_list
+ * (.cu:56-59).  Writes the gathered problem's H (AoS, (n,9), 16-B aligned); algo 0 =
+ * ACA, 1 = SKS. */
 int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
                         const uint32_t* idx, float* H, int64_t n, int algo, int flags,
                         void* stream);
+
+/* Inlier count per hypothesis: counts[h] = #{i : w' != 0 and
+ * (x' - u w')^2 + (y' - v w')^2 <= thresh^2 w'^2}, (x',y',w') = H_h (x_i, y_i, 1),
+ * (u_i, v_i) = pool_tar[i] -- the squared reprojection error against thresh, without
+ * the division (exact FMA placement documented in csrc/hg_ransac.hip).  H: (n,9). */
+int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,
+                        uint32_t npool, float thresh, uint32_t* counts, void* stream);
 
 /* Device-to-device streaming copy (float4) used by bench.py as the measured
  * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */

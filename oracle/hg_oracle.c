@@ -357,3 +357,35 @@ int oracle_tensor_aca_rect_backward_f32(const float* src, const float* tar, cons
     }
     return 0;
 }
+
+/* ------------------------------------------------------ RANSAC helpers ----- */
+/* Restates hg_fill_bits_u32 and hg_ransac_score_f32 (csrc/hg_ransac.hip), the
+ * SURVEY 8(f).2 extension; the reference has no scorer, so these pin our own
+ * definition (the division-free squared reprojection test, fixed FMA placement). */
+int oracle_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset) {
+    const uint64_t base = seed * 0xA0761D6478BD642Full + offset;
+    for (int64_t i = 0; i < count; ++i) out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
+    return 0;
+}
+
+int oracle_ransac_score_f32(const float* H, int64_t n, const float* ps, const float* pt,
+                            uint32_t npool, float thresh, uint32_t* counts) {
+    const float t2 = thresh * thresh;
+    for (int64_t p = 0; p < n; ++p) {
+        const float* h = H + p * 9;
+        uint32_t c = 0;
+        for (uint32_t i = 0; i < npool; ++i) {
+            const float x = ps[2 * i], y = ps[2 * i + 1], u = pt[2 * i], v = pt[2 * i + 1];
+            const float xs = fmaf(h[0], x, fmaf(h[1], y, h[2]));
+            const float ys = fmaf(h[3], x, fmaf(h[4], y, h[5]));
+            const float ws = fmaf(h[6], x, fmaf(h[7], y, h[8]));
+            const float ex = fmaf(-u, ws, xs);
+            const float ey = fmaf(-v, ws, ys);
+            const float e2 = fmaf(ex, ex, ey * ey);
+            const float lim = t2 * (ws * ws);
+            c += (e2 <= lim) && (ws != 0.f);
+        }
+        counts[p] = c;
+    }
+    return 0;
+}

@@ -53,6 +53,9 @@ class Oracle:
                                                             ctypes.c_float, ctypes.c_float,
                                                             _f32p, _f32p, _f32p]
         lib.oracle_tensor_aca_rect_backward_f32.restype = ctypes.c_int
+        lib.oracle_fill_bits_u32.argtypes = [ctypes.c_void_p, _i64, ctypes.c_uint64, ctypes.c_uint64]
+        lib.oracle_ransac_score_f32.argtypes = [_f32p, _i64, _f32p, _f32p, ctypes.c_uint32,
+                                                ctypes.c_float, ctypes.c_void_p]
         lib.oracle_time_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64,
                                         ctypes.c_int, ctypes.c_int]
         lib.oracle_time_f32.restype = ctypes.c_double
@@ -97,6 +100,28 @@ class Oracle:
             _ptr(src, _f32p), _ptr(tar, _f32p), _ptr(gH, _f32p), B, float(np.float32(scale)),
             float(np.float32(div)), _ptr(gs, _f32p), _ptr(gt, _f32p), _ptr(gsd, _f32p))
         return gs, gt, gsd
+
+    def fill_bits(self, count: int, seed: int, offset: int = 0) -> np.ndarray:
+        out = np.empty(count, dtype=np.uint32)
+        self.lib.oracle_fill_bits_u32(out.ctypes.data, count, seed, offset)
+        return out
+
+    def ransac_score(self, H, pool_src, pool_tar, thresh: float) -> np.ndarray:
+        H = np.ascontiguousarray(H, dtype=np.float32).reshape(-1, 9)
+        ps = np.ascontiguousarray(pool_src, dtype=np.float32)
+        pt = np.ascontiguousarray(pool_tar, dtype=np.float32)
+        counts = np.empty(H.shape[0], dtype=np.uint32)
+        self.lib.oracle_ransac_score_f32(_ptr(H, _f32p), H.shape[0], _ptr(ps, _f32p),
+                                         _ptr(pt, _f32p), ps.shape[0], float(np.float32(thresh)),
+                                         counts.ctypes.data)
+        return counts
+
+    def sample_problems(self, pool_src, pool_tar, idx):
+        """Gather like get_rand_list (GPU_Runtime Test.cu:52-78): rows of 4 indices,
+        each reduced modulo the pool size -> (n,8) src, (n,8) tar."""
+        idx = np.asarray(idx).astype(np.uint32) % np.uint32(pool_src.shape[0])
+        return (pool_src[idx].reshape(-1, 8).astype(np.float32),
+                pool_tar[idx].reshape(-1, 8).astype(np.float32))
 
     def fill_uniform(self, count: int, seed: int, offset: int = 0, lo: float = 0.0,
                      hi: float = 1024.0) -> np.ndarray:

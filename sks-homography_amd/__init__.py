@@ -10,14 +10,17 @@ Layers:
   ops.py                     torch-facing wrappers, torch.ops.sks_amd.*
   reference_api.py           TensorACA_rect / ACA_vanilla / getInput / adjust mirrors
   shard.py                   per-GPU block sharding, optional RCCL gather
+  ransac.py                  fused hypothesis sampling + solve + inlier scoring
 """
 from __future__ import annotations
 
 from . import _lib
 from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib, version
-from .ops import (aca, fill_uniform, sample_solve, sks, solve, stream_copy, tensor_aca_rect,
+from .ops import (aca, fill_uniform, sks, solve, stream_copy, tensor_aca_rect,
                   tensor_aca_rect_autograd, tensor_aca_rect_backward,
                   tensor_aca_offsets, tensor_aca_offsets_backward)
+from .ransac import RansacResult, fill_bits, ransac, sample_solve
+from .ransac import score as ransac_score
 from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
 from .shard import gather_blocks, shard_range
 
@@ -27,7 +30,7 @@ RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H (SURV
 __all__ = [
     "aca", "sks", "solve", "tensor_aca_rect", "tensor_aca_rect_autograd",
     "tensor_aca_rect_backward", "tensor_aca_offsets", "tensor_aca_offsets_backward",
-    "fill_uniform", "sample_solve", "stream_copy",
+    "fill_uniform", "sample_solve", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
     "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
     "gather_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
     "HG_FLAG_NORMALIZE", "BYTES_PER_PROBLEM", "RECT_BYTES_PER_PROBLEM",

@@ -36,7 +36,10 @@ SIGNATURES = {
                                            _vp, _vp, _vp], _int),
     "hg_fill_uniform_f32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
                              ctypes.c_float, _vp], _int),
+    "hg_fill_bits_u32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _int),
     "hg_sample_solve_f32": ([_vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_ransac_score_f32": ([_vp, _i64, _vp, _vp, ctypes.c_uint32, ctypes.c_float, _vp, _vp],
+                            _int),
     "hg_stream_copy": ([_vp, _vp, _i64, _vp], _int),
     "hg_version": ([], ctypes.c_char_p),
 }

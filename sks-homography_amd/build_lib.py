@@ -21,7 +21,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsks_homography_amd.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
-SOURCES = ["hg_kernels.hip", "hg_tune.hip", "hg_sks_api.cpp"]
+SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_tune.hip", "hg_sks_api.cpp"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 

@@ -52,6 +52,15 @@ __device__ __forceinline__ void load_row8(const T* p, T (&v)[8]) {
     }
 }
 
+// splitmix64 finaliser: the counter-based generator shared (bit for bit) with the
+// host-side regeneration in oracle/hg_oracle.c.
+__device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z += 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
 __device__ __forceinline__ void wave_lds_sync() {
     __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
     __builtin_amdgcn_wave_barrier();

@@ -230,38 +230,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
 }
 
 // ---------------------------------------------------------------------------
-// Fused sampler + solver: gather 4 correspondences by index from a pool (the
-// reference's get_rand_list, GPU_Runtime Test.cu:52-78) and solve in registers,
-// so each problem reads 16 B of indices instead of 64 B of coordinates.
-template <int ALGO, bool NORM>
-__global__ __launch_bounds__(kBlock) void sample_solve_kernel(
-    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < n; p += stride) {
-        const uint4 r = idx[p];
-        const uint32_t id[4] = {r.x % npool, r.y % npool, r.z % npool, r.w % npool};
-        float s[8], t[8], h[9];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
-            s[2 * k] = a.x; s[2 * k + 1] = a.y;
-            t[2 * k] = b.x; t[2 * k + 1] = b.y;
-        }
-        solve<ALGO, NORM>(s, t, h);
-#pragma unroll
-        for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[k];
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Counter-based uniform generator (bit-identical to oracle_fill_uniform_f32).
-__device__ __forceinline__ uint64_t mix64(uint64_t z) {
-    z += 0x9E3779B97F4A7C15ull;
-    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
-    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
-    return z ^ (z >> 31);
-}
 
 __global__ __launch_bounds__(kBlock) void fill_uniform_kernel(float* __restrict__ out,
                                                               int64_t count, uint64_t seed,
@@ -470,32 +439,6 @@ int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offse
     hg::fill_uniform_kernel<<<hg::generic_grid(count), hg::kBlock, 0,
                               reinterpret_cast<hipStream_t>(stream)>>>(out, count, seed, offset,
                                                                        lo, hi);
-    return hg::launch_status();
-}
-
-int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
-                        const uint32_t* idx, float* H, int64_t n, int algo, int flags,
-                        void* stream) {
-    if (n < 0 || npool == 0 || (algo != 0 && algo != 1) || (flags & ~HG_FLAG_NORMALIZE))
-        return hg::kErrInvalid;
-    if (n == 0) return 0;
-    if (!pool_src || !pool_tar || !idx || !H) return hg::kErrInvalid;
-    if (!hg::aligned16(idx) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
-        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
-        return hg::kErrInvalid;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const auto* ps = reinterpret_cast<const float2*>(pool_src);
-    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
-    const auto* ix = reinterpret_cast<const uint4*>(idx);
-    const unsigned g = hg::generic_grid(n);
-    const bool norm = flags & HG_FLAG_NORMALIZE;
-    if (algo == 0) {
-        if (norm) hg::sample_solve_kernel<hg::kACA, true><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
-        else hg::sample_solve_kernel<hg::kACA, false><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
-    } else {
-        if (norm) hg::sample_solve_kernel<hg::kSKS, true><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
-        else hg::sample_solve_kernel<hg::kSKS, false><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n);
-    }
     return hg::launch_status();
 }
 

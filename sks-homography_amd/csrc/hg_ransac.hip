@@ -1,0 +1,198 @@
+// hg_ransac.hip -- RANSAC-style hypothesis generation and scoring on the solver
+// (the reference's cuRAND + get_rand_list gather, GPU_Runtime
+// Test.cu:52-78 / :1443-1451, fused with the closed-form solve, then inlier scoring).
+//
+//   hg_fill_bits_u32      counter-based 32-bit draws (4 per hypothesis)
+//   hg_sample_solve_f32   idx (n,4) -> gather 4 correspondences from the pool -> H (n,9)
+//   hg_ransac_score_f32   H (n,9) x pool (npool) -> inlier count per hypothesis
+//
+// The scorer is the one compute-bound kernel here: every (hypothesis, point) pair
+// costs ~13 VALU ops and no HBM traffic (the pool sits in LDS, H in VGPRs), so its
+// roofline is the FP32 VALU rate, not HBM.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hg_aos.hpp"
+#include "hg_solvers.hpp"
+#include "sks_homography.h"
+
+#pragma clang fp contract(off)
+
+namespace hg {
+
+constexpr uint64_t kBitsMul = 0xA0761D6478BD642Full;
+
+__global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __restrict__ out,
+                                                           int64_t count, uint64_t seed,
+                                                           uint64_t offset) {
+    const uint64_t base = seed * kBitsMul + offset;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride)
+        out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
+}
+
+// Fused sampler + solver.  A wave owns 64*P hypotheses: its 16-B index rows arrive by
+// LDS-DMA (P = 2: 2 KiB), each lane gathers its 4 correspondences from the pool
+// (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
+// LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
+// does (.cu:56-59, modulo bias and duplicates included).
+template <int ALGO, bool NORM, int P>
+__global__ __launch_bounds__(kBlock) void sample_solve_kernel(
+    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
+    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
+    constexpr int kTile = kWave * P;
+    constexpr int kIdx = kTile * 16;
+    constexpr int kLds = kIdx > kTile * 36 ? kIdx : kTile * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kLds];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= n) return;
+    char* lds = smem[wave];
+    const bool full = base + kTile <= n;
+    uint4 r[P];
+    if (full) {
+        dma_slab_issue<kIdx, true>(reinterpret_cast<const char*>(idx + base), lds, lane);
+        dma_wait_sync();
+#pragma unroll
+        for (int j = 0; j < P; ++j) r[j] = *reinterpret_cast<const uint4*>(lds + (j * kWave + lane) * 16);
+        wave_lds_sync();
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            r[j] = p < n ? idx[p] : make_uint4(0, 0, 0, 0);
+        }
+    }
+    float h[P][9];
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const uint32_t id[4] = {r[j].x % npool, r[j].y % npool, r[j].z % npool, r[j].w % npool};
+        float s[8], t[8];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
+            s[2 * k] = a.x; s[2 * k + 1] = a.y;
+            t[2 * k] = b.x; t[2 * k + 1] = b.y;
+        }
+        solve<ALGO, NORM>(s, t, h[j]);
+    }
+    if (full) {
+        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        if (p < n) {
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+        }
+    }
+}
+
+// Inlier test of one (hypothesis, correspondence) pair, division-free:
+//   (x', y', w') = H (x, y, 1),  inlier <=> w' != 0 and
+//   (x' - u w')^2 + (y' - v w')^2 <= t^2 w'^2        [== |(x'/w', y'/w') - (u, v)|^2 <= t^2]
+// with this exact FMA placement (restated in oracle/hg_oracle.c).
+__device__ __forceinline__ bool is_inlier(const float (&h)[9], float4 q, float t2) {
+    const float xs = __builtin_fmaf(h[0], q.x, __builtin_fmaf(h[1], q.y, h[2]));
+    const float ys = __builtin_fmaf(h[3], q.x, __builtin_fmaf(h[4], q.y, h[5]));
+    const float ws = __builtin_fmaf(h[6], q.x, __builtin_fmaf(h[7], q.y, h[8]));
+    const float ex = __builtin_fmaf(-q.z, ws, xs);
+    const float ey = __builtin_fmaf(-q.w, ws, ys);
+    const float e2 = __builtin_fmaf(ex, ex, ey * ey);
+    const float lim = t2 * (ws * ws);
+    return (e2 <= lim) & (ws != 0.f);
+}
+
+// One lane per hypothesis; the block streams the pool through LDS in chunks of
+// kChunk points {x, y, u, v} (every lane reads the same point: an LDS broadcast).
+constexpr int kScoreChunk = 2048;  // 32 KiB of LDS per block
+
+__global__ __launch_bounds__(kBlock) void ransac_score_kernel(
+    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
+    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
+    __shared__ __attribute__((aligned(16))) float4 pts[kScoreChunk];
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    float h[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) h[k] = p < n ? H[p * 9 + k] : 0.f;
+    uint32_t cnt = 0;
+    for (uint32_t c0 = 0; c0 < npool; c0 += kScoreChunk) {
+        const uint32_t m = npool - c0 < (uint32_t)kScoreChunk ? npool - c0 : kScoreChunk;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += kBlock) {
+            const float2 a = pool_src[c0 + i], b = pool_tar[c0 + i];
+            pts[i] = make_float4(a.x, a.y, b.x, b.y);
+        }
+        __syncthreads();
+        uint32_t i = 0;
+        for (; i + 4 <= m; i += 4) {
+#pragma unroll
+            for (int u = 0; u < 4; ++u) cnt += is_inlier(h, pts[i + u], t2) ? 1u : 0u;
+        }
+        for (; i < m; ++i) cnt += is_inlier(h, pts[i], t2) ? 1u : 0u;
+    }
+    if (p < n) counts[p] = cnt;
+}
+
+}  // namespace hg
+
+extern "C" {
+
+int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset, void* stream) {
+    if (count < 0) return (int)hipErrorInvalidValue;
+    if (count == 0) return 0;
+    if (!out) return (int)hipErrorInvalidValue;
+    const int64_t want = (count + hg::kBlock - 1) / hg::kBlock;
+    const unsigned g = (unsigned)(want < 8192 ? want : 8192);
+    hg::fill_bits_kernel<<<g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        out, count, seed, offset);
+    return (int)hipGetLastError();
+}
+
+int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
+                        const uint32_t* idx, float* H, int64_t n, int algo, int flags,
+                        void* stream) {
+    if (n < 0 || npool == 0 || (algo != 0 && algo != 1) || (flags & ~HG_FLAG_NORMALIZE))
+        return (int)hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!pool_src || !pool_tar || !idx || !H) return (int)hipErrorInvalidValue;
+    if ((reinterpret_cast<uintptr_t>(idx) & 15u) || (reinterpret_cast<uintptr_t>(H) & 15u) ||
+        (reinterpret_cast<uintptr_t>(pool_src) & 7u) || (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return (int)hipErrorInvalidValue;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    constexpr int P = 2;
+    const int64_t blocks = (n + (int64_t)hg::kBlock * P - 1) / ((int64_t)hg::kBlock * P);
+    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const auto* ix = reinterpret_cast<const uint4*>(idx);
+    const unsigned g = (unsigned)blocks;
+    const bool norm = flags & HG_FLAG_NORMALIZE;
+#define HG_SS(A, N) hg::sample_solve_kernel<A, N, P><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n)
+    if (algo == 0) { if (norm) HG_SS(hg::kACA, true); else HG_SS(hg::kACA, false); }
+    else { if (norm) HG_SS(hg::kSKS, true); else HG_SS(hg::kSKS, false); }
+#undef HG_SS
+    return (int)hipGetLastError();
+}
+
+int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,
+                        uint32_t npool, float thresh, uint32_t* counts, void* stream) {
+    if (n < 0) return (int)hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!H || !counts || (npool && (!pool_src || !pool_tar))) return (int)hipErrorInvalidValue;
+    if ((reinterpret_cast<uintptr_t>(pool_src) & 7u) || (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return (int)hipErrorInvalidValue;
+    const int64_t blocks = (n + hg::kBlock - 1) / hg::kBlock;
+    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    const float t2 = thresh * thresh;
+    hg::ransac_score_kernel<<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+        H, n, reinterpret_cast<const float2*>(pool_src), reinterpret_cast<const float2*>(pool_tar),
+        npool, t2, counts);
+    return (int)hipGetLastError();
+}
+
+}  // extern "C"

@@ -240,26 +240,6 @@ def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: fl
     return out
 
 
-def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tensor,
-                 algo: str = "aca", normalize: bool = True) -> torch.Tensor:
-    """Fused hypothesis generation: gather 4 correspondences per row of ``idx``
-    ((n,4) int32/uint32, reduced modulo the pool size like get_rand_list,
-    GPU_Runtime Test.cu:56-59) from (npool,2) pools and solve.  Returns (n,9)."""
-    dev = _require_device(pool_src, pool_tar, idx)
-    if idx.dim() != 2 or idx.shape[1] != 4 or idx.dtype not in (torch.int32, torch.uint32):
-        raise ValueError("idx must be an (n,4) int32/uint32 tensor")
-    pool_src = pool_src.to(torch.float32).contiguous()
-    pool_tar = pool_tar.to(torch.float32).contiguous()
-    idx = idx.contiguous()
-    n = idx.shape[0]
-    out = torch.empty((n, 9), dtype=torch.float32, device=dev)
-    with _guard(dev):
-        _lib.call("hg_sample_solve_f32", pool_src.data_ptr(), pool_tar.data_ptr(),
-                  pool_src.shape[0], idx.data_ptr(), out.data_ptr(), n,
-                  0 if algo == "aca" else 1, HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
-    return out
-
-
 def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
     dev = _require_device(src, dst)
     nbytes = src.numel() * src.element_size()

@@ -1,0 +1,85 @@
+"""RANSAC on the solver: hypothesis sampling, the fused
+gather + closed-form solve, and inlier scoring -- all on the device.
+
+The reference stops at timing random 4-point hypotheses: cuRAND indices, the
+get_rand_list gather and the solver kernel (GPU_Runtime Test.cu:1443-1451, :52-78,
+:81-151), the "sampling number" use case of its Table 8.  This module runs that
+pipeline, adds the scoring step it implies, and returns the best hypothesis.
+"""
+from __future__ import annotations
+
+from typing import NamedTuple
+
+import torch
+
+from . import _lib
+from .ops import _guard, _require_device, _stream
+
+
+def fill_bits(count: int, seed: int, offset: int = 0, device="cuda") -> torch.Tensor:
+    """Counter-based uint32 draws (held in an int32 tensor), bit-identical to the
+    host regeneration."""
+    dev = torch.device(device)
+    out = torch.empty(count, dtype=torch.int32, device=dev)
+    with _guard(dev):
+        _lib.call("hg_fill_bits_u32", out.data_ptr(), count, seed, offset, _stream(dev))
+    return out
+
+
+def _pool(pool: torch.Tensor) -> torch.Tensor:
+    if pool.dim() != 2 or pool.shape[1] != 2:
+        raise ValueError(f"pool must be (npool,2), got {tuple(pool.shape)}")
+    return pool.to(torch.float32).contiguous()
+
+
+def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tensor,
+                 algo: str = "aca", normalize: bool = True) -> torch.Tensor:
+    """H of each row of ``idx`` ((n,4) int32/uint32; entries reduced modulo the pool
+    size like get_rand_list, .cu:56-59) gathered from (npool,2) pools.  (n,9)."""
+    dev = _require_device(pool_src, pool_tar, idx)
+    if idx.dim() != 2 or idx.shape[1] != 4 or idx.dtype not in (torch.int32, torch.uint32):
+        raise ValueError("idx must be an (n,4) int32/uint32 tensor")
+    if algo not in ("aca", "sks"):
+        raise ValueError(f"algo must be 'aca' or 'sks', got {algo!r}")
+    ps, pt, idx = _pool(pool_src), _pool(pool_tar), idx.contiguous()
+    n = idx.shape[0]
+    out = torch.empty((n, 9), dtype=torch.float32, device=dev)
+    with _guard(dev):
+        _lib.call("hg_sample_solve_f32", ps.data_ptr(), pt.data_ptr(), ps.shape[0],
+                  idx.data_ptr(), out.data_ptr(), n, 0 if algo == "aca" else 1,
+                  1 if normalize else 0, _stream(dev))
+    return out
+
+
+def score(H: torch.Tensor, pool_src: torch.Tensor, pool_tar: torch.Tensor,
+          thresh: float) -> torch.Tensor:
+    """Inlier count of every hypothesis H (n,9) over the pool: points whose
+    reprojection error is at most ``thresh`` (division-free test, see
+    include/sks_homography.h).  Returns (n,) int32."""
+    dev = _require_device(H, pool_src, pool_tar)
+    H = H.reshape(-1, 9).to(torch.float32).contiguous()
+    ps, pt = _pool(pool_src), _pool(pool_tar)
+    counts = torch.empty(H.shape[0], dtype=torch.int32, device=dev)
+    with _guard(dev):
+        _lib.call("hg_ransac_score_f32", H.data_ptr(), H.shape[0], ps.data_ptr(), pt.data_ptr(),
+                  ps.shape[0], float(thresh), counts.data_ptr(), _stream(dev))
+    return counts
+
+
+class RansacResult(NamedTuple):
+    H: torch.Tensor          # (9,) best hypothesis (normalised)
+    inliers: int             # its inlier count
+    index: int               # which hypothesis won
+    counts: torch.Tensor     # (n,) inlier count of every hypothesis
+
+
+def ransac(pool_src: torch.Tensor, pool_tar: torch.Tensor, hypotheses: int, thresh: float,
+           seed: int = 11, algo: str = "aca") -> RansacResult:
+    """Draws ``hypotheses`` random 4-point samples, solves them all, scores them all
+    and returns the best (ties: lowest index)."""
+    dev = _require_device(pool_src, pool_tar)
+    idx = fill_bits(hypotheses * 4, seed, 0, dev).view(hypotheses, 4)
+    H = sample_solve(pool_src, pool_tar, idx, algo=algo, normalize=True)
+    counts = score(H, pool_src, pool_tar, thresh)
+    best = int((counts == counts.max()).nonzero()[0].item())
+    return RansacResult(H[best].clone(), int(counts[best].item()), best, counts)

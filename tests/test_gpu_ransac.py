@@ -1,0 +1,59 @@
+"""RANSAC extension on the GPU: draws, fused sampler and inlier scorer
+are bit-exact against the oracle; the pipeline finds the dominant homography of the
+reference's own correspondence file (orig_pts_wall.txt, via tests/golden)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _pool(dev):
+    g = load_golden("cpp_wall.npz")
+    return (g["pool_src"], g["pool_tar"], torch.from_numpy(g["pool_src"]).to(dev),
+            torch.from_numpy(g["pool_tar"]).to(dev))
+
+
+def test_fill_bits_matches_host(oracle, pkg, dev):
+    for off in (0, 977, (1 << 34) + 3):
+        got = pkg.fill_bits(50_001, 7, off, dev).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got, oracle.fill_bits(50_001, 7, off))
+
+
+@pytest.mark.parametrize("n", [1, 127, 128, 129, 1000, 65_537])
+@pytest.mark.parametrize("algo", ["aca", "sks"])
+def test_sample_solve_ragged_vs_oracle(orc, oracle, pkg, dev, n, algo):
+    ps, pt, dps, dpt = _pool(dev)
+    idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
+    H = pkg.sample_solve(dps, dpt, idx, algo=algo)
+    s, t = oracle.sample_problems(ps, pt, idx.cpu().numpy().view(np.uint32))
+    ok = orc.same_bits(H.cpu().numpy(), oracle.solve(algo, s, t))
+    assert ok.all(), f"{(~ok).sum()} differ"
+
+
+@pytest.mark.parametrize("npool", [1, 3, 4, 2047, 2048, 2049, 2540])
+def test_score_vs_oracle(oracle, pkg, dev, npool):
+    ps, pt, dps, dpt = _pool(dev)
+    ps, pt, dps, dpt = ps[:npool], pt[:npool], dps[:npool], dpt[:npool]
+    n = 3001
+    idx = pkg.fill_bits(n * 4, 5, 0, dev).view(n, 4)
+    H = pkg.sample_solve(dps, dpt, idx)
+    for thresh in (0.5, 3.0):
+        got = pkg.ransac_score(H, dps, dpt, thresh).cpu().numpy().view(np.uint32)
+        want = oracle.ransac_score(H.cpu().numpy(), ps, pt, thresh)
+        np.testing.assert_array_equal(got, want)
+
+
+def test_ransac_end_to_end(oracle, pkg, dev):
+    ps, pt, dps, dpt = _pool(dev)
+    res = pkg.ransac(dps, dpt, hypotheses=20_000, thresh=3.0, seed=11)
+    counts = res.counts.cpu().numpy()
+    assert res.inliers == counts.max() and counts[res.index] == res.inliers
+    assert res.index == int(np.flatnonzero(counts == counts.max())[0])
+    # the oracle agrees on the winner's count
+    want = oracle.ransac_score(res.H.cpu().numpy()[None], ps, pt, 3.0)[0]
+    assert want == res.inliers
+    # a wall seen from two views: the best of 20 K hypotheses explains most pairs
+    assert res.inliers > 0.5 * ps.shape[0], res.inliers

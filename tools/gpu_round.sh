@@ -44,6 +44,16 @@ for step in $STEPS; do
                 -d "$OUT/pmc_write_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kbench_soa) run kbench_soa 600 python tools/kbench_soa.py ;;
+        dist2)
+            # rehearse the N>1 control path (barriers, max-over-ranks, one JSON line) with
+            # 2 ranks sharing the one GPU over gloo; the real N>1 run uses RCCL
+            run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 \
+                --warmup 2 --no-extras --dist-backend gloo ;;
+        torchrun1)
+            run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
+                --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 50 \
+                --warmup 5 --no-extras --no-cpu ;;
         *) echo "unknown step $step" ;;
     esac
 done
