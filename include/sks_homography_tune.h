@@ -29,6 +29,12 @@ const char* hg_tune_soa_variant_name(int variant);
 int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H, int64_t n,
                 int per_cu, void* stream);
 
+/* RANSAC scorer variants: 0 = one hypothesis per lane, 1/2 = two per lane packed
+ * (inner unroll 1/4).  Same counts as hg_ransac_score_f32. */
+int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
+                  const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
+                  void* stream);
+
 #ifdef __cplusplus
 }
 #endif

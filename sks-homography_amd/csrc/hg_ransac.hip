@@ -138,9 +138,82 @@ __global__ __launch_bounds__(kBlock) void ransac_score_kernel(
     if (p < n) counts[p] = cnt;
 }
 
+// Two hypotheses per lane, evaluated as packed pairs (v_pk_fma_f32 / v_pk_mul_f32:
+// one instruction serves both), every LDS point read shared by both.  Same per-pair
+// arithmetic (and bits) as is_inlier.
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void ransac_score2_kernel(
+    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
+    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
+    __shared__ __attribute__((aligned(16))) float4 pts[kScoreChunk];
+    // lane owns hypotheses p0 = 2*gid and p0 + 1 (adjacent rows: one 72-B read)
+    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    f32x2 h[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        h[k].x = p0 < n ? H[p0 * 9 + k] : 0.f;
+        h[k].y = p0 + 1 < n ? H[(p0 + 1) * 9 + k] : 0.f;
+    }
+    const f32x2 t2v = {t2, t2};
+    i32x2 cnt = {0, 0};
+    for (uint32_t c0 = 0; c0 < npool; c0 += kScoreChunk) {
+        const uint32_t m = npool - c0 < (uint32_t)kScoreChunk ? npool - c0 : kScoreChunk;
+        __syncthreads();
+        for (uint32_t i = threadIdx.x; i < m; i += kBlock) {
+            const float2 a = pool_src[c0 + i], b = pool_tar[c0 + i];
+            pts[i] = make_float4(a.x, a.y, b.x, b.y);
+        }
+        __syncthreads();
+        auto pair = [&](float4 q) {
+            const f32x2 x = {q.x, q.x}, y = {q.y, q.y}, nu = {-q.z, -q.z}, nv = {-q.w, -q.w};
+            const f32x2 xs = __builtin_elementwise_fma(h[0], x, __builtin_elementwise_fma(h[1], y, h[2]));
+            const f32x2 ys = __builtin_elementwise_fma(h[3], x, __builtin_elementwise_fma(h[4], y, h[5]));
+            const f32x2 ws = __builtin_elementwise_fma(h[6], x, __builtin_elementwise_fma(h[7], y, h[8]));
+            const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
+            const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
+            const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
+            const f32x2 lim = t2v * (ws * ws);
+            const f32x2 zero = {0.f, 0.f};
+            cnt -= (e2 <= lim) & (ws != zero);   // vector compares yield -1 / 0
+        };
+        uint32_t i = 0;
+        for (; i + UNROLL <= m; i += UNROLL) {
+#pragma unroll
+            for (int u = 0; u < UNROLL; ++u) pair(pts[i + u]);
+        }
+        for (; i < m; ++i) pair(pts[i]);
+    }
+    if (p0 < n) counts[p0] = (uint32_t)cnt.x;
+    if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
+}
+
 }  // namespace hg
 
 extern "C" {
+
+// Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
+// 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4).
+int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
+                  const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
+                  void* stream) {
+    if (n <= 0 || !H || !counts) return (int)hipErrorInvalidValue;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const float t2 = thresh * thresh;
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const int64_t b1 = (n + hg::kBlock - 1) / hg::kBlock;
+    const int64_t b2 = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
+    switch (variant) {
+        case 0: hg::ransac_score_kernel<<<(unsigned)b1, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 1: hg::ransac_score2_kernel<1><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 2: hg::ransac_score2_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
 
 int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset, void* stream) {
     if (count < 0) return (int)hipErrorInvalidValue;
@@ -186,10 +259,11 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
     if (!H || !counts || (npool && (!pool_src || !pool_tar))) return (int)hipErrorInvalidValue;
     if ((reinterpret_cast<uintptr_t>(pool_src) & 7u) || (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
         return (int)hipErrorInvalidValue;
-    const int64_t blocks = (n + hg::kBlock - 1) / hg::kBlock;
+    // shipped: two hypotheses per lane, packed (tools/kbench_score.py, profiles/r01)
+    const int64_t blocks = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
     if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
     const float t2 = thresh * thresh;
-    hg::ransac_score_kernel<<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+    hg::ransac_score2_kernel<4><<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
         H, n, reinterpret_cast<const float2*>(pool_src), reinterpret_cast<const float2*>(pool_tar),
         npool, t2, counts);
     return (int)hipGetLastError();

@@ -83,6 +83,18 @@ def test_other_entry_validation(pkg):
     assert lib.hg_fill_uniform_f32(None, 0, 0, 0, 0.0, 1.0, None) == 0
     assert lib.hg_sample_solve_f32(None, None, 0, None, None, 4, 0, 0, None) == 1  # npool 0
     assert lib.hg_sample_solve_f32(None, None, 5, None, None, 4, 9, 0, None) == 1  # algo
+    assert lib.hg_sample_solve_f32(None, None, 5, 8, 16, 4, 0, 0, None) == 1      # unaligned idx
+    assert lib.hg_fill_bits_u32(None, -1, 0, 0, None) == 1
+    assert lib.hg_fill_bits_u32(None, 0, 0, 0, None) == 0
+    assert lib.hg_ransac_score_f32(None, -1, None, None, 0, 1.0, None, None) == 1
+    assert lib.hg_ransac_score_f32(None, 0, None, None, 0, 1.0, None, None) == 0
+    assert lib.hg_ransac_score_f32(None, 3, None, None, 0, 1.0, None, None) == 1
+    assert lib.hg_tensor_aca_offsets_f32(None, None, None, -2, 1.0, 1.0, None) == 1
+    assert lib.hg_tensor_aca_offsets_f32(None, None, None, 0, 1.0, 1.0, None) == 0
+    assert lib.hg_tensor_aca_offsets_backward_f32(None, None, None, 3, 1.0, 1.0, None, None,
+                                                  None) == 1
+    assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
+                                               None) == 1
     assert lib.hg_stream_copy(None, None, 17, None) == 1                          # not x16
     assert lib.hg_stream_copy(None, None, 0, None) == 0
     assert pkg.version().startswith("sks-homography-amd")

@@ -44,6 +44,7 @@ for step in $STEPS; do
                 -d "$OUT/pmc_write_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kbench_soa) run kbench_soa 600 python tools/kbench_soa.py ;;
+        kbench_score) run kbench_score 600 python tools/kbench_score.py ;;
         dist2)
             # rehearse the N>1 control path (barriers, max-over-ranks, one JSON line) with
             # 2 ranks sharing the one GPU over gloo; the real N>1 run uses RCCL
