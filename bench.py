@@ -217,6 +217,49 @@ def reference_layout(d: Dist, pkg):
     return out
 
 
+def host_boundary_section(d: Dist, pkg, n: int):
+    """What the host-buffer side of the boundary costs (reported, never `value`):
+    (1) the reference's single-problem C++ call sks::runKernel_ACA on host pointers
+    (one H2D + launch + D2H each, synchronous like ACA_SKS.cpp:24); (2) a host-resident
+    n-problem batch: pinned H2D of src/tar + the kernel + D2H of H, i.e. the
+    PCIe-inclusive rate of a caller whose data lives in host memory."""
+    import ctypes
+    lib = pkg.lib()
+    f = lib._ZN3sks13runKernel_ACAEPfS0_S0_
+    f.restype = ctypes.c_int
+    s8 = (ctypes.c_float * 8)(*[0, 0, 200, 0, 50, 139, 181, 93])
+    t8 = (ctypes.c_float * 8)(*[10, 12, 220, 5, 40, 160, 190, 110])
+    h9 = (ctypes.c_float * 9)()
+    for _ in range(100):
+        f(s8, t8, h9)
+    reps = 2000
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        f(s8, t8, h9)
+    single_us = (time.perf_counter() - t0) / reps * 1e6
+    hs = torch.empty((n, 8), dtype=torch.float32).pin_memory()
+    ht = torch.empty((n, 8), dtype=torch.float32).pin_memory()
+    hH = torch.empty((n, 9), dtype=torch.float32).pin_memory()
+    hs.copy_(pkg.fill_uniform(n * 8, SEED, 0, device=d.dev).view(n, 8).cpu())
+    ht.copy_(pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(n, 8).cpu())
+    ds = torch.empty((n, 8), device=d.dev)
+    dt = torch.empty((n, 8), device=d.dev)
+    dH = torch.empty((n, 9), device=d.dev)
+
+    def step():
+        ds.copy_(hs, non_blocking=True)
+        dt.copy_(ht, non_blocking=True)
+        pkg.solve("aca", ds, dt, out=dH)
+        hH.copy_(dH, non_blocking=True)
+
+    step()
+    wall, _ = timed_region(d, step, 5)
+    return {"single_problem_host_ptr_us": round(single_us, 2),
+            "pcie_inclusive_batch": n, "pcie_inclusive_ms": round(wall / 5 * 1e3, 3),
+            "pcie_inclusive_M_homographies_per_s": round(n * 5 / wall / 1e6, 1),
+            "pcie_bytes_per_problem": 100}
+
+
 def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     """1M random 4-point hypotheses over the reference's own
     correspondence file (orig_pts_wall.txt, 2540 pairs, committed in tests/golden):
@@ -380,6 +423,18 @@ def main():
         del bs_h, bt_h, Hb
         line["reference_layout"] = reference_layout(d, pkg)
         line["ransac"] = ransac_section(d, pkg)
+        line["host_boundary"] = host_boundary_section(d, pkg, n)
+        # f64 AoS (sks::runKernel_ACA_double semantics) on the same inputs
+        s64, t64 = src.double(), tar.double()
+        H64 = torch.empty((n, 9), dtype=torch.float64, device=d.dev)
+        f64 = lambda: pkg.solve("aca", s64, t64, normalize=True, out=H64)  # noqa: E731
+        for _ in range(5):
+            f64()
+        _, ms64 = timed_region(d, f64, 50)
+        line["aca_f64_aos"] = {"us_per_launch": round(ms64 * 1e3, 2),
+                               "G_homographies_per_s": round(n / (ms64 * 1e-3) / 1e9, 2),
+                               "achieved_gbps": round(n * 200 / (ms64 * 1e-3) / 1e9, 1)}
+        del s64, t64, H64
 
     if args.gather and d.world > 1:
         d.barrier()

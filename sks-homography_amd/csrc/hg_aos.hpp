@@ -112,6 +112,30 @@ __device__ __forceinline__ void dma_slab_issue(const char* __restrict__ g, char*
                                          (lds_ptr_t)(l + 16 * c * kWave), 16, 0, NT ? 2 : 0);
 }
 
+// The same issue through inline asm (cdna_hip_programming.md section 5.7): hipcc then
+// does not see LDS writes in flight, so it inserts no `s_waitcnt vmcnt(0)` before
+// later ds_reads -- the caller's counted `s_waitcnt vmcnt(N)` alone orders them.
+// Needed to keep a next tile's DMA in flight while the current tile is read.
+template <int kBytes, bool NT>
+__device__ __forceinline__ void dma_slab_issue_asm(const char* __restrict__ g, char* l, int lane) {
+    static_assert(kBytes % (16 * kWave) == 0, "slab must be whole 1 KiB pieces");
+    const uint32_t lbase = __builtin_amdgcn_readfirstlane(
+        (uint32_t)(uintptr_t)(__attribute__((address_space(3))) char*)l);
+#pragma unroll
+    for (int c = 0; c < kBytes / (16 * kWave); ++c) {
+        const char* gp = g + 16 * (c * kWave + lane);
+        uint32_t keep;
+        if constexpr (NT)
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                         "global_load_lds_dwordx4 %1, off nt\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(gp), "s"(lbase + 1024u * c) : "memory");
+        else
+            asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\t"
+                         "global_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                         : "=&s"(keep) : "v"(gp), "s"(lbase + 1024u * c) : "memory");
+    }
+}
+
 __device__ __forceinline__ void dma_wait_sync() {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     wave_lds_sync();
@@ -234,6 +258,62 @@ __global__ __launch_bounds__(kBlock) void solve_aos(const T* __restrict__ src,
         if (t < tiles)
             aos_wave_tile<ALGO, NORM, T, P, FL>(src, tar, H, n, t * S::kTile, smem[wave], lane);
     }
+}
+
+// Pipelined AoS kernel (experiment, hg_tune.hip): each wave walks TPW consecutive
+// full tiles with a 2-deep LDS ring -- the LDS-DMA of tile i+1 is in flight while
+// tile i is solved and stored; a counted `s_waitcnt vmcnt(N)` (N = the next tile's
+// DMA instructions) retires tile i only.  The ragged tail tile takes the per-lane path.
+template <int ALGO, bool NORM, int P, int TPW>
+__global__ __launch_bounds__(kBlock) void solve_aos_pipe(const float* __restrict__ src,
+                                                         const float* __restrict__ tar,
+                                                         float* __restrict__ H, int64_t n) {
+    constexpr int kTile = kWave * P;
+    constexpr int kSlab = kTile * 32;               // bytes per operand per tile
+    constexpr int kPieces = kSlab / (16 * kWave);   // DMA instructions per operand
+    constexpr int kBuf = 2 * kSlab;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][2 * kBuf];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t full_tiles = n / kTile;
+    const int64_t t0 = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * TPW;
+    char* ring = smem[wave];
+    auto issue = [&](int64_t t, char* buf) {
+        dma_slab_issue_asm<kSlab, true>(reinterpret_cast<const char*>(src + t * kTile * 8), buf,
+                                        lane);
+        dma_slab_issue_asm<kSlab, true>(reinterpret_cast<const char*>(tar + t * kTile * 8),
+                                        buf + kSlab, lane);
+    };
+    const int64_t cnt = full_tiles - t0 < TPW ? full_tiles - t0 : TPW;
+    if (cnt > 0) {
+        issue(t0, ring);
+        for (int i = 0; i < cnt; ++i) {
+            char* cur = ring + (i & 1) * kBuf;
+            if (i + 1 < cnt) {
+                issue(t0 + i + 1, ring + ((i + 1) & 1) * kBuf);
+                asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * kPieces) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            }
+            wave_lds_sync();
+            float h[P][9];
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int row = j * kWave + lane;
+                float s[8], t[8];
+                __builtin_memcpy(s, cur + row * 32, 32);
+                __builtin_memcpy(t, cur + kSlab + row * 32, 32);
+                solve<ALGO, NORM>(s, t, h[j]);
+            }
+            wave_lds_sync();
+            store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + (t0 + i) * kTile * 9),
+                                               h, cur, lane);
+        }
+    }
+    // the ragged tail tile belongs to the wave whose range holds tile index full_tiles
+    if (n % kTile && t0 <= full_tiles && full_tiles < t0 + TPW)
+        aos_wave_tile<ALGO, NORM, float, P, kNtLoad | kNtStore | kDirectSt>(
+            src, tar, H, n, full_tiles * kTile, ring, lane);
 }
 
 // Grid for solve_aos: one block per 4 tiles, or a persistent grid of `per_cu`

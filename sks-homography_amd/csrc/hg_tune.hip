@@ -25,6 +25,17 @@ int launch_variant(int algo, const float* s, const float* t, float* H, int64_t n
     return (int)hipGetLastError();
 }
 
+template <int P, int TPW>
+int launch_pipe(int algo, const float* s, const float* t, float* H, int64_t n, int,
+                hipStream_t st) {
+    const int64_t tiles = (n + kWave * P - 1) / (kWave * P);
+    const int64_t waves = (tiles + TPW - 1) / TPW;
+    const unsigned g = (unsigned)((waves + kWavesPerBlock - 1) / kWavesPerBlock);
+    if (algo == 0) solve_aos_pipe<kACA, true, P, TPW><<<g, kBlock, 0, st>>>(s, t, H, n);
+    else solve_aos_pipe<kSKS, true, P, TPW><<<g, kBlock, 0, st>>>(s, t, H, n);
+    return (int)hipGetLastError();
+}
+
 const Variant kVariants[] = {
     {"P4 nt-ld nt-st stage (first version)", launch_variant<4, kNtLoad | kNtStore>},
     {"P4 plain", launch_variant<4, 0>},
@@ -51,6 +62,10 @@ const Variant kVariants[] = {
     {"P1 nt lds-dma", launch_variant<1, kNtLoad | kNtStore | kLdsLoad | kLdsDma>},
     {"P2 lds-dma nt-ld plain-st", launch_variant<2, kNtLoad | kLdsLoad | kLdsDma>},
     {"P3 nt lds-dma", launch_variant<3, kNtLoad | kNtStore | kLdsLoad | kLdsDma>},
+    {"P2 pipe x2 tiles/wave", launch_pipe<2, 2>},
+    {"P2 pipe x4 tiles/wave", launch_pipe<2, 4>},
+    {"P2 pipe x8 tiles/wave", launch_pipe<2, 8>},
+    {"P1 pipe x4 tiles/wave", launch_pipe<1, 4>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.

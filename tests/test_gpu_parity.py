@@ -344,3 +344,25 @@ def test_rect_autograd_matches_reference_autograd(pkg, dev):
     with torch.no_grad():
         H2 = pkg.TensorACA_rect(B, sh, th, 50.0, 1.25)
     assert torch.equal(H.detach(), H2)
+
+
+@pytest.mark.slow
+def test_beyond_int32_problem_count(orc, oracle, pkg, dev):
+    """n > 2^31 (the reference kernels index with int, .cu:82; ours with int64):
+    215 GB of HBM.  The first and the last 2^20+ problems are regenerated on the host
+    from the counter stream and compared bit for bit."""
+    n = (1 << 31) + (1 << 20) + 7
+    free, _ = torch.cuda.mem_get_info(dev)
+    if free < n * 100 + (8 << 30):
+        pytest.skip(f"needs {n * 100 / 2**30:.0f} GiB of free HBM, have {free / 2**30:.0f}")
+    src = pkg.fill_uniform(n * 8, 21, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 21, n * 8, device=dev).view(n, 8)
+    H = torch.empty(n, 9, device=dev)
+    pkg.aca(src, tar, out=H)
+    head, tail = 4096, (1 << 20) + 7
+    for lo, cnt in ((0, head), (n - tail, tail)):
+        s = oracle.fill_uniform(cnt * 8, 21, lo * 8).reshape(cnt, 8)
+        t = oracle.fill_uniform(cnt * 8, 21, n * 8 + lo * 8).reshape(cnt, 8)
+        _bits(orc, H[lo:lo + cnt], oracle.solve("aca", s, t), f"aca rows [{lo}, {lo + cnt})")
+    del src, tar, H
+    torch.cuda.empty_cache()

@@ -1,0 +1,72 @@
+"""Property tests (hypothesis for projective consistency).
+
+CPU: the oracle's H maps every source point onto its target (f64), ACA and SKS agree,
+normalisation fixes H[8] = 1.  GPU: arbitrary float32 bit patterns (NaN, Inf,
+subnormals, huge) drawn by hypothesis, solved as one batch, equal the oracle bit for
+bit."""
+import numpy as np
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+from hypothesis.extra.numpy import arrays
+
+
+def _project(H, pts):
+    ph = np.c_[pts, np.ones(len(pts))] @ H.reshape(3, 3).T
+    return ph[:, :2] / ph[:, 2:3]
+
+
+@st.composite
+def well_posed(draw):
+    """A convex-ish source quad and a moderate random homography (f64)."""
+    jitter = draw(arrays(np.float64, (4, 2), elements=st.floats(-20, 20)))
+    base = np.array([[0, 0], [200, 0], [0, 160], [200, 160]], np.float64) + jitter
+    off = draw(st.tuples(st.floats(-500, 500), st.floats(-500, 500)))
+    base = base + np.array(off)
+    a = draw(arrays(np.float64, (8,), elements=st.floats(-0.2, 0.2)))
+    Ht = np.array([[1 + a[0], a[1], 30 * a[2]], [a[3], 1 + a[4], 30 * a[5]],
+                   [1e-4 * a[6], 1e-4 * a[7], 1.0]])
+    return base, Ht
+
+
+@settings(max_examples=200, deadline=None)
+@given(well_posed())
+def test_oracle_recovers_true_homography_f64(oracle, case):
+    src, Ht = case
+    tar = _project(Ht, src)
+    for algo in ("aca", "sks"):
+        H = oracle.solve(algo, src.reshape(1, 8), tar.reshape(1, 8))[0]
+        assert H[8] == 1.0
+        np.testing.assert_allclose(H, (Ht / Ht[2, 2]).ravel(), rtol=1e-6, atol=1e-9)
+        np.testing.assert_allclose(_project(H, src), tar, rtol=0, atol=1e-6)
+
+
+@settings(max_examples=200, deadline=None)
+@given(well_posed())
+def test_oracle_aca_sks_agree_f32(oracle, case):
+    src, Ht = case
+    tar = _project(Ht, src)
+    s = src.reshape(1, 8).astype(np.float32)
+    t = tar.reshape(1, 8).astype(np.float32)
+    a = oracle.solve("aca", s, t)[0].astype(np.float64)
+    k = oracle.solve("sks", s, t)[0].astype(np.float64)
+    assert np.linalg.norm(a - k) / np.linalg.norm(a) < 1e-3
+
+
+@pytest.mark.gpu
+@settings(max_examples=25, deadline=None, suppress_health_check=list(HealthCheck))
+@given(arrays(np.float32, (257, 16), elements=st.floats(width=32, allow_nan=True,
+                                                          allow_infinity=True,
+                                                          allow_subnormal=True)))
+def test_gpu_bit_exact_on_arbitrary_floats(orc, oracle, pkg, dev, batch):
+    src = np.ascontiguousarray(batch[:, :8])
+    tar = np.ascontiguousarray(batch[:, 8:])
+    ds, dt = torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev)
+    for algo in ("aca", "sks"):
+        for norm in (True, False):
+            H = pkg.solve(algo, ds, dt, normalize=norm).cpu().numpy()
+            assert orc.same_bits(H, oracle.solve(algo, src, tar, normalize=norm)).all()
+        H64 = pkg.solve(algo, ds.double(), dt.double()).cpu().numpy()
+        assert orc.same_bits(H64, oracle.solve(algo, src.astype(np.float64),
+                                               tar.astype(np.float64))).all()
