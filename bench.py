@@ -152,7 +152,8 @@ def cpu_baseline(n_sample: int):
     tar = gen.fill_uniform(n_sample * 8, SEED, n_sample * 8).reshape(n_sample, 8)
     H = np.empty((n_sample, 9), dtype=np.float32)
     out = {}
-    for algo in ("aca", "sks"):
+    algos = ("aca", "sks", "ge") if kind == "reference" else ("aca", "sks")
+    for algo in algos:
         t1 = engine.time_batch(algo, src, tar, H, threads, 1)
         reps = max(1, int(1.5 / max(t1, 1e-6)))
         t = engine.time_batch(algo, src, tar, H, threads, reps)
@@ -161,11 +162,11 @@ def cpu_baseline(n_sample: int):
     single = {}
     if kind == "reference":
         # the reference's own CPU methodology (main.cpp:87-92): one set, 10 M calls
-        for algo in ("aca", "sks"):
+        for algo in algos:
             single[algo] = engine.time_repeat(algo, src[0], tar[0], 10_000_000) / 1e7 * 1e6
     return {
         "value": out["aca"], "unit": "M homographies/s", "cores": threads, "kind": kind,
-        "sks_value": out["sks"],
+        "sks_value": out["sks"], "ge_value": out.get("ge"),
         "sample": (f"AoS f32 normalised batch of {n_sample} problems (seed {SEED}, U[0,1024)), "
                    f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, {threads} std::threads"),
         "single_core_same_points_us_per_H": single or None,
@@ -351,6 +352,18 @@ def main():
             "frac": round(n * bpp / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             "sks_over_aca_time": round(ms_s / ms_launch, 3),
             "traffic": pmc_traffic("sks_f32_aos_norm"),
+        }
+        # the reference's RHO-GE comparison baseline on the same inputs
+        for _ in range(args.warmup):
+            run("ge")()
+        wall_g, ms_g = timed_region(d, run("ge"), args.steps)
+        line["ge_baseline"] = {
+            "value": round(n_total * args.steps / wall_g / 1e6, 2), "unit": "M homographies/s",
+            "ms_per_step": round(wall_g / args.steps * 1e3, 5),
+            "achieved_gbps": round(n * bpp / (ms_g * 1e-3) / 1e9, 1),
+            "aca_speedup_over_ge": round(ms_g / ms_launch, 3),
+            "note": "all three closed forms are HBM-bound on MI355X: FLOP savings no longer "
+                    "show at 10M; the CPU baseline shows them",
         }
         # streaming-copy yardstick over the same byte count
         nb = (n * bpp) // 2 // 16 * 16

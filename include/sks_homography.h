@@ -60,6 +60,13 @@ int hg_sks_f32(const float* src, const float* tar, float* H, int64_t n, int layo
 int hg_sks_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
                int flags, void* stream);
 
+/* RHO Gaussian elimination, binary32 -- the reference's comparison baseline
+ * cv::runKernel_GE (C++ Codes/modules/GE.cpp:41-188; OpenCV rho.cpp hFuncRefC), batched
+ * (SURVEY 8(f).4).  Its H[8] is 1 by construction; HG_FLAG_NORMALIZE is accepted and
+ * changes no bits. */
+int hg_ge_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
+              void* stream);
+
 /* TensorACA, rectangle -> quadrangle, binary32, unnormalised.  Replaces
  * TensorACA_rect(bs, src, tar, scale, div) (PyTorch Codes/Modules_Runtime_Test.py:286-309).
  * src, tar: (B,3,4) homogeneous point tensors (rows x, y, 1; columns M, N, P, Q);

@@ -12,12 +12,15 @@
 # `#include "SKS.hpp"` -- a header name that does not exist in the reference (the
 # shipped header is ACA_SKS.hpp, which only pulls an unused OpenCV include).  The
 # solver bodies use no symbol from either, so the recipe streams the file through
-# `sed` dropping its #include line(s) and compiles it from stdin.  No stand-in
+# `sed` dropping its #include line(s) and compiles it from stdin.  GE.cpp (the RHO-GE
+# baseline) gets the same treatment: its only include is GE.hpp -> opencv2/core.hpp,
+# and its body (OpenCV rho.cpp hFuncRefC) uses no OpenCV symbol.  No stand-in
 # header is written and no reference text is copied into this repository.
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REF_ROOT="${SKS_REFERENCE_ROOT:-/root/reference}"
 REF_SRC="$REF_ROOT/C++ Codes/modules/ACA_SKS.cpp"
+REF_GE="$REF_ROOT/C++ Codes/modules/GE.cpp"   # RHO-GE baseline (includes only GE.hpp -> OpenCV)
 CFLAGS=(-O2 -fPIC -ffp-contract=off -fno-fast-math)
 
 mkdir -p "$HERE/_build"
@@ -28,8 +31,11 @@ if [[ -f "$REF_SRC" ]]; then
     mkdir -p "$HERE/_ref"
     sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_SRC" |
         g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/aca_sks_ref.o"
+    sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_GE" |
+        g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/ge_ref.o"
     g++ -std=c++17 "${CFLAGS[@]}" -c "$HERE/ref_batch.cpp" -o "$HERE/_ref/ref_batch.o"
-    g++ -shared -o "$HERE/_ref/libsks_ref.so" "$HERE/_ref/aca_sks_ref.o" "$HERE/_ref/ref_batch.o" -lpthread
+    g++ -shared -o "$HERE/_ref/libsks_ref.so" "$HERE/_ref/aca_sks_ref.o" "$HERE/_ref/ge_ref.o" \
+        "$HERE/_ref/ref_batch.o" -lpthread
     rm -f "$HERE/_ref/"*.o
     echo "built oracle/_ref/libsks_ref.so from $REF_SRC"
 else

@@ -23,7 +23,7 @@ _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)
 _i64 = ctypes.c_int64
 
-ALGOS = {"aca": 0, "sks": 1}
+ALGOS = {"aca": 0, "sks": 1, "ge": 2}
 
 
 def _ptr(a: np.ndarray, ctype):
@@ -39,7 +39,8 @@ class Oracle:
             raise FileNotFoundError(f"{path} missing: run oracle/build.sh")
         lib = ctypes.CDLL(path)
         for name, fp in (("oracle_aca_f32", _f32p), ("oracle_sks_f32", _f32p),
-                         ("oracle_aca_f64", _f64p), ("oracle_sks_f64", _f64p)):
+                         ("oracle_aca_f64", _f64p), ("oracle_sks_f64", _f64p),
+                         ("oracle_ge_f32", _f32p)):
             fn = getattr(lib, name)
             fn.argtypes = [fp, fp, fp, _i64, ctypes.c_int, ctypes.c_int]
             fn.restype = ctypes.c_int

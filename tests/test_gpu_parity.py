@@ -366,3 +366,24 @@ def test_beyond_int32_problem_count(orc, oracle, pkg, dev):
         _bits(orc, H[lo:lo + cnt], oracle.solve("aca", s, t), f"aca rows [{lo}, {lo + cnt})")
     del src, tar, H
     torch.cuda.empty_cache()
+
+
+@pytest.mark.parametrize("fixture,sk,tk,hk", [("cpp_uniform.npz", "src_f32", "tar_f32", "ge_f32"),
+                                              ("cpp_wall.npz", "src", "tar", "ge"),
+                                              ("cpp_edge.npz", "src", "tar", "ge")])
+def test_golden_ge_baseline(orc, oracle, pkg, dev, fixture, sk, tk, hk):
+    """The reference's RHO-GE comparison baseline on the GPU, bit-exact (AoS + SoA)."""
+    g = load_golden(fixture)
+    src, tar = _t(g[sk], dev), _t(g[tk], dev)
+    _bits(orc, pkg.solve("ge", src, tar), g[hk], f"ge {fixture}")
+    Hs = pkg.solve("ge", src.T.contiguous(), tar.T.contiguous(), layout="soa")
+    _bits(orc, Hs.T, g[hk], f"ge soa {fixture}")
+
+
+def test_ge_random_1m_vs_oracle(orc, oracle, pkg, dev):
+    n = 1_000_003
+    src = pkg.fill_uniform(n * 8, 4, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 4, n * 8, device=dev).view(n, 8)
+    want = oracle.solve("ge", src.cpu().numpy(), tar.cpu().numpy())
+    for norm in (True, False):
+        _bits(orc, pkg.solve("ge", src, tar, normalize=norm), want, f"ge 1M norm={norm}")

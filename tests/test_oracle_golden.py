@@ -164,3 +164,12 @@ def test_oracle_rect_backward_vs_autograd_f64(oracle, scale, div):
     assert rel(gs, s64.grad.numpy()) < 1e-6
     assert abs(gsd[:, 0].astype(np.float64).sum() / sc.grad.item() - 1) < 1e-5
     assert abs(gsd[:, 1].astype(np.float64).sum() / dv.grad.item() - 1) < 1e-5
+
+
+def test_oracle_ge_vs_reference(orc, oracle):
+    """RHO-GE baseline (cv::runKernel_GE, GE.cpp:41-188) against the compiled reference."""
+    for fx, sk, tk, hk in (("cpp_uniform.npz", "src_f32", "tar_f32", "ge_f32"),
+                           ("cpp_wall.npz", "src", "tar", "ge"),
+                           ("cpp_edge.npz", "src", "tar", "ge")):
+        g = load_golden(fx)
+        _assert_bits(orc, oracle.solve("ge", g[sk], g[tk]), g[hk], f"ge {fx}")

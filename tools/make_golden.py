@@ -180,6 +180,7 @@ def main():
     t64 = rng.uniform(-512, 512, (n, 8))
     np.savez(os.path.join(OUT, "cpp_uniform.npz"), src_f32=s32, tar_f32=t32,
              aca_f32=ref.solve("aca", s32, t32), sks_f32=ref.solve("sks", s32, t32),
+             ge_f32=ref.solve("ge", s32, t32),
              src_f64=s64, tar_f64=t64, aca_f64=ref.solve("aca", s64, t64),
              sks_f64=ref.solve("sks", s64, t64))
     manifest.append("cpp_uniform.npz: 1024 U[0,1024) f32 + 1024 U[-512,512) f64 quads; "
@@ -189,7 +190,8 @@ def main():
     ws, wt, widx = wall_problems(1024, 11)
     ps, pt = read_wall()
     np.savez(os.path.join(OUT, "cpp_wall.npz"), src=ws, tar=wt, idx=widx, pool_src=ps,
-             pool_tar=pt, aca=ref.solve("aca", ws, wt), sks=ref.solve("sks", ws, wt))
+             pool_tar=pt, aca=ref.solve("aca", ws, wt), sks=ref.solve("sks", ws, wt),
+             ge=ref.solve("ge", ws, wt))
     manifest.append("cpp_wall.npz: 1024 4-subsets of orig_pts_wall.txt (reference data file), "
                     "pool + indices kept for the fused sampler; reference C++ outputs")
 
@@ -197,6 +199,7 @@ def main():
     es, et = edge_problems()
     np.savez(os.path.join(OUT, "cpp_edge.npz"), src=es, tar=et,
              aca=ref.solve("aca", es, et), sks=ref.solve("sks", es, et),
+             ge=ref.solve("ge", es, et),
              src_f64=es.astype(np.float64), tar_f64=et.astype(np.float64),
              aca_f64=ref.solve("aca", es.astype(np.float64), et.astype(np.float64)),
              sks_f64=ref.solve("sks", es.astype(np.float64), et.astype(np.float64)))
