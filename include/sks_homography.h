@@ -67,6 +67,12 @@ int hg_sks_f64(const double* src, const double* tar, double* H, int64_t n, int l
 int hg_ge_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
               void* stream);
 
+/* 8x8 LU with partial pivoting, binary64 -- the reference GPU harness's
+ * getPerspectiveTransform baseline cal_Homo_GPT (GPU_Runtime Test.cu:301-357, helpers
+ * :242-300), batched.  H[8] is 1 by construction. */
+int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream);
+
 /* TensorACA, rectangle -> quadrangle, binary32, unnormalised.  Replaces
  * TensorACA_rect(bs, src, tar, scale, div) (PyTorch Codes/Modules_Runtime_Test.py:286-309).
  * src, tar: (B,3,4) homogeneous point tensors (rows x, y, 1; columns M, N, P, Q);

@@ -464,3 +464,47 @@ static void ge_one_f32(const float* s, const float* t, float* h) {
 }
 
 DEFINE_BATCH(oracle_ge_f32, float, ge_one_f32, normalize_f32)
+
+/* ---------------------------------------------------- GPT-LU baseline ------ */
+/* Restates the reference GPU harness's cal_Homo_GPT ("GPU_Runtime Test.cu:301-357")
+ * and its helpers find_pivot / scaleIndex / eliminate / down_tri_solve /
+ * up_tri_solve (:242-300) in binary64.  The reference needs nvcc (absent), so this is
+ * pinned only by our GPU kernel (bit for bit) and by numpy's LAPACK solve (tests). */
+static void gpt_one_f64(const double* s, const double* t, double* h) {
+    double a[8][8], b[8];
+    for (int i = 0; i < 4; ++i) {
+        const double x = s[2 * i], y = s[2 * i + 1], u = t[2 * i], v = t[2 * i + 1];
+        for (int c = 0; c < 8; ++c) a[i][c] = a[i + 4][c] = 0.0;
+        a[i][0] = x; a[i][1] = y; a[i][2] = 1.0;
+        a[i][6] = -x * u; a[i][7] = -y * u;
+        a[i + 4][3] = x; a[i + 4][4] = y; a[i + 4][5] = 1.0;
+        a[i + 4][6] = -x * v; a[i + 4][7] = -y * v;
+        b[i] = u;
+        b[i + 4] = v;
+    }
+    for (int i = 0; i < 8; ++i) {
+        double best = fabs(a[i][i]);
+        int p = i;
+        for (int r = i + 1; r < 8; ++r)
+            if (best < fabs(a[r][i])) { best = fabs(a[r][i]); p = r; }
+        for (int c = 0; c < 8; ++c) { double tmp = a[i][c]; a[i][c] = a[p][c]; a[p][c] = tmp; }
+        { double tmp = b[i]; b[i] = b[p]; b[p] = tmp; }
+        for (int c = i + 1; c < 8; ++c) a[i][c] = a[i][c] / a[i][i];
+        for (int r = i + 1; r < 8; ++r)
+            for (int c = i + 1; c < 8; ++c) a[r][c] = a[r][c] - a[r][i] * a[i][c];
+    }
+    for (int k = 0; k < 8; ++k) {
+        double acc = b[k];
+        for (int j = 0; j < k; ++j) acc = acc - a[k][j] * b[j];
+        b[k] = acc / a[k][k];
+    }
+    for (int k = 6; k >= 0; --k) {
+        double acc = b[k];
+        for (int j = 7; j > k; --j) acc = acc - a[k][j] * b[j];
+        b[k] = acc;
+    }
+    for (int k = 0; k < 8; ++k) h[k] = b[k];
+    h[8] = 1.0;
+}
+
+DEFINE_BATCH(oracle_gpt_f64, double, gpt_one_f64, normalize_f64)

@@ -369,6 +369,11 @@ int hg_ge_f32(const float* src, const float* tar, float* H, int64_t n, int layou
     return hg::dispatch<hg::kGE>(src, tar, H, n, layout, flags, stream);
 }
 
+int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+               int flags, void* stream) {
+    return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream);
+}
+
 int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
                            const float* scale, const float* div, void* stream) {
     return hg::launch_rect<false>(src, tar, H, B, scale, div, 0.f, 0.f, stream);

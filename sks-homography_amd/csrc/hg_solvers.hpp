@@ -226,13 +226,85 @@ __device__ __forceinline__ void ge_solve(const T (&s)[8], const T (&t)[8], T (&h
     h[6] = m[2][7]; h[7] = m[2][3]; h[8] = T(1);
 }
 
-enum Algo : int { kACA = 0, kSKS = 1, kGE = 2 };
+// 8x8 LU with partial pivoting -- the reference GPU harness's getPerspectiveTransform
+// baseline cal_Homo_GPT (GPU_Runtime Test.cu:301-357 with its helpers find_pivot,
+// scaleIndex, eliminate, down_tri_solve, up_tri_solve, :242-300).  Crout form: row i
+// right of the diagonal is divided by the pivot, the trailing rows are updated, L
+// keeps the unscaled column.  The matrix lives in VGPRs: every loop is unrolled with
+// compile-time indices and the row swap is a select per candidate row (a runtime row
+// index would push the array to scratch, as the reference's local-memory a[64] is).
+template <typename T>
+__device__ __forceinline__ void gpt_solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
+    T a[8][8], b[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const T x = s[2 * i], y = s[2 * i + 1], u = t[2 * i], v = t[2 * i + 1];
+        a[i][0] = x; a[i][1] = y; a[i][2] = T(1);
+        a[i][3] = T(0); a[i][4] = T(0); a[i][5] = T(0);
+        a[i][6] = -x * u; a[i][7] = -y * u;
+        a[i + 4][0] = T(0); a[i + 4][1] = T(0); a[i + 4][2] = T(0);
+        a[i + 4][3] = x; a[i + 4][4] = y; a[i + 4][5] = T(1);
+        a[i + 4][6] = -x * v; a[i + 4][7] = -y * v;
+        b[i] = u;
+        b[i + 4] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        // pivot: first row of max |a[r][i]|, r >= i (strict <, as find_pivot)
+        T best = __builtin_fabs(a[i][i]);
+        int p = i;
+#pragma unroll
+        for (int r = i + 1; r < 8; ++r) {
+            const T c = __builtin_fabs(a[r][i]);
+            if (best < c) { best = c; p = r; }
+        }
+#pragma unroll
+        for (int r = i + 1; r < 8; ++r) {
+            const bool sw = p == r;
+#pragma unroll
+            for (int c = 0; c < 8; ++c) {
+                const T lo = a[i][c], hi = a[r][c];
+                a[i][c] = sw ? hi : lo;
+                a[r][c] = sw ? lo : hi;
+            }
+            const T lo = b[i], hi = b[r];
+            b[i] = sw ? hi : lo;
+            b[r] = sw ? lo : hi;
+        }
+#pragma unroll
+        for (int c = i + 1; c < 8; ++c) a[i][c] = a[i][c] / a[i][i];
+#pragma unroll
+        for (int r = i + 1; r < 8; ++r)
+#pragma unroll
+            for (int c = i + 1; c < 8; ++c) a[r][c] = a[r][c] - a[r][i] * a[i][c];
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {  // L y = b (L carries the pivots on its diagonal)
+        T acc = b[k];
+#pragma unroll
+        for (int j = 0; j < k; ++j) acc = acc - a[k][j] * b[j];
+        b[k] = acc / a[k][k];
+    }
+#pragma unroll
+    for (int k = 6; k >= 0; --k) {  // U x = y (unit diagonal), columns right to left
+        T acc = b[k];
+#pragma unroll
+        for (int j = 7; j > k; --j) acc = acc - a[k][j] * b[j];
+        b[k] = acc;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) h[k] = b[k];
+    h[8] = T(1);
+}
+
+enum Algo : int { kACA = 0, kSKS = 1, kGE = 2, kGPT = 3 };
 
 template <int ALGO, bool NORM, typename T>
 __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
     if constexpr (ALGO == kACA) aca_solve(s, t, h);
     else if constexpr (ALGO == kSKS) sks_solve(s, t, h);
-    else ge_solve(s, t, h);
+    else if constexpr (ALGO == kGE) ge_solve(s, t, h);
+    else gpt_solve(s, t, h);
     if constexpr (NORM) normalize_h(h);
 }
 

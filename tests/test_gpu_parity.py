@@ -387,3 +387,23 @@ def test_ge_random_1m_vs_oracle(orc, oracle, pkg, dev):
     want = oracle.solve("ge", src.cpu().numpy(), tar.cpu().numpy())
     for norm in (True, False):
         _bits(orc, pkg.solve("ge", src, tar, normalize=norm), want, f"ge 1M norm={norm}")
+
+
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_gpt_lu_baseline_vs_oracle(orc, oracle, pkg, dev, layout):
+    """The reference GPU harness's pivoted-LU baseline (cal_Homo_GPT), f64, bit-exact
+    against the restatement; includes the golden edge cases (pivoting on zeros/NaN)."""
+    rng = np.random.default_rng(9)
+    n = 200_003
+    s = rng.uniform(-1024, 1024, (n, 8))
+    t = rng.uniform(-1024, 1024, (n, 8))
+    g = load_golden("cpp_edge.npz")
+    s = np.concatenate([s, g["src_f64"]])
+    t = np.concatenate([t, g["tar_f64"]])
+    src, tar = _t(s, dev), _t(t, dev)
+    if layout == "soa":
+        src, tar = src.T.contiguous(), tar.T.contiguous()
+    H = pkg.solve("gpt", src, tar, layout=layout)
+    if layout == "soa":
+        H = H.T
+    _bits(orc, H, oracle.solve("gpt", s, t), f"gpt {layout}")

@@ -173,3 +173,24 @@ def test_oracle_ge_vs_reference(orc, oracle):
                            ("cpp_edge.npz", "src", "tar", "ge")):
         g = load_golden(fx)
         _assert_bits(orc, oracle.solve("ge", g[sk], g[tk]), g[hk], f"ge {fx}")
+
+
+def test_oracle_gpt_lu_vs_lapack(oracle):
+    """GPT-LU baseline (cal_Homo_GPT, GPU_Runtime Test.cu:301-357): the reference needs
+    nvcc, so the restatement is pinned against LAPACK's solve of the same 8x8 system."""
+    rng = np.random.default_rng(8)
+    n = 2000
+    s = rng.uniform(0, 1024, (n, 8))
+    t = rng.uniform(0, 1024, (n, 8))
+    H = oracle.solve("gpt", s, t)
+    for i in range(0, n, 7):
+        A = np.zeros((8, 8))
+        b = np.zeros(8)
+        for k in range(4):
+            x, y, u, v = s[i, 2 * k], s[i, 2 * k + 1], t[i, 2 * k], t[i, 2 * k + 1]
+            A[k] = [x, y, 1, 0, 0, 0, -x * u, -y * u]
+            A[k + 4] = [0, 0, 0, x, y, 1, -x * v, -y * v]
+            b[k], b[k + 4] = u, v
+        want = np.linalg.solve(A, b)
+        np.testing.assert_allclose(H[i, :8], want, rtol=1e-7, atol=1e-9 * np.abs(want).max())
+        assert H[i, 8] == 1.0
