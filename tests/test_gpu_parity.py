@@ -407,3 +407,40 @@ def test_gpt_lu_baseline_vs_oracle(orc, oracle, pkg, dev, layout):
     if layout == "soa":
         H = H.T
     _bits(orc, H, oracle.solve("gpt", s, t), f"gpt {layout}")
+
+
+# ------------------------------------------- directly against the reference itself
+@pytest.fixture(scope="module")
+def ref(orc):
+    if not orc.RefOracle.available():
+        pytest.skip("oracle/_ref (the compiled reference) not present")
+    return orc.RefOracle()
+
+
+@pytest.mark.parametrize("n", [1000, 1_000_000])
+def test_config1_gpu_equals_compiled_reference(orc, ref, pkg, dev, n):
+    """BASELINE configs[0]: ACA (and SKS, GE) batch vs the reference's OWN C++ solver
+    bodies (ACA_SKS.cpp / GE.cpp compiled from source into oracle/_ref), bit for bit."""
+    src = pkg.fill_uniform(n * 8, 11, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 11, n * 8, device=dev).view(n, 8)
+    s, t = src.cpu().numpy(), tar.cpu().numpy()
+    for algo in ("aca", "sks", "ge"):
+        _bits(orc, pkg.solve(algo, src, tar), ref.solve(algo, s, t), f"{algo} n={n} vs reference")
+    s64, t64 = s.astype(np.float64), t.astype(np.float64)
+    for algo in ("aca", "sks"):
+        _bits(orc, pkg.solve(algo, src.double(), tar.double()), ref.solve(algo, s64, t64),
+              f"{algo} f64 n={n} vs reference")
+
+
+@pytest.mark.slow
+def test_config2_full_batch_equals_compiled_reference(orc, ref, pkg, dev):
+    """BASELINE configs[1]/[2] at full size: the bench's exact 10 M inputs, GPU vs the
+    reference's own C++ (multi-threaded batch driver), every element."""
+    n = 10_000_000
+    src = pkg.fill_uniform(n * 8, 11, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 11, n * 8, device=dev).view(n, 8)
+    s, t = src.cpu().numpy(), tar.cpu().numpy()
+    H = np.empty((n, 9), np.float32)
+    for algo in ("aca", "sks"):
+        ref.time_batch(algo, s, t, H, 16, 1)  # threaded pass of the reference solver
+        _bits(orc, pkg.solve(algo, src, tar), H, f"{algo} 10M vs reference")
