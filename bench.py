@@ -110,6 +110,57 @@ def timed_region(d: Dist, fn, steps: int):
     return d.max(wall), e0.elapsed_time(e1) / steps
 
 
+def launch_stats(d: Dist, fn, launches: int = 200):
+    """Per-launch device-time distribution: a HIP event pair around every launch on the
+    launch stream (report the median beside the mean)."""
+    stream = torch.cuda.current_stream(d.dev)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(launches)]
+    torch.cuda.synchronize(d.dev)
+    for a, b in ev:
+        a.record(stream)
+        fn()
+        b.record(stream)
+    torch.cuda.synchronize(d.dev)
+    ts = np.sort(np.array([a.elapsed_time(b) for a, b in ev])) * 1e3
+    return {"launches": launches, "median_us": round(float(np.median(ts)), 2),
+            "p10_us": round(float(ts[launches // 10]), 2),
+            "p90_us": round(float(ts[(9 * launches) // 10]), 2),
+            "min_us": round(float(ts[0]), 2)}
+
+
+def reference_statistic(d: Dist, fn):
+    """cal_ACA's own statistic (GPU_Runtime Test.cu:1183-1200): time one launch,
+    loops = 10000 / ms (about 10 s of back-to-back launches), report the mean."""
+    _, ms1 = timed_region(d, fn, 1)
+    loops = max(1, int(10000.0 / max(ms1, 1e-3)))
+    _, ms = timed_region(d, fn, loops)
+    return {"loops": loops, "mean_us": round(ms * 1e3, 2)}
+
+
+def host_info():
+    model = None
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    tpc = None
+    try:  # "0,128" or "0-1" -> 2 hardware threads per core
+        with open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list") as f:
+            tpc = 0
+            for part in f.read().strip().split(","):
+                a, _, b = part.partition("-")
+                tpc += int(b or a) - int(a) + 1
+    except (OSError, ValueError):
+        pass
+    return {"cpu_model": model, "nproc": os.cpu_count(),
+            "usable_cpus": len(os.sched_getaffinity(0)), "threads_per_core": tpc}
+
+
 def graph_of(d: Dist, fn, calls: int):
     """HIP graph of `calls` back-to-back invocations (captured on a side stream)."""
     s = torch.cuda.Stream(d.dev)
@@ -159,6 +210,13 @@ def cpu_baseline(n_sample: int):
         t = engine.time_batch(algo, src, tar, H, threads, reps)
         out[algo] = n_sample * reps / t / 1e6
         out[algo + "_reps"] = reps
+    # methodology (ii)/(iii) of SURVEY 8(d): the streaming batch on 1, 2, 4 ... threads
+    sweep = {}
+    for t_count in sorted({min(1 << k, threads) for k in range(threads.bit_length() + 1)}):
+        t1 = engine.time_batch("aca", src, tar, H, t_count, 1)
+        reps = max(1, int(0.5 / max(t1, 1e-6)))
+        sweep[str(t_count)] = round(n_sample * reps / engine.time_batch(
+            "aca", src, tar, H, t_count, reps) / 1e6, 1)
     single = {}
     if kind == "reference":
         # the reference's own CPU methodology (main.cpp:87-92): one set, 10 M calls
@@ -170,6 +228,8 @@ def cpu_baseline(n_sample: int):
         "sample": (f"AoS f32 normalised batch of {n_sample} problems (seed {SEED}, U[0,1024)), "
                    f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, {threads} std::threads"),
         "single_core_same_points_us_per_H": single or None,
+        "aca_thread_sweep_M_per_s": sweep,
+        "host": host_info(),
     }
 
 
@@ -317,6 +377,7 @@ def main():
         run("aca")()
     wall, ms_launch = timed_region(d, run("aca"), args.steps)
     value = n_total * args.steps / wall / 1e6
+    per_launch = launch_stats(d, run("aca"), max(200, args.steps))
     achieved = n * bpp / (ms_launch * 1e-3) / 1e9
     traffic = pmc_traffic("aca_f32_aos_norm")
     line = {
@@ -346,9 +407,11 @@ def main():
             "algorithmic_bytes_per_launch": n * bpp,
             "launch_ms": round(ms_launch, 5),
         },
+        "launch_stats": per_launch,
     }
 
     if not args.no_extras:
+        line["reference_statistic"] = reference_statistic(d, run("aca"))
         for _ in range(args.warmup):
             run("sks")()
         wall_s, ms_s = timed_region(d, run("sks"), args.steps)

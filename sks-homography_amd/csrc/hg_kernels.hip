@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kBlock) void solve_generic(const T* __restrict__ sr
 // loads per lane (offsets 0 and 16 of the 48-B src record) issued before the DMA
 // wait.  H is written through the LDS-staged 16-B store.  Ragged/unaligned tiles
 // use per-lane loads and stores.
-template <int P, bool VEC, bool SCALAR_ARGS>
+template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -92,7 +92,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
         for (int j = 0; j < P; ++j) {
             float tr[12];
             __builtin_memcpy(tr, lds + (j * kWave + lane) * 48, 48);
-            tensor_aca_rect_solve(tr, mx[j], my[j], scale, div, h[j]);
+            tensor_aca_rect_solve<SQUARE>(tr, mx[j], my[j], scale, div, h[j]);
         }
         wave_lds_sync();
         store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
@@ -105,7 +105,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
             float tr[12];
 #pragma unroll
             for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
-            tensor_aca_rect_solve(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
+            tensor_aca_rect_solve<SQUARE>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
 #pragma unroll
             for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
         }
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
 // Compact TensorACA: corner (B,2) + offsets (B,4,2) -> H (B,3,3) = 8 + 32 + 36 B per
 // problem instead of the (B,3,4) tensors' 48 + 48 + 36.  Full tiles: both slabs by
 // LDS-DMA (P = 2: 1 KiB of corners + 4 KiB of offsets per wave), staged 16-B H stores.
-template <int P, bool VEC>
+template <int P, bool VEC, bool SQUARE>
 __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
     const float* __restrict__ corner, const float* __restrict__ offsets, float* __restrict__ H,
     int64_t B, float w, float h) {
@@ -176,7 +176,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
             __builtin_memcpy(c, lds + row * 8, 8);
             __builtin_memcpy(off, lds + kCorner + row * 32, 32);
             rect_target_from_offsets(c[0], c[1], w, h, off, tr);
-            tensor_aca_rect_solve(tr, c[0], c[1], w, div, hm[j]);
+            tensor_aca_rect_solve<SQUARE>(tr, c[0], c[1], w, div, hm[j]);
         }
         wave_lds_sync();
         store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), hm, lds, lane);
@@ -191,7 +191,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
             for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
             const float mx = corner[p * 2], my = corner[p * 2 + 1];
             rect_target_from_offsets(mx, my, w, h, off, tr);
-            tensor_aca_rect_solve(tr, mx, my, w, div, hm[j]);
+            tensor_aca_rect_solve<SQUARE>(tr, mx, my, w, div, hm[j]);
 #pragma unroll
             for (int k = 0; k < 9; ++k) H[p * 9 + k] = hm[j][k];
         }
@@ -318,6 +318,10 @@ int dispatch(const T* src, const T* tar, T* H, int64_t n, int layout, int flags,
     return launch_solver<ALGO, false>(src, tar, H, n, layout, s);
 }
 
+// The square specialisation (ACA_rect.m:28) is taken only where the ratio is known on
+// the host and is exactly 1, so dropping the multiply cannot change a bit.
+inline bool is_unit_ratio(float div) { return div == 1.0f; }
+
 template <bool SCALAR>
 int launch_rect(const float* src, const float* tar, float* H, int64_t B, const float* sp,
                 const float* dp, float sv, float dv, void* stream) {
@@ -328,7 +332,10 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
     constexpr int P = kRectP;
     const int64_t blocks = ceil_div(B, (int64_t)kBlock * P);
     if (blocks > 0x7fffffffLL) return kErrInvalid;
-    if (aligned16(src) && aligned16(tar) && aligned16(H))
+    if (SCALAR && is_unit_ratio(dv) && aligned16(src) && aligned16(tar) && aligned16(H))
+        tensor_aca_rect_kernel<P, true, true, true>
+            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    else if (aligned16(src) && aligned16(tar) && aligned16(H))
         tensor_aca_rect_kernel<P, true, SCALAR>
             <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
     else
@@ -414,12 +421,16 @@ int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* 
     constexpr int P = 2;
     const int64_t blocks = hg::ceil_div(B, (int64_t)hg::kBlock * P);
     if (blocks > 0x7fffffffLL) return hg::kErrInvalid;
-    if (hg::aligned16(corner) && hg::aligned16(offsets) && hg::aligned16(H))
-        hg::tensor_aca_offsets_kernel<P, true><<<(unsigned)blocks, hg::kBlock, 0, s>>>(
-            corner, offsets, H, B, width, height);
-    else  // unaligned views: per-lane loads and stores
-        hg::tensor_aca_offsets_kernel<P, false><<<(unsigned)blocks, hg::kBlock, 0, s>>>(
-            corner, offsets, H, B, width, height);
+    const bool vec = hg::aligned16(corner) && hg::aligned16(offsets) && hg::aligned16(H);
+    // width / height == 1 exactly iff the two are equal, finite and non-zero
+    const bool square = width == height && width != 0.f && std::isfinite(width);
+#define HG_OFFSETS(V, SQ)                                                                     \
+    hg::tensor_aca_offsets_kernel<P, V, SQ><<<(unsigned)blocks, hg::kBlock, 0, s>>>(          \
+        corner, offsets, H, B, width, height)
+    if (vec && square) HG_OFFSETS(true, true);
+    else if (vec) HG_OFFSETS(true, false);
+    else HG_OFFSETS(false, false);  // unaligned views: per-lane loads and stores
+#undef HG_OFFSETS
     return hg::launch_status();
 }
 

@@ -312,6 +312,9 @@ __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9
 // evaluated as ATen evaluates it: the cross product contracts one product per
 // component into an FMA, the 3-term sum runs left to right, every other op rounds
 // on its own.  tr = (3,4) target tensor rows {x, y, w} x cols {M, N, P, Q}.
+// SQUARE: the square specialisation of ACA_rect.m:28 (ratio 1, 44 FLOPs) -- drops the
+// multiply by div, which is exact when div == 1, so the bits are those of the general form.
+template <bool SQUARE = false>
 __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], float mx, float my,
                                                       float scale, float div, float (&h)[9]) {
     const float ax = tr[5] - tr[4], ay = tr[6] - tr[4], az = tr[7] - tr[4];  // d[1]: MN, MP, MQ (y)
@@ -324,7 +327,7 @@ __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], flo
     for (int r = 0; r < 3; ++r) {
         const float b = sum * tr[4 * r];
         const float h0 = tr[4 * r + 1] * c0 - b;
-        const float h1 = div * (tr[4 * r + 2] * c1 - b);
+        const float h1 = SQUARE ? tr[4 * r + 2] * c1 - b : div * (tr[4 * r + 2] * c1 - b);
         h[3 * r + 0] = h0;
         h[3 * r + 1] = h1;
         h[3 * r + 2] = (scale * b - mx * h0) - my * h1;

@@ -79,3 +79,29 @@ def test_offsets_autograd_vs_float64(pkg, dev):
 
     assert rel(offsets.grad, o64.grad) < 1e-5
     assert rel(corner.grad, c64.grad) < 1e-4
+
+
+@pytest.mark.parametrize("wh", [(128.0, 128.0), (64.0, 64.0), (0.0, 0.0), (np.inf, np.inf),
+                                (96.0, 64.0)])
+def test_square_specialisation_same_bits(orc, oracle, pkg, dev, wh):
+    """ACA_rect.m:28's square case (ratio 1, no multiply by div) is dispatched on the host
+    when width == height (compact form) or div == 1.0 (host-scalar rect form); it must give
+    the general form's bits, and 0/0 or inf/inf ratios (NaN) must stay on the general path."""
+    w, h = wh
+    B = 4096 + 37
+    g = torch.Generator(device=dev).manual_seed(5)
+    corner = (torch.rand(B, 2, device=dev, generator=g) * 20 + 10).floor()
+    offsets = (torch.rand(B, 4, 2, device=dev, generator=g) * 32).floor()
+    H = pkg.tensor_aca_offsets(corner, offsets, w, h)
+    src, tar = _build_h(corner.cpu().numpy(), offsets.cpu().numpy(), w, h)
+    with np.errstate(invalid="ignore"):
+        div = float(np.float32(w) / np.float32(h))
+    want = oracle.tensor_aca_rect(src, tar, w, div)
+    assert orc.same_bits(H.cpu().numpy(), want).all()
+    # rect form: host scalars (square path when div == 1) vs device scalars (general path)
+    s_d, t_d = torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev)
+    Hh = pkg.tensor_aca_rect(s_d, t_d, w, div)
+    Hd = pkg.tensor_aca_rect(s_d, t_d, torch.tensor([w], device=dev),
+                             torch.tensor([div], device=dev))
+    assert orc.same_bits(Hh.cpu().numpy(), Hd.cpu().numpy()).all()
+    assert orc.same_bits(Hh.cpu().numpy(), want).all()
