@@ -41,7 +41,8 @@ def parse():
     ap.add_argument("--rect-batch", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-extras", action="store_true", help="ACA headline only")
-    ap.add_argument("--gather", action="store_true", help="also time an RCCL gather of H")
+    ap.add_argument("--no-gather", action="store_true",
+                    help="N>1: skip the timed gather of every H block to rank 0")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
@@ -358,6 +359,35 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     }
 
 
+def gather_section(d: Dist, pkg, H, n: int, n_total: int, step_ms: float):
+    """SURVEY 8(e)'s second number: every rank's H block gathered to rank 0 (paired
+    send/recv; RCCL over xGMI, bound by rank 0's ingress), outside the timed steps.
+    Rank 0 then re-solves a slice of the last rank's block from regenerated inputs and
+    checks the gathered bits.  Over gloo (one-GPU rehearsal) the blocks go via the host."""
+    blk = H if d.backend == "nccl" else H.cpu()
+    small = blk[:1024].contiguous()
+    pkg.gather_blocks(small, 1024 * d.world, d.world, d.rank)  # open the p2p connections
+    torch.cuda.synchronize(d.dev)
+    d.barrier()
+    t0 = time.perf_counter()
+    full = pkg.gather_blocks(blk, n_total, d.world, d.rank)
+    torch.cuda.synchronize(d.dev)
+    d.barrier()
+    secs = d.max(time.perf_counter() - t0)
+    out = {"gather_to_rank0_ms": round(secs * 1e3, 3), "gathered_bytes": n_total * 36,
+           "rank0_ingress_gbps": round((n_total - n) * 36 / secs / 1e9, 1),
+           "end_to_end_M_homographies_per_s": round(n_total / (secs + step_ms * 1e-3) / 1e6, 1)}
+    if d.rank == 0:
+        lo, m = (d.world - 1) * n, min(n, 1 << 20)
+        s = pkg.fill_uniform(m * 8, SEED, lo * 8, device=d.dev).view(m, 8)
+        t = pkg.fill_uniform(m * 8, SEED, (n_total + lo) * 8, device=d.dev).view(m, 8)
+        want = pkg.solve("aca", s, t, normalize=True)
+        got = full[lo:lo + m].to(d.dev)
+        out["gather_verified"] = bool(torch.equal(want.view(torch.int32), got.view(torch.int32)))
+    del full
+    return out
+
+
 def main():
     args = parse()
     d = Dist(args.dist_backend)
@@ -519,14 +549,9 @@ def main():
                                "achieved_gbps": round(n * 200 / (ms64 * 1e-3) / 1e9, 1)}
         del s64, t64, H64
 
-    if args.gather and d.world > 1:
-        d.barrier()
-        torch.cuda.synchronize(d.dev)
-        t0 = time.perf_counter()
-        pkg.gather_blocks(H, n_total, d.world, d.rank)
-        torch.cuda.synchronize(d.dev)
-        d.barrier()
-        line["gather_to_rank0_ms"] = round(d.max(time.perf_counter() - t0) * 1e3, 3)
+    if d.world > 1 and not args.no_gather:
+        run("aca")()
+        line["gather"] = gather_section(d, pkg, H, n, n_total, wall / args.steps * 1e3)
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(min(n, 10_000_000))
