@@ -31,6 +31,11 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
 
 /* RANSAC scorer variants: 0 = one hypothesis per lane, 1/2 = two per lane packed
  * (inner unroll 1/4).  Same counts as hg_ransac_score_f32. */
+/* TensorACA tile sweep: 0-2 rect form P = 1/2/4 (a = scale, b = div); 3-5 compact form
+ * P = 1/2/4 (src = corner, tar = offsets, a = width, b = height). */
+int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
+                 float b, void* stream);
+
 int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream);

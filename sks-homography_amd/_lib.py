@@ -11,6 +11,7 @@ import threading
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_amd.so")
+TORCH_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_torch.so")
 
 HG_LAYOUT_AOS = 0
 HG_LAYOUT_SOA = 1

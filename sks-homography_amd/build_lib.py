@@ -19,6 +19,7 @@ CSRC = os.path.join(HERE, "csrc")
 BUILD = os.path.join(HERE, "build")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsks_homography_amd.so")
+TORCH_LIB = os.path.join(LIB_DIR, "libsks_homography_torch.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
 SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_tune.hip", "hg_sks_api.cpp"]
@@ -66,7 +67,33 @@ def build(verbose: bool = False, force: bool = False) -> str:
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
+    build_torch_ops(verbose, force, headers)
     return LIB
+
+
+def build_torch_ops(verbose: bool = False, force: bool = False, headers=()) -> str:
+    """lib/libsks_homography_torch.so: the native torch.ops.sks_amd operators
+    (csrc/hg_torch_ops.cpp), host C++ against torch's headers, linked to the product
+    library (found next to it via $ORIGIN)."""
+    import torch
+
+    src = os.path.join(CSRC, "hg_torch_ops.cpp")
+    if not force and not _stale(TORCH_LIB, [src, LIB, *headers]):
+        return TORCH_LIB
+    tdir = os.path.dirname(torch.__file__)
+    abi = int(torch._C._GLIBCXX_USE_CXX11_ABI)
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", TORCH_LIB, src,
+           "-D__HIP_PLATFORM_AMD__=1", "-DUSE_ROCM=1", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           "-DTORCH_API_INCLUDE_EXTENSION_H", "-DTORCH_EXTENSION_NAME=sks_homography_torch",
+           f"-I{os.path.join(ROOT, 'include')}", f"-I{os.path.join(tdir, 'include')}",
+           f"-I{os.path.join(tdir, 'include', 'torch', 'csrc', 'api', 'include')}",
+           "-I/opt/rocm/include", f"-L{os.path.join(tdir, 'lib')}", f"-L{LIB_DIR}",
+           "-lsks_homography_amd", "-lc10", "-lc10_hip", "-ltorch", "-ltorch_cpu", "-ltorch_hip",
+           "-Wl,-rpath,$ORIGIN", f"-Wl,-rpath,{os.path.join(tdir, 'lib')}"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return TORCH_LIB
 
 
 if __name__ == "__main__":

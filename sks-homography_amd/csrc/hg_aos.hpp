@@ -102,14 +102,22 @@ __device__ __forceinline__ void slabs_to_lds(const char* const (&g)[NS], char* c
 }
 
 // Issue-only LDS-DMA of one kBytes slab (no wait): for slabs of different sizes,
-// issue each, then call dma_wait_sync() once.
+// issue each, then call dma_wait_sync() once.  A last piece under 1 KiB is issued by
+// the lanes it covers only.
 template <int kBytes, bool NT>
 __device__ __forceinline__ void dma_slab_issue(const char* __restrict__ g, char* l, int lane) {
-    static_assert(kBytes % (16 * kWave) == 0, "slab must be whole 1 KiB pieces");
+    static_assert(kBytes % 16 == 0, "slab must be whole 16-B granules");
+    constexpr int kWhole = kBytes / (16 * kWave), kTail = (kBytes % (16 * kWave)) / 16;
 #pragma unroll
-    for (int c = 0; c < kBytes / (16 * kWave); ++c)
+    for (int c = 0; c < kWhole; ++c)
         __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + 16 * (c * kWave + lane)),
                                          (lds_ptr_t)(l + 16 * c * kWave), 16, 0, NT ? 2 : 0);
+    if constexpr (kTail > 0) {
+        if (lane < kTail)
+            __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g + 16 * (kWhole * kWave + lane)),
+                                             (lds_ptr_t)(l + 16 * kWhole * kWave), 16, 0,
+                                             NT ? 2 : 0);
+    }
 }
 
 // The same issue through inline asm (cdna_hip_programming.md section 5.7): hipcc then

@@ -1,0 +1,195 @@
+// hg_rect.hpp -- TensorACA kernels (rect (B,3,4) form, compact corner+offsets form,
+// and their backward passes).  Included by hg_kernels.hip
+// (the C ABI) and hg_tune.hip (the variant sweep).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "hg_aos.hpp"
+#include "hg_solvers.hpp"
+
+namespace hg {
+
+// ---------------------------------------------------------------------------
+// TensorACA rect: src/tar (B,3,4) f32, H (B,3,3) f32, unnormalised.
+// A wave owns 64*P problems.  Full tiles (VEC: 16-B aligned tensors): the wave's
+// contiguous tar slab (64*P*48 B) lands in LDS by LDS-DMA, each lane then reads its
+// 48-B record with three ds_read_b128; M's x and y come from src with two dword
+// loads per lane (offsets 0 and 16 of the 48-B src record) issued before the DMA
+// wait.  H is written through the LDS-staged 16-B store.  Ragged/unaligned tiles
+// use per-lane loads and stores.
+template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float scale_v, float div_v) {
+    constexpr int kTile = kWave * P;
+    constexpr int kSlab = kTile * 48;
+    constexpr int kLds = kSlab > kTile * 36 ? kSlab : kTile * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][VEC ? kLds : 16];
+
+    const float scale = SCALAR_ARGS ? scale_v : scale_p[0];
+    const float div = SCALAR_ARGS ? div_v : div_p[0];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= B) return;
+    const bool full = VEC && base + kTile <= B;
+    char* lds = smem[wave];
+
+    float h[P][9];
+    if (full) {
+        float mx[P], my[P];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = base + j * kWave + lane;
+            mx[j] = __builtin_nontemporal_load(src + p * 12 + 0);
+            my[j] = __builtin_nontemporal_load(src + p * 12 + 4);
+        }
+        const char* const g[1] = {reinterpret_cast<const char*>(tar + base * 12)};
+        char* const l[1] = {lds};
+        slabs_to_lds<kSlab, 1, true, true>(g, l, lane);
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            float tr[12];
+            __builtin_memcpy(tr, lds + (j * kWave + lane) * 48, 48);
+            tensor_aca_rect_solve<SQUARE>(tr, mx[j], my[j], scale, div, h[j]);
+        }
+        wave_lds_sync();
+        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        if (p < B) {
+            float tr[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+            tensor_aca_rect_solve<SQUARE>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// TensorACA rect backward: one lane per problem, grid-stride.  Writes dL/dtar
+// (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and the
+// per-problem (dL/dscale, dL/ddiv) partials (B,2) that the caller reduces.
+template <bool WANT_SRC, bool WANT_SD>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float* __restrict__ gsrc, float* __restrict__ gtar, float* __restrict__ gsd) {
+    const float scale = scale_p[0], div = div_p[0];
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float tr[12], g[9], gt[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        float gmx, gmy, gscale, gdiv;
+        tensor_aca_rect_grad(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx, gmy,
+                             gscale, gdiv);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
+        if constexpr (WANT_SRC) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
+        }
+        if constexpr (WANT_SD) {
+            gsd[p * 2 + 0] = gscale;
+            gsd[p * 2 + 1] = gdiv;
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Compact TensorACA: corner (B,2) + offsets (B,4,2) -> H (B,3,3) = 8 + 32 + 36 B per
+// problem instead of the (B,3,4) tensors' 48 + 48 + 36.  Full tiles: both slabs by
+// LDS-DMA (P = 1: 512 B of corners + 2 KiB of offsets per wave), staged 16-B H stores.
+template <int P, bool VEC, bool SQUARE>
+__global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
+    const float* __restrict__ corner, const float* __restrict__ offsets, float* __restrict__ H,
+    int64_t B, float w, float h) {
+    constexpr int kTile = kWave * P;
+    constexpr int kCorner = kTile * 8, kOff = kTile * 32;
+    constexpr int kLds = kCorner + kOff > kTile * 36 ? kCorner + kOff : kTile * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][VEC ? kLds : 16];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= B) return;
+    const float div = w / h;
+    char* lds = smem[wave];
+    float hm[P][9];
+    if (VEC && base + kTile <= B) {
+        dma_slab_issue<kCorner, true>(reinterpret_cast<const char*>(corner + base * 2), lds, lane);
+        dma_slab_issue<kOff, true>(reinterpret_cast<const char*>(offsets + base * 8),
+                                   lds + kCorner, lane);
+        dma_wait_sync();
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int row = j * kWave + lane;
+            float c[2], off[8], tr[12];
+            __builtin_memcpy(c, lds + row * 8, 8);
+            __builtin_memcpy(off, lds + kCorner + row * 32, 32);
+            rect_target_from_offsets(c[0], c[1], w, h, off, tr);
+            tensor_aca_rect_solve<SQUARE>(tr, c[0], c[1], w, div, hm[j]);
+        }
+        wave_lds_sync();
+        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), hm, lds, lane);
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < P; ++j) {
+        const int64_t p = base + j * kWave + lane;
+        if (p < B) {
+            float off[8], tr[12];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
+            const float mx = corner[p * 2], my = corner[p * 2 + 1];
+            rect_target_from_offsets(mx, my, w, h, off, tr);
+            tensor_aca_rect_solve<SQUARE>(tr, mx, my, w, div, hm[j]);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[p * 9 + k] = hm[j][k];
+        }
+    }
+}
+
+// Backward of the compact form: dL/doffsets (B,4,2) and optionally dL/dcorner (B,2).
+template <bool WANT_CORNER>
+__global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
+    const float* __restrict__ corner, const float* __restrict__ offsets,
+    const float* __restrict__ gH, int64_t B, float w, float h, float* __restrict__ g_off,
+    float* __restrict__ g_corner) {
+    const float div = w / h;
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float off[8], tr[12], g[9], gt[12];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        const float mx = corner[p * 2], my = corner[p * 2 + 1];
+        rect_target_from_offsets(mx, my, w, h, off, tr);
+        float gmx, gmy, gsc, gdv;
+        tensor_aca_rect_grad(tr, mx, my, w, div, g, gt, gmx, gmy, gsc, gdv);
+        // tar[0][j] = x_j + off[j].x, tar[1][j] = y_j + off[j].y
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            g_off[p * 8 + 2 * j] = gt[j];
+            g_off[p * 8 + 2 * j + 1] = gt[4 + j];
+        }
+        if constexpr (WANT_CORNER) {
+            g_corner[p * 2] = gmx + (((gt[0] + gt[1]) + gt[2]) + gt[3]);
+            g_corner[p * 2 + 1] = gmy + (((gt[4] + gt[5]) + gt[6]) + gt[7]);
+        }
+    }
+}
+
+}  // namespace hg

@@ -1,0 +1,386 @@
+// hg_torch_ops.cpp -- the PyTorch-ROCm operators of SURVEY.md 8(b).3, native.
+//
+// torch.ops.sks_amd.{aca, sks, tensor_aca_rect, tensor_aca_offsets} (+ .out overloads and
+// the backward ops) are registered here with the dispatcher: CUDA (= HIP on ROCm) kernels
+// that call the C ABI (include/sks_homography.h) on torch's current stream, Meta kernels
+// for shape propagation, and C++ autograd for the two TensorACA forms.  Compared with a
+// Python custom op this keeps the per-call host cost to one dispatcher hop plus the
+// launch, which is what bounds the reference's B = 64 K case (Modules_Runtime_Test.py:
+// 286-309 is launch-bound).  There is no CPU kernel: CPU tensors raise.
+#include <ATen/ATen.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
+#include <torch/autograd.h>
+#include <torch/library.h>
+
+#include "sks_homography.h"
+
+namespace {
+
+using torch::autograd::AutogradContext;
+using torch::autograd::variable_list;
+
+void* stream_of(const at::Tensor& t) {
+    return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
+}
+
+void hip_ok(int rc, const char* fn) {
+    TORCH_CHECK(rc == 0, fn, " failed with hipError_t ", rc);
+}
+
+void on_gpu(const at::Tensor& t, const char* name, const at::Device& dev) {
+    TORCH_CHECK(t.is_cuda(), "sks_amd: ", name, " must be a GPU tensor (no CPU path), got ",
+                t.device());
+    TORCH_CHECK(t.device() == dev, "sks_amd: ", name, " is on ", t.device(), ", expected ", dev);
+    TORCH_CHECK(t.scalar_type() == at::kFloat, "sks_amd: ", name, " must be float32, got ",
+                t.scalar_type());
+}
+
+void check_rect(const at::Tensor& src, const at::Tensor& tar) {
+    for (const auto* p : {&src, &tar}) {
+        TORCH_CHECK(p->dim() == 3 && p->size(1) == 3 && p->size(2) == 4,
+                    "sks_amd::tensor_aca_rect: src/tar must be (B,3,4), got ", p->sizes());
+    }
+    TORCH_CHECK(src.size(0) == tar.size(0), "sks_amd::tensor_aca_rect: batch sizes differ");
+}
+
+void check_out(const at::Tensor& out, at::IntArrayRef shape, const at::Device& dev) {
+    on_gpu(out, "out", dev);
+    TORCH_CHECK(out.sizes() == shape && out.is_contiguous(), "sks_amd: out must be a contiguous ",
+                shape, " tensor, got ", out.sizes());
+}
+
+// ------------------------------------------------------------------ TensorACA rect
+at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& scale_,
+                     const at::Tensor& div_, at::Tensor& out) {
+    const at::Device dev = tar_.device();
+    on_gpu(src_, "src", dev);
+    on_gpu(tar_, "tar", dev);
+    on_gpu(scale_, "scale", dev);
+    on_gpu(div_, "div", dev);
+    check_rect(src_, tar_);
+    TORCH_CHECK(scale_.numel() >= 1 && div_.numel() >= 1, "sks_amd: scale/div must be non-empty");
+    const int64_t B = tar_.size(0);
+    check_out(out, {B, 3, 3}, dev);
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
+    const at::Tensor scale = scale_.contiguous(), div = div_.contiguous();
+    const c10::DeviceGuard guard(dev);
+    hip_ok(hg_tensor_aca_rect_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                  out.data_ptr<float>(), B, scale.data_ptr<float>(),
+                                  div.data_ptr<float>(), stream_of(tar)),
+           "hg_tensor_aca_rect_f32");
+    return out;
+}
+
+at::Tensor rect(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
+                const at::Tensor& div) {
+    at::Tensor out = at::empty({tar.size(0), 3, 3}, tar.options());
+    rect_out(src, tar, scale, div, out);
+    return out;
+}
+
+at::Tensor& rect_scalar_out(const at::Tensor& src_, const at::Tensor& tar_, double scale,
+                            double div, at::Tensor& out) {
+    const at::Device dev = tar_.device();
+    on_gpu(src_, "src", dev);
+    on_gpu(tar_, "tar", dev);
+    check_rect(src_, tar_);
+    const int64_t B = tar_.size(0);
+    check_out(out, {B, 3, 3}, dev);
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
+    const c10::DeviceGuard guard(dev);
+    hip_ok(hg_tensor_aca_rect_f32_hostscalar(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                             out.data_ptr<float>(), B, (float)scale, (float)div,
+                                             stream_of(tar)),
+           "hg_tensor_aca_rect_f32_hostscalar");
+    return out;
+}
+
+at::Tensor rect_scalar(const at::Tensor& src, const at::Tensor& tar, double scale, double div) {
+    at::Tensor out = at::empty({tar.size(0), 3, 3}, tar.options());
+    rect_scalar_out(src, tar, scale, div, out);
+    return out;
+}
+
+// (grad_src (B,3,4) or (0,), grad_tar (B,3,4), [dscale, ddiv] (2,) or (0,))
+std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
+    const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& grad_,
+    const at::Tensor& scale_, const at::Tensor& div_, bool need_src, bool need_scale_div) {
+    const at::Device dev = tar_.device();
+    on_gpu(src_, "src", dev);
+    on_gpu(tar_, "tar", dev);
+    on_gpu(grad_, "grad", dev);
+    on_gpu(scale_, "scale", dev);
+    on_gpu(div_, "div", dev);
+    check_rect(src_, tar_);
+    const int64_t B = tar_.size(0);
+    TORCH_CHECK(grad_.dim() == 3 && grad_.size(0) == B && grad_.size(1) == 3 && grad_.size(2) == 3,
+                "sks_amd::tensor_aca_rect_backward: grad must be (B,3,3)");
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous(), grad = grad_.contiguous();
+    const at::Tensor scale = scale_.contiguous(), div = div_.contiguous();
+    at::Tensor g_tar = at::empty({B, 3, 4}, tar.options());
+    at::Tensor g_src = need_src ? at::empty({B, 3, 4}, tar.options()) : at::empty({0}, tar.options());
+    at::Tensor part = need_scale_div ? at::empty({B, 2}, tar.options()) : at::empty({0}, tar.options());
+    const c10::DeviceGuard guard(dev);
+    hip_ok(hg_tensor_aca_rect_backward_f32(
+               src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+               scale.data_ptr<float>(), div.data_ptr<float>(),
+               need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
+               need_scale_div && B ? part.data_ptr<float>() : nullptr, stream_of(tar)),
+           "hg_tensor_aca_rect_backward_f32");
+    // per-problem partials summed on the device, deterministically
+    at::Tensor g_sd = need_scale_div ? part.sum(0) : part;
+    return {g_src, g_tar, g_sd};
+}
+
+// ------------------------------------------------------------------ compact offsets form
+void check_offsets(const at::Tensor& corner, const at::Tensor& offsets) {
+    TORCH_CHECK((offsets.dim() == 3 && offsets.size(1) == 4 && offsets.size(2) == 2) ||
+                    (offsets.dim() == 2 && offsets.size(1) == 8),
+                "sks_amd::tensor_aca_offsets: offsets must be (B,4,2) or (B,8), got ",
+                offsets.sizes());
+    TORCH_CHECK(corner.dim() == 2 && corner.size(0) == offsets.size(0) && corner.size(1) == 2,
+                "sks_amd::tensor_aca_offsets: corner must be (B,2), got ", corner.sizes());
+}
+
+at::Tensor& offsets_out(const at::Tensor& corner_, const at::Tensor& offsets_, double width,
+                        double height, at::Tensor& out) {
+    const at::Device dev = offsets_.device();
+    on_gpu(corner_, "corner", dev);
+    on_gpu(offsets_, "offsets", dev);
+    check_offsets(corner_, offsets_);
+    const int64_t B = offsets_.size(0);
+    check_out(out, {B, 3, 3}, dev);
+    const at::Tensor corner = corner_.contiguous(), offsets = offsets_.contiguous();
+    const c10::DeviceGuard guard(dev);
+    hip_ok(hg_tensor_aca_offsets_f32(corner.data_ptr<float>(), offsets.data_ptr<float>(),
+                                     out.data_ptr<float>(), B, (float)width, (float)height,
+                                     stream_of(offsets)),
+           "hg_tensor_aca_offsets_f32");
+    return out;
+}
+
+at::Tensor offsets_fwd(const at::Tensor& corner, const at::Tensor& offsets, double width,
+                       double height) {
+    at::Tensor out = at::empty({offsets.size(0), 3, 3}, offsets.options());
+    offsets_out(corner, offsets, width, height, out);
+    return out;
+}
+
+std::tuple<at::Tensor, at::Tensor> offsets_backward(const at::Tensor& corner_,
+                                                    const at::Tensor& offsets_,
+                                                    const at::Tensor& grad_, double width,
+                                                    double height, bool need_corner) {
+    const at::Device dev = offsets_.device();
+    on_gpu(corner_, "corner", dev);
+    on_gpu(offsets_, "offsets", dev);
+    on_gpu(grad_, "grad", dev);
+    check_offsets(corner_, offsets_);
+    const int64_t B = offsets_.size(0);
+    TORCH_CHECK(grad_.numel() == B * 9, "sks_amd::tensor_aca_offsets_backward: grad must be (B,3,3)");
+    const at::Tensor corner = corner_.contiguous(), offsets = offsets_.contiguous();
+    const at::Tensor grad = grad_.contiguous();
+    at::Tensor g_off = at::empty(offsets.sizes(), offsets.options());
+    at::Tensor g_cor = need_corner ? at::empty({B, 2}, offsets.options())
+                                   : at::empty({0}, offsets.options());
+    const c10::DeviceGuard guard(dev);
+    hip_ok(hg_tensor_aca_offsets_backward_f32(
+               corner.data_ptr<float>(), offsets.data_ptr<float>(), grad.data_ptr<float>(), B,
+               (float)width, (float)height, g_off.data_ptr<float>(),
+               need_corner && B ? g_cor.data_ptr<float>() : nullptr, stream_of(offsets)),
+           "hg_tensor_aca_offsets_backward_f32");
+    return {g_off, g_cor};
+}
+
+// ------------------------------------------------------------------ general-quad ACA / SKS
+// ACA_vanilla's layout (Modules_Runtime_Test.py:312): (B,4,2) or (B,8) -> (B,3,3).
+template <int ALGO>
+at::Tensor& quad_out(const at::Tensor& src_, const at::Tensor& tar_, bool normalize,
+                     at::Tensor& out) {
+    const at::Device dev = tar_.device();
+    on_gpu(src_, "src", dev);
+    on_gpu(tar_, "tar", dev);
+    for (const auto* p : {&src_, &tar_}) {
+        TORCH_CHECK((p->dim() == 3 && p->size(1) == 4 && p->size(2) == 2) ||
+                        (p->dim() == 2 && p->size(1) == 8),
+                    "sks_amd::aca/sks: src/tar must be (B,4,2) or (B,8), got ", p->sizes());
+    }
+    TORCH_CHECK(src_.size(0) == tar_.size(0), "sks_amd::aca/sks: batch sizes differ");
+    const int64_t B = tar_.size(0);
+    check_out(out, {B, 3, 3}, dev);
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
+    const c10::DeviceGuard guard(dev);
+    auto fn = ALGO == 0 ? hg_aca_f32 : hg_sks_f32;
+    hip_ok(fn(src.data_ptr<float>(), tar.data_ptr<float>(), out.data_ptr<float>(), B,
+              HG_LAYOUT_AOS, normalize ? HG_FLAG_NORMALIZE : 0, stream_of(tar)),
+           ALGO == 0 ? "hg_aca_f32" : "hg_sks_f32");
+    return out;
+}
+
+template <int ALGO>
+at::Tensor quad(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
+    at::Tensor out = at::empty({tar.size(0), 3, 3}, tar.options());
+    quad_out<ALGO>(src, tar, normalize, out);
+    return out;
+}
+
+// ------------------------------------------------------------------ Meta (shapes only)
+at::Tensor meta_b33(const at::Tensor& t) { return at::empty({t.size(0), 3, 3}, t.options()); }
+
+// ------------------------------------------------------------------ autograd
+at::Tensor call_rect(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
+                     const at::Tensor& div) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::tensor_aca_rect", "")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&,
+                                           const at::Tensor&, const at::Tensor&)>();
+    return op.call(src, tar, scale, div);
+}
+
+class RectFunction : public torch::autograd::Function<RectFunction> {
+   public:
+    static at::Tensor forward(AutogradContext* ctx, const at::Tensor& src, const at::Tensor& tar,
+                              const at::Tensor& scale, const at::Tensor& div) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        ctx->save_for_backward({src, tar, scale, div});
+        return call_rect(src, tar, scale, div);
+    }
+
+    static variable_list backward(AutogradContext* ctx, variable_list grads) {
+        const auto saved = ctx->get_saved_variables();
+        const at::Tensor &src = saved[0], &tar = saved[1], &scale = saved[2], &div = saved[3];
+        const bool need_src = ctx->needs_input_grad(0);
+        const bool need_sd = ctx->needs_input_grad(2) || ctx->needs_input_grad(3);
+        auto [g_src, g_tar, g_sd] =
+            rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd);
+        at::Tensor none;
+        return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none,
+                ctx->needs_input_grad(2) ? g_sd.slice(0, 0, 1).reshape(scale.sizes()) : none,
+                ctx->needs_input_grad(3) ? g_sd.slice(0, 1, 2).reshape(div.sizes()) : none};
+    }
+};
+
+bool any_requires_grad(std::initializer_list<const at::Tensor*> ts) {
+    if (!at::GradMode::is_enabled()) return false;
+    for (const at::Tensor* t : ts)
+        if (t->requires_grad()) return true;
+    return false;
+}
+
+at::Tensor rect_autograd(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
+                         const at::Tensor& div) {
+    if (!any_requires_grad({&src, &tar, &scale, &div})) {  // inference: no graph node
+        at::AutoDispatchBelowADInplaceOrView below;
+        return call_rect(src, tar, scale, div);
+    }
+    return RectFunction::apply(src, tar, scale, div);
+}
+
+at::Tensor call_offsets(const at::Tensor& corner, const at::Tensor& offsets, double w, double h) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::tensor_aca_offsets", "")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&, double, double)>();
+    return op.call(corner, offsets, w, h);
+}
+
+class OffsetsFunction : public torch::autograd::Function<OffsetsFunction> {
+   public:
+    static at::Tensor forward(AutogradContext* ctx, const at::Tensor& corner,
+                              const at::Tensor& offsets, double w, double h) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        ctx->save_for_backward({corner, offsets});
+        ctx->saved_data["w"] = w;
+        ctx->saved_data["h"] = h;
+        return call_offsets(corner, offsets, w, h);
+    }
+
+    static variable_list backward(AutogradContext* ctx, variable_list grads) {
+        const auto saved = ctx->get_saved_variables();
+        const bool need_c = ctx->needs_input_grad(0);
+        auto [g_off, g_cor] =
+            offsets_backward(saved[0], saved[1], grads[0].contiguous(),
+                             ctx->saved_data["w"].toDouble(), ctx->saved_data["h"].toDouble(),
+                             need_c);
+        at::Tensor none;
+        return {need_c ? g_cor : none, ctx->needs_input_grad(1) ? g_off : none, none, none};
+    }
+};
+
+at::Tensor offsets_autograd(const at::Tensor& corner, const at::Tensor& offsets, double w,
+                            double h) {
+    if (!any_requires_grad({&corner, &offsets})) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        return call_offsets(corner, offsets, w, h);
+    }
+    return OffsetsFunction::apply(corner, offsets, w, h);
+}
+
+}  // namespace
+
+TORCH_LIBRARY(sks_amd, m) {
+    m.def("aca(Tensor src, Tensor tar, bool normalize=False) -> Tensor");
+    m.def("aca.out(Tensor src, Tensor tar, bool normalize=False, *, Tensor(a!) out) -> Tensor(a!)");
+    m.def("sks(Tensor src, Tensor tar, bool normalize=False) -> Tensor");
+    m.def("sks.out(Tensor src, Tensor tar, bool normalize=False, *, Tensor(a!) out) -> Tensor(a!)");
+    m.def("tensor_aca_rect(Tensor src, Tensor tar, Tensor scale, Tensor div) -> Tensor");
+    m.def("tensor_aca_rect.out(Tensor src, Tensor tar, Tensor scale, Tensor div, *, "
+          "Tensor(a!) out) -> Tensor(a!)");
+    m.def("tensor_aca_rect.scalar(Tensor src, Tensor tar, float scale, float div) -> Tensor");
+    m.def("tensor_aca_rect.scalar_out(Tensor src, Tensor tar, float scale, float div, *, "
+          "Tensor(a!) out) -> Tensor(a!)");
+    m.def("tensor_aca_rect_backward(Tensor src, Tensor tar, Tensor grad, Tensor scale, "
+          "Tensor div, bool need_src, bool need_scale_div) -> (Tensor, Tensor, Tensor)");
+    m.def("tensor_aca_offsets(Tensor corner, Tensor offsets, float width, float height) -> Tensor");
+    m.def("tensor_aca_offsets.out(Tensor corner, Tensor offsets, float width, float height, *, "
+          "Tensor(a!) out) -> Tensor(a!)");
+    m.def("tensor_aca_offsets_backward(Tensor corner, Tensor offsets, Tensor grad, float width, "
+          "float height, bool need_corner) -> (Tensor, Tensor)");
+}
+
+TORCH_LIBRARY_IMPL(sks_amd, CUDA, m) {
+    m.impl("aca", quad<0>);
+    m.impl("aca.out", quad_out<0>);
+    m.impl("sks", quad<1>);
+    m.impl("sks.out", quad_out<1>);
+    m.impl("tensor_aca_rect", rect);
+    m.impl("tensor_aca_rect.out", rect_out);
+    m.impl("tensor_aca_rect.scalar", rect_scalar);
+    m.impl("tensor_aca_rect.scalar_out", rect_scalar_out);
+    m.impl("tensor_aca_rect_backward", rect_backward);
+    m.impl("tensor_aca_offsets", offsets_fwd);
+    m.impl("tensor_aca_offsets.out", offsets_out);
+    m.impl("tensor_aca_offsets_backward", offsets_backward);
+}
+
+TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
+    m.impl("aca", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
+    m.impl("sks", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
+    m.impl("tensor_aca_rect", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&,
+                                 const at::Tensor&) { return meta_b33(t); });
+    m.impl("tensor_aca_rect.scalar",
+           [](const at::Tensor& s, const at::Tensor& t, double, double) { return meta_b33(t); });
+    m.impl("tensor_aca_offsets", [](const at::Tensor& c, const at::Tensor& o, double, double) {
+        return meta_b33(o);
+    });
+    m.impl("tensor_aca_rect_backward",
+           [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&, const at::Tensor&,
+              const at::Tensor&, bool need_src, bool need_sd) {
+               const int64_t B = t.size(0);
+               return std::make_tuple(need_src ? at::empty({B, 3, 4}, t.options())
+                                               : at::empty({0}, t.options()),
+                                      at::empty({B, 3, 4}, t.options()),
+                                      at::empty({need_sd ? 2 : 0}, t.options()));
+           });
+    m.impl("tensor_aca_offsets_backward",
+           [](const at::Tensor& c, const at::Tensor& o, const at::Tensor&, double, double,
+              bool need_c) {
+               return std::make_tuple(at::empty(o.sizes(), o.options()),
+                                      need_c ? at::empty({o.size(0), 2}, o.options())
+                                             : at::empty({0}, o.options()));
+           });
+}
+
+TORCH_LIBRARY_IMPL(sks_amd, Autograd, m) {
+    m.impl("tensor_aca_rect", rect_autograd);
+    m.impl("tensor_aca_offsets", offsets_autograd);
+}

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hg_aos.hpp"
+#include "hg_rect.hpp"
 #include "hg_soa.hpp"
 #include "sks_homography.h"
 
@@ -182,6 +183,26 @@ int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, f
         return (int)hipErrorInvalidValue;
     return kVariants[variant].launch(algo, src, tar, H, n, per_cu > 0 ? per_cu : 8,
                                      reinterpret_cast<hipStream_t>(stream));
+}
+
+// TensorACA tile sweep (tools/kbench_rect.py).  Variants 0-2: rect form (host scalars
+// scale = a, div = b), P = 1 / 2 / 4 problems per lane; 3-5: compact form (src = corner,
+// tar = offsets, a = width, b = height), P = 1 / 2 / 4.  16-B aligned inputs only.
+int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
+                 float b, void* stream) {
+    if (B <= 0 || !src || !tar || !H) return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const auto blocks = [B](int P) { return (unsigned)((B + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P)); };
+    switch (variant) {
+        case 0: tensor_aca_rect_kernel<1, true, true><<<blocks(1), kBlock, 0, st>>>(src, tar, H, B, nullptr, nullptr, a, b); break;
+        case 1: tensor_aca_rect_kernel<2, true, true><<<blocks(2), kBlock, 0, st>>>(src, tar, H, B, nullptr, nullptr, a, b); break;
+        case 2: tensor_aca_rect_kernel<4, true, true><<<blocks(4), kBlock, 0, st>>>(src, tar, H, B, nullptr, nullptr, a, b); break;
+        case 3: tensor_aca_offsets_kernel<1, true, false><<<blocks(1), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
+        case 4: tensor_aca_offsets_kernel<2, true, false><<<blocks(2), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
+        case 5: tensor_aca_offsets_kernel<4, true, false><<<blocks(4), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

@@ -127,3 +127,29 @@ def test_product_never_imports_oracle():
             if f.endswith((".py", ".hip", ".cpp", ".hpp", ".h")):
                 text = open(os.path.join(dirpath, f)).read()
                 assert not forbidden.search(text), f"{f} reaches the oracle"
+
+
+def test_native_torch_ops_registered(pkg):
+    """torch.ops.sks_amd.* come from lib/libsks_homography_torch.so (C++ dispatcher
+    registrations): every schema is there, Meta kernels give the shapes, and there is no
+    CPU kernel."""
+    import torch
+    ops = torch.ops.sks_amd
+    want = {
+        "aca": ["default", "out"], "sks": ["default", "out"],
+        "tensor_aca_rect": ["default", "out", "scalar", "scalar_out"],
+        "tensor_aca_rect_backward": ["default"],
+        "tensor_aca_offsets": ["default", "out"], "tensor_aca_offsets_backward": ["default"],
+    }
+    for name, overloads in want.items():
+        assert sorted(getattr(ops, name).overloads()) == sorted(overloads), name
+    m = lambda *s: torch.empty(*s, device="meta")  # noqa: E731
+    assert ops.tensor_aca_rect(m(5, 3, 4), m(5, 3, 4), m(1), m(1)).shape == (5, 3, 3)
+    assert ops.tensor_aca_offsets(m(5, 2), m(5, 4, 2), 1.0, 2.0).shape == (5, 3, 3)
+    assert ops.aca(m(5, 4, 2), m(5, 4, 2), True).shape == (5, 3, 3)
+    g = ops.tensor_aca_rect_backward(m(5, 3, 4), m(5, 3, 4), m(5, 3, 3), m(1), m(1), True, False)
+    assert [tuple(x.shape) for x in g] == [(5, 3, 4), (5, 3, 4), (0,)]
+    with pytest.raises(NotImplementedError):
+        ops.tensor_aca_offsets(torch.zeros(2, 2), torch.zeros(2, 4, 2), 1.0, 1.0)
+    with open("/proc/self/maps") as f:
+        assert "libsks_homography_torch.so" in f.read()
