@@ -24,6 +24,7 @@ enum : int {
     kDirectSt = 8,   // store H rows per lane (9 x 4-B stores) instead of LDS-staged 16-B stores
     kPersist = 16,   // persistent grid: blocks loop over tiles
     kLdsDma = 32,    // with kLdsLoad: global_load_lds_dwordx4 (LDS-DMA, no VGPR staging)
+    kXcdMap = 64,    // one-shot grid: each XCD's blocks take one contiguous range of tiles
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -262,7 +263,15 @@ __global__ __launch_bounds__(kBlock) void solve_aos(const T* __restrict__ src,
              t += (int64_t)gridDim.x * kWavesPerBlock)
             aos_wave_tile<ALGO, NORM, T, P, FL>(src, tar, H, n, t * S::kTile, smem[wave], lane);
     } else {
-        const int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+        int64_t b = blockIdx.x;
+        if constexpr (FL & kXcdMap) {
+            // blocks are dispatched to the 8 XCDs round-robin (b % 8); renumber so that
+            // XCD x's blocks cover one contiguous slice of the batch
+            const uint32_t G = gridDim.x, per = G / 8, rem = G % 8;
+            const uint32_t x = blockIdx.x % 8, k = blockIdx.x / 8;
+            b = (int64_t)(x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+        }
+        const int64_t t = b * kWavesPerBlock + wave;
         if (t < tiles)
             aos_wave_tile<ALGO, NORM, T, P, FL>(src, tar, H, n, t * S::kTile, smem[wave], lane);
     }

@@ -67,6 +67,9 @@ const Variant kVariants[] = {
     {"P2 pipe x4 tiles/wave", launch_pipe<2, 4>},
     {"P2 pipe x8 tiles/wave", launch_pipe<2, 8>},
     {"P1 pipe x4 tiles/wave", launch_pipe<1, 4>},
+    {"P2 nt lds-dma xcd-contig", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
+    {"P1 nt lds-dma xcd-contig", launch_variant<1, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
+    {"P4 nt lds-dma xcd-contig", launch_variant<4, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.
