@@ -16,6 +16,28 @@ from . import _lib
 from .ops import _guard, _require_device, _stream
 
 
+def read_points(filename: str):
+    """The reference's correspondence-file reader (CPU_Runtime Test/utils.cpp:6-21): the
+    first line holds the count N, then N lines "x1 y1 x2 y2" (source point, target
+    point).  Returns (pool_src, pool_tar), each an (N,2) float32 numpy array, ready for
+    sample_solve / score / ransac (orig_pts_wall.txt is the reference's own file)."""
+    import numpy as np
+
+    with open(filename) as f:
+        head = f.readline().split()
+        if not head:
+            raise ValueError(f"{filename}: empty file (expected the point count first)")
+        count = int(head[0])
+        rows = []
+        for i in range(count):
+            vals = f.readline().split()[:4]
+            if len(vals) < 4:
+                raise ValueError(f"{filename}: line {i + 2} has fewer than 4 values")
+            rows.append(vals)
+    a = np.asarray(rows, dtype=np.float32).reshape(count, 4)
+    return np.ascontiguousarray(a[:, 0:2]), np.ascontiguousarray(a[:, 2:4])
+
+
 def fill_bits(count: int, seed: int, offset: int = 0, device="cuda") -> torch.Tensor:
     """Counter-based uint32 draws (held in an int32 tensor), bit-identical to the
     host regeneration."""

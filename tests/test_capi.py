@@ -153,3 +153,26 @@ def test_native_torch_ops_registered(pkg):
         ops.tensor_aca_offsets(torch.zeros(2, 2), torch.zeros(2, 4, 2), 1.0, 1.0)
     with open("/proc/self/maps") as f:
         assert "libsks_homography_torch.so" in f.read()
+
+
+def test_read_points_matches_reference_format(pkg, tmp_path):
+    """read_points parses the reference's correspondence-file format (utils.cpp:6-21:
+    count line, then "x1 y1 x2 y2" rows) to the same float32 pools as the committed
+    orig_pts_wall.txt fixture."""
+    import numpy as np
+    from conftest import load_golden
+    g = load_golden("cpp_wall.npz")
+    ps, pt = g["pool_src"], g["pool_tar"]
+    path = tmp_path / "pts.txt"
+    with open(path, "w") as f:
+        f.write(f"{ps.shape[0]}\n")
+        for a, b in zip(ps, pt):  # shortest decimals that round-trip (the file's own style)
+            f.write(" ".join(np.format_float_positional(v, unique=True)
+                             for v in (a[0], a[1], b[0], b[1])) + "\n")
+    rs, rt = pkg.read_points(str(path))
+    assert rs.dtype == np.float32 and rs.shape == ps.shape
+    assert np.array_equal(rs, ps) and np.array_equal(rt, pt)
+    bad = tmp_path / "short.txt"
+    bad.write_text("3\n1 2 3 4\n")
+    with pytest.raises(ValueError):
+        pkg.read_points(str(bad))
