@@ -9,9 +9,11 @@
 //       -Lsks-homography_amd/lib -lsks_homography_amd -L/opt/rocm/lib -lamdhip64 -o dropin
 #include <hip/hip_runtime_api.h>
 
+#include <atomic>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #include "sks_aca_sks.hpp"
@@ -67,6 +69,36 @@ int main() {
     float row[9];
     (void)hipMemcpy(row, dH, 36, hipMemcpyDeviceToHost);
     if (std::memcmp(row, h_sks, sizeof row) != 0) return 8;
+    // the reference's functions are pure and re-entrant: 8 host threads
+    // calling the single-problem API at once must each get their own problem's bits
+    const int kThreads = 8, kCalls = 200;
+    std::vector<float> ts(kThreads * 8), tt(kThreads * 8), want(kThreads * 9);
+    for (int t = 0; t < kThreads; ++t)
+        for (int k = 0; k < 8; ++k) {
+            ts[t * 8 + k] = src[k] + 3.25f * t * (k % 3);
+            tt[t * 8 + k] = tar[k] - 1.5f * t * (k % 2);
+        }
+    (void)hipMemcpy(ds, ts.data(), kThreads * 32, hipMemcpyHostToDevice);
+    (void)hipMemcpy(dt, tt.data(), kThreads * 32, hipMemcpyHostToDevice);
+    if (check(sks::runKernel_SKS_batch(ds, dt, dH, kThreads), "runKernel_SKS_batch")) return 9;
+    (void)hipMemcpy(want.data(), dH, kThreads * 36, hipMemcpyDeviceToHost);
+    std::atomic<int> mismatches{0};
+    std::vector<std::thread> pool;
+    for (int t = 0; t < kThreads; ++t)
+        pool.emplace_back([&, t] {
+            float h[9];
+            for (int c = 0; c < kCalls; ++c) {
+                if (sks::runKernel_SKS(&ts[t * 8], &tt[t * 8], h) != 0 ||
+                    std::memcmp(h, &want[t * 9], sizeof h) != 0)
+                    mismatches.fetch_add(1);
+            }
+        });
+    for (auto& th : pool) th.join();
+    if (mismatches.load() != 0) {
+        std::fprintf(stderr, "%d threaded calls differ from the batch result\n", mismatches.load());
+        return 10;
+    }
+    std::printf("%d threads x %d calls: every result bit-identical to the batch\n", kThreads, kCalls);
     (void)hipFree(ds); (void)hipFree(dt); (void)hipFree(dH);
     std::printf("dropin ok: %lld batch rows bit-identical to the single call\n", (long long)n);
     return 0;
