@@ -190,12 +190,52 @@ __global__ __launch_bounds__(kBlock) void ransac_score2_kernel(
     if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
 }
 
+// Pool points through the scalar unit instead of LDS: every lane of a wave needs the
+// same point, so the loads are wave-uniform -- s_load into SGPRs that the packed VALU
+// ops read directly.  No LDS (occupancy is then set by VGPRs alone), no block barriers,
+// no chunking; the pool (16 B per pair) streams through the scalar cache / L2.
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void ransac_score_sgpr_kernel(
+    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
+    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
+    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
+    f32x2 h[9];
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        h[k].x = p0 < n ? H[p0 * 9 + k] : 0.f;
+        h[k].y = p0 + 1 < n ? H[(p0 + 1) * 9 + k] : 0.f;
+    }
+    const f32x2 t2v = {t2, t2};
+    i32x2 cnt = {0, 0};
+    auto pair = [&](float2 a, float2 b) {
+        const f32x2 x = {a.x, a.x}, y = {a.y, a.y}, nu = {-b.x, -b.x}, nv = {-b.y, -b.y};
+        const f32x2 xs = __builtin_elementwise_fma(h[0], x, __builtin_elementwise_fma(h[1], y, h[2]));
+        const f32x2 ys = __builtin_elementwise_fma(h[3], x, __builtin_elementwise_fma(h[4], y, h[5]));
+        const f32x2 ws = __builtin_elementwise_fma(h[6], x, __builtin_elementwise_fma(h[7], y, h[8]));
+        const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
+        const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
+        const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
+        const f32x2 lim = t2v * (ws * ws);
+        const f32x2 zero = {0.f, 0.f};
+        cnt -= (e2 <= lim) & (ws != zero);
+    };
+    uint32_t i = 0;
+    for (; i + UNROLL <= npool; i += UNROLL) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) pair(pool_src[i + u], pool_tar[i + u]);
+    }
+    for (; i < npool; ++i) pair(pool_src[i], pool_tar[i]);
+    if (p0 < n) counts[p0] = (uint32_t)cnt.x;
+    if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
+}
+
 }  // namespace hg
 
 extern "C" {
 
 // Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
-// 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4).
+// 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4), 3 / 4 = two
+// per lane packed, pool through scalar loads (unroll 4 / 8).
 int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream) {
@@ -210,6 +250,8 @@ int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
         case 0: hg::ransac_score_kernel<<<(unsigned)b1, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         case 1: hg::ransac_score2_kernel<1><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         case 2: hg::ransac_score2_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 3: hg::ransac_score_sgpr_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 4: hg::ransac_score_sgpr_kernel<8><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -259,11 +301,12 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
     if (!H || !counts || (npool && (!pool_src || !pool_tar))) return (int)hipErrorInvalidValue;
     if ((reinterpret_cast<uintptr_t>(pool_src) & 7u) || (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
         return (int)hipErrorInvalidValue;
-    // shipped: two hypotheses per lane, packed (tools/kbench_score.py, profiles/r01)
+    // shipped: two hypotheses per lane, packed, pool through scalar loads, unroll 8
+    // (tools/kbench_score.py, profiles/r01/kbench_score.json)
     const int64_t blocks = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
     if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
     const float t2 = thresh * thresh;
-    hg::ransac_score2_kernel<4><<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
+    hg::ransac_score_sgpr_kernel<8><<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
         H, n, reinterpret_cast<const float2*>(pool_src), reinterpret_cast<const float2*>(pool_tar),
         npool, t2, counts);
     return (int)hipGetLastError();

@@ -14,6 +14,9 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 
+NV = 5  # hg_tune_score variants (csrc/hg_ransac.hip)
+
+
 def main():
     pkg = ge.load_package()
     lib = pkg.lib()
@@ -32,14 +35,14 @@ def main():
     out = torch.empty_like(want)
     sp = torch.cuda.current_stream(dev).cuda_stream
     res = {}
-    times = {v: [] for v in range(3)}
-    for v in range(3):
+    times = {v: [] for v in range(NV)}
+    for v in range(NV):
         assert lib.hg_tune_score(v, H.data_ptr(), n, ps.data_ptr(), pt.data_ptr(), ps.shape[0],
                                  3.0, out.data_ptr(), sp) == 0
         torch.cuda.synchronize()
         res[v] = bool(torch.equal(out, want))
     for _ in range(5):
-        for v in range(3):
+        for v in range(NV):
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(5):
@@ -50,7 +53,7 @@ def main():
             times[v].append(e0.elapsed_time(e1) / 5)
     pairs = n * ps.shape[0]
     recs = []
-    for v in range(3):
+    for v in range(NV):
         med = statistics.median(times[v])
         rec = {"variant": v, "ms": round(med, 4), "G_pairs_per_s": round(pairs / med / 1e6, 1),
                "exact": res[v]}
