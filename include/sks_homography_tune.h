@@ -36,6 +36,10 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
 int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
                  float b, void* stream);
 
+/* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2). */
+int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
+                   const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
+
 int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream);

@@ -92,6 +92,95 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     }
 }
 
+// r mod d for every 32-bit r and d >= 1 by one 64-bit multiply and a high multiply
+// (Lemire, Kaser & Kurz, "Faster remainder by direct computation", 2019), with
+// M = floor((2^64 - 1) / d) + 1 computed once on the host.  Equals r % d exactly.
+__device__ __forceinline__ uint32_t fastmod_u32(uint32_t r, uint64_t M, uint32_t d) {
+    return (uint32_t)__umul64hi(M * (uint64_t)r, (uint64_t)d);
+}
+
+inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
+
+// The same sampler with the pool staged in LDS once per block: {x, y, u, v} 16-B
+// records, so a hypothesis gathers with 4 ds_read_b128 instead of 8 scattered global
+// loads through the texture path (the bound of sample_solve_kernel: 47 G hyp/s, 30 % of
+// HBM).  Persistent grid sized to the resident blocks; each wave walks its tiles with
+// the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
+// and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
+// staging to fit the block's LDS (checked on the host).
+template <int ALGO, bool NORM, int P>
+__global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
+    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
+    uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
+    constexpr int kTile = kWave * P;
+    constexpr int kStage = kTile * 36;
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    float4* pool = reinterpret_cast<float4*>(dyn);
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    char* stage = dyn + (size_t)npool * 16 + (size_t)wave * kStage;
+    for (uint32_t i = threadIdx.x; i < npool; i += kBlock) {
+        const float2 a = pool_src[i], b = pool_tar[i];
+        pool[i] = make_float4(a.x, a.y, b.x, b.y);
+    }
+    __syncthreads();
+
+    const int64_t tiles = (n + kTile - 1) / kTile;
+    const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock;
+    int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    auto load = [&](int64_t tile, u32x4 (&r)[P]) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const int64_t p = tile * kTile + j * kWave + lane;
+            r[j] = p < n ? ld16<true>(reinterpret_cast<const char*>(idx + p)) : u32x4{0, 0, 0, 0};
+        }
+    };
+    u32x4 cur[P];
+    if (t < tiles) load(t, cur);
+    for (; t < tiles; t += stride) {
+        u32x4 nxt[P]{};
+        if (t + stride < tiles) load(t + stride, nxt);
+        float h[P][9];
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const uint32_t id[4] = {fastmod_u32(cur[j].x, magic, npool),
+                                    fastmod_u32(cur[j].y, magic, npool),
+                                    fastmod_u32(cur[j].z, magic, npool),
+                                    fastmod_u32(cur[j].w, magic, npool)};
+            float s[8], tt[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 q = pool[id[k]];
+                s[2 * k] = q.x; s[2 * k + 1] = q.y;
+                tt[2 * k] = q.z; tt[2 * k + 1] = q.w;
+            }
+            solve<ALGO, NORM>(s, tt, h[j]);
+        }
+        const int64_t base = t * kTile;
+        if (base + kTile <= n) {
+            store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, stage, lane);
+        } else {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const int64_t p = base + j * kWave + lane;
+                if (p < n) {
+#pragma unroll
+                    for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
+                }
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < P; ++j) cur[j] = nxt[j];
+    }
+}
+
+// LDS bytes of sample_solve_lds_kernel<P> for a pool of npool points.
+template <int P>
+constexpr size_t sample_lds_bytes(uint32_t npool) {
+    return (size_t)npool * 16 + (size_t)kWavesPerBlock * kWave * P * 36;
+}
+constexpr size_t kSampleLdsMax = 64 * 1024;  // per-block dynamic LDS without opt-in
+
 // Inlier test of one (hypothesis, correspondence) pair, division-free:
 //   (x', y', w') = H (x, y, 1),  inlier <=> w' != 0 and
 //   (x' - u w')^2 + (y' - v w')^2 <= t^2 w'^2        [== |(x'/w', y'/w') - (u, v)|^2 <= t^2]
@@ -229,9 +318,77 @@ __global__ __launch_bounds__(kBlock) void ransac_score_sgpr_kernel(
     if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
 }
 
+int cu_count() {
+    static int cus = [] {
+        int dev = 0, v = 0;
+        if (hipGetDevice(&dev) != hipSuccess ||
+            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+            return 256;
+        return v > 0 ? v : 256;
+    }();
+    return cus;
+}
+
+// variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
+// P = 1 / 2 (falls back to 0 when the pool does not fit).
+int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
+                        const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
+    constexpr int kShippedP = 2;
+    int use_p = variant == -1 ? kShippedP : variant;
+    const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
+    if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
+    if (use_p == 0) {
+        constexpr int P = 2;
+        const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
+        if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+        const unsigned g = (unsigned)blocks;
+#define HG_SS(A, N) sample_solve_kernel<A, N, P><<<g, kBlock, 0, s>>>(ps, pt, npool, ix, H, n)
+        if (algo == 0) { if (norm) HG_SS(kACA, true); else HG_SS(kACA, false); }
+        else { if (norm) HG_SS(kSKS, true); else HG_SS(kSKS, false); }
+#undef HG_SS
+        return (int)hipGetLastError();
+    }
+    // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
+    const int64_t tiles = (n + (int64_t)kWave * use_p - 1) / ((int64_t)kWave * use_p);
+    const int64_t want = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
+    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+    const int64_t cap = per_cu * cu_count();
+    const unsigned g = (unsigned)(want < cap ? want : cap);
+    const uint64_t magic = fastmod_magic(npool);
+#define HG_SL(PP, A, N) \
+    sample_solve_lds_kernel<A, N, PP><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
+    if (use_p == 1) {
+        if (algo == 0) { if (norm) HG_SL(1, kACA, true); else HG_SL(1, kACA, false); }
+        else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
+    } else {
+        if (algo == 0) { if (norm) HG_SL(2, kACA, true); else HG_SL(2, kACA, false); }
+        else { if (norm) HG_SL(2, kSKS, true); else HG_SL(2, kSKS, false); }
+    }
+#undef HG_SL
+    return (int)hipGetLastError();
+}
+
 }  // namespace hg
 
 extern "C" {
+
+// Sampler variants for tools/kbench_sample.py (0 global gather, 1 / 2 LDS pool P1 / P2);
+// same argument checks as hg_sample_solve_f32.
+int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
+                   const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 2 || (algo != 0 && algo != 1))
+        return (int)hipErrorInvalidValue;
+    if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
+        (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
+        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return (int)hipErrorInvalidValue;
+    return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
+                                   reinterpret_cast<const float2*>(pool_tar), npool,
+                                   reinterpret_cast<const uint4*>(idx), H, n, algo,
+                                   (flags & HG_FLAG_NORMALIZE) != 0,
+                                   reinterpret_cast<hipStream_t>(stream));
+}
 
 // Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
 // 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4), 3 / 4 = two
@@ -278,20 +435,11 @@ int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t n
     if ((reinterpret_cast<uintptr_t>(idx) & 15u) || (reinterpret_cast<uintptr_t>(H) & 15u) ||
         (reinterpret_cast<uintptr_t>(pool_src) & 7u) || (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
         return (int)hipErrorInvalidValue;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    constexpr int P = 2;
-    const int64_t blocks = (n + (int64_t)hg::kBlock * P - 1) / ((int64_t)hg::kBlock * P);
-    if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
-    const auto* ps = reinterpret_cast<const float2*>(pool_src);
-    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
-    const auto* ix = reinterpret_cast<const uint4*>(idx);
-    const unsigned g = (unsigned)blocks;
-    const bool norm = flags & HG_FLAG_NORMALIZE;
-#define HG_SS(A, N) hg::sample_solve_kernel<A, N, P><<<g, hg::kBlock, 0, s>>>(ps, pt, npool, ix, H, n)
-    if (algo == 0) { if (norm) HG_SS(hg::kACA, true); else HG_SS(hg::kACA, false); }
-    else { if (norm) HG_SS(hg::kSKS, true); else HG_SS(hg::kSKS, false); }
-#undef HG_SS
-    return (int)hipGetLastError();
+    return hg::launch_sample_solve(-1, reinterpret_cast<const float2*>(pool_src),
+                                   reinterpret_cast<const float2*>(pool_tar), npool,
+                                   reinterpret_cast<const uint4*>(idx), H, n, algo,
+                                   (flags & HG_FLAG_NORMALIZE) != 0,
+                                   reinterpret_cast<hipStream_t>(stream));
 }
 
 int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,

@@ -57,3 +57,37 @@ def test_ransac_end_to_end(oracle, pkg, dev):
     assert want == res.inliers
     # a wall seen from two views: the best of 20 K hypotheses explains most pairs
     assert res.inliers > 0.5 * ps.shape[0], res.inliers
+
+
+def _tune_sample(pkg):
+    import ctypes
+    f = pkg.lib().hg_tune_sample
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    return f
+
+
+@pytest.mark.parametrize("npool", [1, 2, 3, 7, 2540, 3900, 20_000])
+@pytest.mark.parametrize("variant", [0, 1, 2])
+def test_sample_solve_variants_vs_oracle(orc, oracle, pkg, dev, npool, variant):
+    """Every sampler form (global gather; pool staged in LDS, P = 1/2) against the oracle:
+    pools from 1 point (fastmod's magic wraps to 0) to beyond the LDS limit (the LDS
+    forms fall back), ragged batches over the persistent grid, indices spanning all of
+    uint32 (modulo reduction as get_rand_list, .cu:56-59)."""
+    g = np.random.default_rng(npool)
+    ps = (g.random((npool, 2)) * 1000).astype(np.float32)
+    pt = (g.random((npool, 2)) * 1000).astype(np.float32)
+    dps, dpt = torch.from_numpy(ps).to(dev), torch.from_numpy(pt).to(dev)
+    f = _tune_sample(pkg)
+    for n in (1, 255, 70_001):
+        idx = pkg.fill_bits(n * 4, npool + n, 0, dev).view(n, 4)
+        idx[0, 0] = -1  # 0xFFFFFFFF
+        for algo in (0, 1):
+            H = torch.empty((n, 9), device=dev)
+            rc = f(variant, dps.data_ptr(), dpt.data_ptr(), npool, idx.data_ptr(), H.data_ptr(), n,
+                   algo, 1, torch.cuda.current_stream(dev).cuda_stream)
+            assert rc == 0
+            s, t = oracle.sample_problems(ps, pt, idx.cpu().numpy().view(np.uint32))
+            ok = orc.same_bits(H.cpu().numpy(), oracle.solve("aca" if algo == 0 else "sks", s, t))
+            assert ok.all(), f"variant {variant} npool {npool} n {n}: {(~ok).sum()} differ"

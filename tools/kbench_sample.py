@@ -1,0 +1,74 @@
+"""Fused RANSAC sampler + solver (hg_tune_sample variants: 0 global gather, 1 / 2 pool in
+LDS with P = 1 / 2) across batch sizes over the reference's orig_pts_wall.txt pool
+(tests/golden).  Device time per launch from event-bracketed back-to-back launches,
+interleaved rounds, median; algorithmic GB/s at 16 B of indices + 36 B of H per
+hypothesis (the pool is cache-resident).  Outputs compared bit for bit with variant 0."""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2"}
+
+
+def main():
+    pkg = ge.load_package()
+    f = pkg.lib().hg_tune_sample
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
+                  ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    dev = torch.device("cuda:0")
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"]).to(dev)
+    pt = torch.from_numpy(g["pool_tar"]).to(dev)
+    npool = ps.shape[0]
+    out = {}
+    for n in (1 << 20, 1 << 22, 1 << 24):
+        idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
+        outs = {v: torch.empty((n, 9), device=dev) for v in NAMES}
+        st = torch.cuda.current_stream(dev).cuda_stream
+
+        def run(v):
+            assert f(v, ps.data_ptr(), pt.data_ptr(), npool, idx.data_ptr(), outs[v].data_ptr(), n,
+                     0, 1, st) == 0
+
+        for v in NAMES:
+            for _ in range(3):
+                run(v)
+        torch.cuda.synchronize()
+        exact = {v: bool(torch.equal(outs[v].view(torch.int32), outs[0].view(torch.int32)))
+                 for v in NAMES}
+        times = {v: [] for v in NAMES}
+        reps = 20
+        for _ in range(7):
+            for v in NAMES:
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(reps):
+                    run(v)
+                e1.record()
+                torch.cuda.synchronize()
+                times[v].append(e0.elapsed_time(e1) / reps * 1e3)
+        res = {}
+        for v, name in NAMES.items():
+            us = statistics.median(times[v])
+            res[name] = {"us": round(us, 2), "G_hyp_per_s": round(n / us / 1e3, 2),
+                         "algorithmic_gbps": round(n * 52 / us / 1e3, 1), "bit_exact": exact[v]}
+            print(n, name, res[name], flush=True)
+        out[str(n)] = res
+        del idx, outs
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "kbench_sample.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
