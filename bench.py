@@ -111,22 +111,25 @@ def timed_region(d: Dist, fn, steps: int):
     return d.max(wall), e0.elapsed_time(e1) / steps
 
 
-def launch_stats(d: Dist, fn, launches: int = 200):
-    """Per-launch device-time distribution: a HIP event pair around every launch on the
-    launch stream (report the median beside the mean)."""
+def launch_stats(d: Dist, fn, groups: int = 40, per_group: int = 10):
+    """Per-launch device-time distribution (the median beside the mean):
+    HIP events bracket groups of `per_group` back-to-back launches on the launch stream,
+    and each group's mean is one sample.  (An event pair around every single launch
+    adds its own ~5 us to each sample -- tools/prof_agree.py against rocprofv3.)"""
     stream = torch.cuda.current_stream(d.dev)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(launches)]
+          for _ in range(groups)]
     torch.cuda.synchronize(d.dev)
     for a, b in ev:
         a.record(stream)
-        fn()
+        for _ in range(per_group):
+            fn()
         b.record(stream)
     torch.cuda.synchronize(d.dev)
-    ts = np.sort(np.array([a.elapsed_time(b) for a, b in ev])) * 1e3
-    return {"launches": launches, "median_us": round(float(np.median(ts)), 2),
-            "p10_us": round(float(ts[launches // 10]), 2),
-            "p90_us": round(float(ts[(9 * launches) // 10]), 2),
+    ts = np.sort(np.array([a.elapsed_time(b) for a, b in ev])) / per_group * 1e3
+    return {"launches": groups * per_group, "groups": groups, "median_us": round(float(np.median(ts)), 2),
+            "p10_us": round(float(ts[groups // 10]), 2),
+            "p90_us": round(float(ts[(9 * groups) // 10]), 2),
             "min_us": round(float(ts[0]), 2)}
 
 
@@ -348,11 +351,22 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     _, ms_score = timed_region(d, f_score, 5)
     counts = pkg.ransac_score(H, ps, pt, thresh)
     pairs = hyps * ps.shape[0]
+    big = 16 * hyps  # the sampler's HBM-rate figure (16 B idx + 36 B H per hypothesis)
+    idx_b = pkg.fill_bits(big * 4, SEED, 0, d.dev).view(big, 4)
+    f_big = lambda: pkg.sample_solve(ps, pt, idx_b)  # noqa: E731
+    for _ in range(3):
+        f_big()
+    _, ms_big = timed_region(d, f_big, 10)
+    del idx_b
     return {
         "hypotheses": hyps, "pool": int(ps.shape[0]), "thresh_px": thresh,
         "sample_solve_us": round(ms_solve * 1e3, 2),
         "sample_solve_G_hyp_per_s": round(hyps / (ms_solve * 1e-3) / 1e9, 2),
         "sample_solve_gbps": round(hyps * 52 / (ms_solve * 1e-3) / 1e9, 1),
+        "sample_solve_large": {"hypotheses": big, "us": round(ms_big * 1e3, 2),
+                               "G_hyp_per_s": round(big / (ms_big * 1e-3) / 1e9, 2),
+                               "achieved_gbps": round(big * 52 / (ms_big * 1e-3) / 1e9, 1),
+                               "frac": round(big * 52 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
         "score_ms": round(ms_score, 3),
         "score_G_pairs_per_s": round(pairs / (ms_score * 1e-3) / 1e9, 1),
         "best_inliers": int(counts.max().item()),
@@ -407,7 +421,7 @@ def main():
         run("aca")()
     wall, ms_launch = timed_region(d, run("aca"), args.steps)
     value = n_total * args.steps / wall / 1e6
-    per_launch = launch_stats(d, run("aca"), max(200, args.steps))
+    per_launch = launch_stats(d, run("aca"))
     achieved = n * bpp / (ms_launch * 1e-3) / 1e9
     traffic = pmc_traffic("aca_f32_aos_norm")
     line = {

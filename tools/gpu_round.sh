@@ -37,11 +37,12 @@ for step in $STEPS; do
             run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$OUT/prof_$TAG" -o run -- python3 bench.py --no-cpu ;;
         pmc)
-            # HBM traffic: separate passes, FETCH_SIZE and WRITE_SIZE can't share one
-            run pmc_fetch 900 rocprofv3 --pmc FETCH_SIZE --output-format csv \
-                -d "$OUT/pmc_fetch_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2
-            run pmc_write 900 rocprofv3 --pmc WRITE_SIZE --output-format csv \
-                -d "$OUT/pmc_write_$TAG" -o run -- python3 bench.py --no-cpu --steps 20 --warmup 2 ;;
+            # HBM traffic: separate passes (FETCH_SIZE and WRITE_SIZE can't share one), no
+            # tracing domains; a fixed short dispatch list (tools/pmc_run.py)
+            run pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE --output-format csv \
+                -d "$OUT/pmc_fetch_$TAG" -o run -- python3 tools/pmc_run.py
+            run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
+                -d "$OUT/pmc_write_$TAG" -o run -- python3 tools/pmc_run.py ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kbench_soa) run kbench_soa 600 python tools/kbench_soa.py ;;
         kbench_score) run kbench_score 600 python tools/kbench_score.py ;;

@@ -1,0 +1,63 @@
+"""Workload for the rocprofv3 PMC passes (tools/gpu_round.sh pmc): each kernel whose
+HBM traffic bench.py or DESIGN.md quotes, launched a few times at its measured size,
+nothing else -- a short, fixed dispatch list (the full bench under --pmc is tens of
+thousands of serialized dispatches).  tools/pmc_traffic.py reduces the counters."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+REPS = 5
+
+
+def main():
+    pkg = ge.load_package()
+    dev = torch.device("cuda:0")
+    n = 10_000_000
+    src = pkg.fill_uniform(n * 8, 11, 0, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, 11, n * 8, device=dev).view(n, 8)
+    H = torch.empty((n, 9), device=dev)
+    for algo in ("aca", "sks"):
+        for _ in range(REPS):
+            pkg.solve(algo, src, tar, normalize=True, out=H)
+    nb = (n * 100) // 2 // 16 * 16
+    a = torch.ones(nb // 4, device=dev)
+    b = torch.empty_like(a)
+    for _ in range(REPS):
+        pkg.stream_copy(a, b)
+    del a, b
+    s64, t64 = src.view(8, n).double(), tar.view(8, n).double()
+    H64 = torch.empty((9, n), dtype=torch.float64, device=dev)
+    for algo in ("aca", "sks"):
+        for _ in range(REPS):
+            pkg.solve(algo, s64, t64, normalize=False, layout="soa", out=H64)
+    del s64, t64, H64, src, tar, H
+    big = 16 * 1024 * 1024
+    torch.manual_seed(0)
+    _, _, bs, bt, sc, dv = pkg.adjust(dev, big)
+    Hb = torch.empty((big, 3, 3), device=dev)
+    for _ in range(REPS):
+        pkg.ops.tensor_aca_rect(bs, bt, sc, dv, out=Hb)
+    corner = bs[:, 0:2, 0].contiguous()
+    offs = (bt[:, 0:2, :] - bs[:, 0:2, :]).transpose(1, 2).contiguous()
+    del bs, bt
+    for _ in range(REPS):
+        pkg.ops.tensor_aca_offsets(corner, offs, 128.0, 128.0, out=Hb)
+    del corner, offs, Hb
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"]).to(dev)
+    pt = torch.from_numpy(g["pool_tar"]).to(dev)
+    idx = pkg.fill_bits(big * 4, 11, 0, dev).view(big, 4)
+    for _ in range(REPS):
+        pkg.sample_solve(ps, pt, idx)
+    torch.cuda.synchronize()
+    print("pmc workload done")
+
+
+if __name__ == "__main__":
+    main()

@@ -28,6 +28,9 @@ KEYS = {
     "sks_f32_aos_norm": ("void hg::solve_aos<1, true, float", 10_000_000 * 100),
     "stream_copy": ("hg::stream_copy_kernel", None),
     "tensor_aca_rect": ("void hg::tensor_aca_rect_kernel", None),
+    "tensor_aca_offsets": ("void hg::tensor_aca_offsets_kernel", None),
+    "sample_solve_lds": ("void hg::sample_solve_lds_kernel", None),
+    "solve_soa": ("void hg::solve_soa_vec", None),
 }
 
 
@@ -70,7 +73,8 @@ def main():
     doc["detail"] = res
     doc["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, csv; "
                      "bytes = KiB*1024, FETCH x2 (gfx950 wide-read correction, calibrated on "
-                     "stream_copy); median over launches of `python3 bench.py --no-cpu --steps 20`")
+                     "stream_copy); median over the launches of `python3 tools/pmc_run.py` (each kernel 5x at "
+                     "its bench size)")
     print(json.dumps(doc, indent=1))
     if out_path:
         with open(out_path, "w") as fh:
