@@ -142,6 +142,18 @@ int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t n
 int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,
                         uint32_t npool, float thresh, uint32_t* counts, void* stream);
 
+/* ONE problem, latency path: src[8] and tar[8] are read on the HOST and passed in the
+ * kernel launch itself (no copy); H[9] is written by the device -- pass device memory,
+ * or host memory mapped into the device address space (hipHostMalloc(...,
+ * hipHostMallocMapped) and its hipHostGetDevicePointer) to skip the D2H copy too.
+ * Asynchronous like every entry point: synchronise `stream` before reading H.  algo 0 =
+ * ACA, 1 = SKS.  What sks::runKernel_* (ACA_SKS.cpp:24, :104, :189, :305) use for host
+ * pointers (hg_sks_api.cpp). */
+int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int flags,
+                     void* stream);
+int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, int flags,
+                     void* stream);
+
 /* Device-to-device streaming copy (float4) used by bench.py as the measured
  * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */
 int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);

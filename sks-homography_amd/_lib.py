@@ -43,6 +43,8 @@ SIGNATURES = {
     "hg_sample_solve_f32": ([_vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _int, _vp], _int),
     "hg_ransac_score_f32": ([_vp, _i64, _vp, _vp, ctypes.c_uint32, ctypes.c_float, _vp, _vp],
                             _int),
+    "hg_solve_one_f32": ([_int, _vp, _vp, _vp, _int, _vp], _int),
+    "hg_solve_one_f64": ([_int, _vp, _vp, _vp, _int, _vp], _int),
     "hg_stream_copy": ([_vp, _vp, _i64, _vp], _int),
     "hg_version": ([], ctypes.c_char_p),
 }

@@ -68,6 +68,23 @@ __global__ __launch_bounds__(kBlock) void fill_uniform_kernel(float* __restrict_
     }
 }
 
+// One problem whose points travel in the kernel arguments (no H2D copy); one lane
+// solves and writes H (9 values) straight to `H`, typically host memory mapped into the
+// device address space -- the latency path of the single-problem sks:: calls.
+template <typename T>
+struct Quad {
+    T src[8], tar[8];
+};
+
+template <int ALGO, bool NORM, typename T>
+__global__ __launch_bounds__(kWave) void solve_one_kernel(Quad<T> q, T* __restrict__ H) {
+    if (threadIdx.x != 0) return;
+    T h[9];
+    solve<ALGO, NORM>(q.src, q.tar, h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H[k] = h[k];
+}
+
 // Streaming copy, 16 B per lane per iteration (bandwidth yardstick).
 __global__ __launch_bounds__(kBlock) void stream_copy_kernel(const u32x4* __restrict__ src,
                                                              u32x4* __restrict__ dst,
@@ -162,6 +179,27 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
     else
         tensor_aca_rect_kernel<P, false, SCALAR>
             <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    return launch_status();
+}
+
+template <typename T>
+int launch_one(int algo, const T* src, const T* tar, T* H, int flags, void* stream) {
+    if (!src || !tar || !H || (flags & ~HG_FLAG_NORMALIZE)) return kErrInvalid;
+    if (algo != kACA && algo != kSKS) return kErrInvalid;
+    Quad<T> q;
+    for (int k = 0; k < 8; ++k) {
+        q.src[k] = src[k];
+        q.tar[k] = tar[k];
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool norm = flags & HG_FLAG_NORMALIZE;
+    if (algo == kACA) {
+        if (norm) solve_one_kernel<kACA, true, T><<<1, kWave, 0, s>>>(q, H);
+        else solve_one_kernel<kACA, false, T><<<1, kWave, 0, s>>>(q, H);
+    } else {
+        if (norm) solve_one_kernel<kSKS, true, T><<<1, kWave, 0, s>>>(q, H);
+        else solve_one_kernel<kSKS, false, T><<<1, kWave, 0, s>>>(q, H);
+    }
     return launch_status();
 }
 
@@ -294,6 +332,16 @@ int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
     hg::stream_copy_kernel<<<g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
         reinterpret_cast<const hg::u32x4*>(src), reinterpret_cast<hg::u32x4*>(dst), n16);
     return hg::launch_status();
+}
+
+int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int flags,
+                     void* stream) {
+    return hg::launch_one<float>(algo, src, tar, H, flags, stream);
+}
+
+int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, int flags,
+                     void* stream) {
+    return hg::launch_one<double>(algo, src, tar, H, flags, stream);
 }
 
 const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }

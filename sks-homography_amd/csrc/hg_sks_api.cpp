@@ -17,20 +17,28 @@ bool is_device_pointer(const void* p) {
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
 }
 
-// Per-thread staging for one problem: device buffer [src 8 | tar 8 | H 9] and a
-// pinned host mirror.  Allocated on first use, kept for the thread's lifetime.
+// Per-thread state for host-pointer calls: a non-blocking stream (threads never
+// serialise on the legacy default stream) and 9 values of host memory mapped into the
+// device address space, which the kernel writes directly.  The points go in the kernel
+// arguments (hg_solve_one_*), so a call is one launch + one stream synchronisation.
 template <typename T>
 struct Scratch {
-    T* dev = nullptr;
     T* host = nullptr;
+    T* mapped = nullptr;
+    hipStream_t stream = nullptr;
     int device = -1;
     int ensure() {
         int cur = 0;
         hipError_t e = hipGetDevice(&cur);
         if (e != hipSuccess) return (int)e;
-        if (dev && device == cur) return 0;
-        if ((e = hipMalloc(&dev, 32 * sizeof(T))) != hipSuccess) return (int)e;
-        if ((e = hipHostMalloc(&host, 32 * sizeof(T), hipHostMallocDefault)) != hipSuccess)
+        if (host && device == cur) return 0;
+        if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess)
+            return (int)e;
+        if ((e = hipHostMalloc(reinterpret_cast<void**>(&host), 16 * sizeof(T),
+                               hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+            return (int)e;
+        if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&mapped), host, 0)) !=
+            hipSuccess)
             return (int)e;
         device = cur;
         return 0;
@@ -45,11 +53,15 @@ Scratch<T>& scratch() {
 
 template <typename T>
 using BatchFn = int (*)(const T*, const T*, T*, int64_t, int, int, void*);
+template <typename T>
+using OneFn = int (*)(int, const T*, const T*, T*, int, void*);
 
-template <typename T, BatchFn<T> F>
+template <typename T, BatchFn<T> F, OneFn<T> ONE, int ALGO>
 int solve_one(T* src, T* tar, T* result) {
     if (!src || !tar || !result) return (int)hipErrorInvalidValue;
-    if (is_device_pointer(src) && is_device_pointer(tar) && is_device_pointer(result)) {
+    const bool ds = is_device_pointer(src), dt = is_device_pointer(tar);
+    const bool dr = is_device_pointer(result);
+    if (ds && dt && dr) {
         int rc = F(src, tar, result, 1, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, nullptr);
         if (rc) return rc;
         return (int)hipStreamSynchronize(nullptr);
@@ -57,16 +69,21 @@ int solve_one(T* src, T* tar, T* result) {
     Scratch<T>& s = scratch<T>();
     int rc = s.ensure();
     if (rc) return rc;
-    std::memcpy(s.host, src, 8 * sizeof(T));
-    std::memcpy(s.host + 8, tar, 8 * sizeof(T));
-    hipError_t e = hipMemcpyAsync(s.dev, s.host, 16 * sizeof(T), hipMemcpyHostToDevice, nullptr);
-    if (e != hipSuccess) return (int)e;
-    rc = F(s.dev, s.dev + 8, s.dev + 16, 1, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, nullptr);
+    if (ds || dt) {
+        // mixed: stage device-resident inputs to the host first (rare)
+        T in[16];
+        hipError_t e = hipMemcpy(in, src, 8 * sizeof(T), hipMemcpyDefault);
+        if (e == hipSuccess) e = hipMemcpy(in + 8, tar, 8 * sizeof(T), hipMemcpyDefault);
+        if (e != hipSuccess) return (int)e;
+        rc = ONE(ALGO, in, in + 8, s.mapped, HG_FLAG_NORMALIZE, s.stream);
+    } else {
+        rc = ONE(ALGO, src, tar, s.mapped, HG_FLAG_NORMALIZE, s.stream);
+    }
     if (rc) return rc;
-    e = hipMemcpyAsync(s.host + 16, s.dev + 16, 9 * sizeof(T), hipMemcpyDeviceToHost, nullptr);
+    hipError_t e = hipStreamSynchronize(s.stream);
     if (e != hipSuccess) return (int)e;
-    if ((e = hipStreamSynchronize(nullptr)) != hipSuccess) return (int)e;
-    std::memcpy(result, s.host + 16, 9 * sizeof(T));
+    if (dr) return (int)hipMemcpy(result, s.host, 9 * sizeof(T), hipMemcpyHostToDevice);
+    std::memcpy(result, s.host, 9 * sizeof(T));
     return 0;
 }
 
@@ -75,16 +92,16 @@ int solve_one(T* src, T* tar, T* result) {
 namespace sks {
 
 int runKernel_ACA(float* src, float* tar, float* result) {
-    return solve_one<float, hg_aca_f32>(src, tar, result);
+    return solve_one<float, hg_aca_f32, hg_solve_one_f32, 0>(src, tar, result);
 }
 int runKernel_ACA_double(double* src, double* tar, double* result) {
-    return solve_one<double, hg_aca_f64>(src, tar, result);
+    return solve_one<double, hg_aca_f64, hg_solve_one_f64, 0>(src, tar, result);
 }
 int runKernel_SKS(float* src, float* tar, float* result) {
-    return solve_one<float, hg_sks_f32>(src, tar, result);
+    return solve_one<float, hg_sks_f32, hg_solve_one_f32, 1>(src, tar, result);
 }
 int runKernel_SKS_double(double* src, double* tar, double* result) {
-    return solve_one<double, hg_sks_f64>(src, tar, result);
+    return solve_one<double, hg_sks_f64, hg_solve_one_f64, 1>(src, tar, result);
 }
 
 int runKernel_ACA_batch(const float* src, const float* tar, float* result, int64_t n,

@@ -265,6 +265,49 @@ def test_cpp_api_single_problem_host_and_device(orc, pkg, dev):
         _bits(orc, dh, g[f"{algo}_{sfx}"][5], f"sks::{key} device ptrs")
 
 
+def test_cpp_api_mixed_pointers_and_edge_cases(orc, pkg, dev):
+    """The single-problem calls on every host/device pointer mix, over the edge-case
+    fixture (duplicates, collinear, zero area, +-Inf, NaN, subnormals): host inputs ride
+    in the launch arguments (hg_solve_one_*), device ones are staged."""
+    g = load_golden("cpp_edge.npz")
+    fns = _sks_api(pkg)
+    for key, algo in (("aca", "aca"), ("sks", "sks")):
+        f, ct = fns[key]
+        P = ctypes.POINTER(ct)
+        for i in range(g["src"].shape[0]):
+            s = np.ascontiguousarray(g["src"][i])
+            t = np.ascontiguousarray(g["tar"][i])
+            want = g[algo][i]
+            h = np.zeros(9, np.float32)
+            assert f(s.ctypes.data_as(P), t.ctypes.data_as(P), h.ctypes.data_as(P)) == 0
+            _bits(orc, h, want, f"sks::{key} edge #{i} host")
+            if i % 8 == 0:
+                ds = _t(s, dev)
+                dh = torch.zeros(9, device=dev)
+                assert f(ctypes.c_void_p(ds.data_ptr()), t.ctypes.data_as(P),
+                         ctypes.c_void_p(dh.data_ptr())) == 0
+                _bits(orc, dh, want, f"sks::{key} edge #{i} mixed")
+
+
+def test_solve_one_c_abi(orc, pkg, dev):
+    """hg_solve_one_*: host points in the launch, H to device memory, on a stream."""
+    g = load_golden("cpp_uniform.npz")
+    lib = pkg.lib()
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    for sfx, fn, dt in (("f32", lib.hg_solve_one_f32, torch.float32),
+                        ("f64", lib.hg_solve_one_f64, torch.float64)):
+        for algo_id, algo in ((0, "aca"), (1, "sks")):
+            H = torch.empty((16, 9), dtype=dt, device=dev)
+            for i in range(16):
+                s = np.ascontiguousarray(g[f"src_{sfx}"][i])
+                t = np.ascontiguousarray(g[f"tar_{sfx}"][i])
+                assert fn(algo_id, s.ctypes.data, t.ctypes.data, H[i].data_ptr(), 1, stream) == 0
+            torch.cuda.synchronize(dev)
+            _bits(orc, H, g[f"{algo}_{sfx}"][:16], f"hg_solve_one {algo} {sfx}")
+        assert fn(2, s.ctypes.data, t.ctypes.data, H.data_ptr(), 1, stream) == 1
+        assert fn(0, None, t.ctypes.data, H.data_ptr(), 1, stream) == 1
+
+
 # --------------------------------------------------------------- full size
 @pytest.mark.slow
 def test_full_size_10m_bit_exact(orc, oracle, pkg, dev):
