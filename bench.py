@@ -253,6 +253,52 @@ def torch_tensor_aca_rect(src, tar, scale, div):
 
 # imgs/GPU-runtime.png (Table 8), N = 1M, FP64 SoA, unnamed CUDA GPU
 TABLE8_US = {"aca": 245.0, "sks": 436.0, "gpt": 8390.0, "ge": 589.0}
+# the same table's full rows, N = 1 .. 1M
+TABLE8_ROWS = {"aca": [3.11, 3.16, 3.19, 3.20, 5.26, 29.3, 245.0],
+               "sks": [4.20, 4.26, 4.31, 4.83, 7.45, 49.9, 436.0]}
+TABLE8_N = [1, 10, 100, 1000, 10_000, 100_000, 1_000_000]
+
+
+def table8_sweep(d: Dist, pkg):
+    """Table 8 row by row: ACA and SKS, f64 SoA unnormalised (cal_Homo_ACA/SKS), N = 1 ..
+    1M.  `native`: cal_ACA's own method (.cu:1183-1200) -- back-to-back launches from a
+    C++ loop (hg_tune_launch_loop), event-timed, mean per launch; host-launch-bound at
+    small N on both GPUs.  `python`: the same through pkg.solve.  `graph`: device time per
+    launch from a HIP graph of 100 launches."""
+    import ctypes
+    loop = pkg.lib().hg_tune_launch_loop
+    loop.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
+                     ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                     ctypes.c_void_p]
+    loop.restype = ctypes.c_double
+    stream = torch.cuda.current_stream(d.dev).cuda_stream
+    w = torch.zeros((8, 1024), dtype=torch.float64, device=d.dev)
+    wh = torch.empty((9, 1024), dtype=torch.float64, device=d.dev)
+    loop(0, 8, w.data_ptr(), w.data_ptr(), wh.data_ptr(), 1024, 1, 0, 20000, stream)  # clocks up
+    out = {}
+    for algo in ("aca", "sks"):
+        rows = []
+        for n, ref_us in zip(TABLE8_N, TABLE8_ROWS[algo]):
+            src = pkg.fill_uniform(n * 8, SEED, 0, device=d.dev).view(8, n).double()
+            tar = pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(8, n).double()
+            H = torch.empty((9, n), dtype=torch.float64, device=d.dev)
+            f = lambda: pkg.solve(algo, src, tar, normalize=False, layout="soa", out=H)  # noqa
+            for _ in range(20):
+                f()
+            _, ms1 = timed_region(d, f, 20)
+            loops = max(20, min(20000, int(300.0 / max(ms1, 1e-3))))
+            _, ms = timed_region(d, f, loops)
+            native = loop(0 if algo == "aca" else 1, 8, src.data_ptr(), tar.data_ptr(),
+                          H.data_ptr(), n, 1, 0, loops, stream)
+            g = graph_of(d, f, 100)
+            _, ms_g = timed_region(d, g.replay, 5)
+            del g
+            rows.append({"n": n, "native_us_per_launch": round(native, 2),
+                         "python_us_per_launch": round(ms * 1e3, 2),
+                         "graph_us_per_launch": round(ms_g * 1e3 / 100, 2),
+                         "table8_us": ref_us, "speedup_vs_table8": round(ref_us / native, 2)})
+        out[algo] = rows
+    return out
 
 
 def reference_layout(d: Dist, pkg):
@@ -549,6 +595,7 @@ def main():
         }
         del bs_h, bt_h, Hb
         line["reference_layout"] = reference_layout(d, pkg)
+        line["table8_sweep"] = table8_sweep(d, pkg)
         line["ransac"] = ransac_section(d, pkg)
         line["host_boundary"] = host_boundary_section(d, pkg, n)
         # f64 AoS (sks::runKernel_ACA_double semantics) on the same inputs

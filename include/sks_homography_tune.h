@@ -40,6 +40,11 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
 
+/* cal_ACA's launch loop in native code: `loops` back-to-back C-ABI launches, timed with
+ * HIP events on `stream`; returns us per launch or -(hipError_t).  elem 4 / 8 bytes. */
+double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
+                           int64_t n, int layout, int flags, int loops, void* stream);
+
 int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream);

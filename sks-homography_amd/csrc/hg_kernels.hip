@@ -109,6 +109,13 @@ constexpr int kErrInvalid = (int)hipErrorInvalidValue;
 template <typename T>
 constexpr int kAosP = sizeof(T) == 4 ? 2 : 1;
 constexpr int kAosFlags = kNtLoad | kNtStore | kLdsLoad | kLdsDma;
+// Batches whose bytes (in + out) fit the 256 MB Infinity Cache (MALL) with room to spare
+// use the default cache policy instead: a caller that re-reads or just produced them
+// (back-to-back launches, a pipeline) hits the MALL -- 7 % faster at 1-2 M f32 AoS, 11 %
+// at 1 M f64 SoA; beyond it non-temporal wins (10 M: 154 vs 171 us).  Same arithmetic,
+// same bits (tools/kbench.py, tools/kbench_soa_small.py).
+constexpr int kAosCachedFlags = kLdsLoad | kLdsDma;
+constexpr int64_t kMallResidentBytes = 200000000;
 constexpr int kRectP = 1;  // TensorACA problems per lane (tools/kbench_rect.py, profiles/r01/kbench_rect.json)
 constexpr int kSoaG = 1;  // 16-B groups per lane (SoA path)
 
@@ -126,18 +133,25 @@ inline int launch_status() { return (int)hipGetLastError(); }
 
 template <int ALGO, bool NORM, typename T>
 int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipStream_t s) {
+    const bool cached = n <= kMallResidentBytes / (25 * (int64_t)sizeof(T));  // 25 values/problem
     if (layout == HG_LAYOUT_SOA) {
         constexpr int V = 16 / sizeof(T);
-        if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H))
-            solve_soa_vec<ALGO, NORM, T, kSoaG, false>
-                <<<(unsigned)soa_grid<kSoaG, false>(n / V), kBlock, 0, s>>>(src, tar, H, n);
-        else
+        if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H)) {
+            const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
+            if (cached)
+                solve_soa_vec<ALGO, NORM, T, kSoaG, false, false><<<g, kBlock, 0, s>>>(src, tar, H, n);
+            else
+                solve_soa_vec<ALGO, NORM, T, kSoaG, false, true><<<g, kBlock, 0, s>>>(src, tar, H, n);
+        } else
             solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {
         constexpr int P = kAosP<T>;
         const int64_t blocks = aos_grid<T, P, kAosFlags>(n);
         if (blocks > 0x7fffffffLL) return kErrInvalid;
-        solve_aos<ALGO, NORM, T, P, kAosFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
+        if (cached)
+            solve_aos<ALGO, NORM, T, P, kAosCachedFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
+        else
+            solve_aos<ALGO, NORM, T, P, kAosFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
     } else {
         solve_generic<ALGO, NORM, T, false><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     }

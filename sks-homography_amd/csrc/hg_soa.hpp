@@ -11,7 +11,7 @@
 
 namespace hg {
 
-template <int ALGO, bool NORM, typename T, int G, bool PERSIST>
+template <int ALGO, bool NORM, typename T, int G, bool PERSIST, bool NT = true>
 __global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ src,
                                                         const T* __restrict__ tar,
                                                         T* __restrict__ H, int64_t n) {
@@ -27,8 +27,8 @@ __global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ sr
             if (q < groups) {
 #pragma unroll
                 for (int k = 0; k < 8; ++k) {
-                    u32x4 a = ld16<true>(src + (int64_t)k * n + q * V);
-                    u32x4 b = ld16<true>(tar + (int64_t)k * n + q * V);
+                    u32x4 a = ld16<NT>(src + (int64_t)k * n + q * V);
+                    u32x4 b = ld16<NT>(tar + (int64_t)k * n + q * V);
                     __builtin_memcpy(s[g][k], &a, 16);
                     __builtin_memcpy(t[g][k], &b, 16);
                 }
@@ -53,7 +53,7 @@ __global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ sr
                 for (int v = 0; v < V; ++v) o[v] = h[v][k];
                 u32x4 w;
                 __builtin_memcpy(&w, o, 16);
-                st16<true>(H + (int64_t)k * n + q * V, w);
+                st16<NT>(H + (int64_t)k * n + q * V, w);
             }
         }
     }

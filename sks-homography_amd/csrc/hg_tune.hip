@@ -70,6 +70,7 @@ const Variant kVariants[] = {
     {"P2 nt lds-dma xcd-contig", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
     {"P1 nt lds-dma xcd-contig", launch_variant<1, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
     {"P4 nt lds-dma xcd-contig", launch_variant<4, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
+    {"P2 lds-dma plain (cached)", launch_variant<2, kLdsLoad | kLdsDma>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.
@@ -107,7 +108,7 @@ __global__ __launch_bounds__(kBlock) void copy_dma(const char* __restrict__ src,
                    *reinterpret_cast<const u32x4*>(smem[wave] + 16 * (c * 64 + lane)));
 }
 
-template <typename T, int G, bool PERSIST>
+template <typename T, int G, bool PERSIST, bool NT = true>
 int launch_soa(int algo, const void* s, const void* t, void* H, int64_t n, int per_cu,
                hipStream_t st) {
     constexpr int V = 16 / sizeof(T);
@@ -116,8 +117,8 @@ int launch_soa(int algo, const void* s, const void* t, void* H, int64_t n, int p
     const T* a = (const T*)s;
     const T* b = (const T*)t;
     T* h = (T*)H;
-    if (algo == 0) solve_soa_vec<kACA, false, T, G, PERSIST><<<g, kBlock, 0, st>>>(a, b, h, n);
-    else solve_soa_vec<kSKS, false, T, G, PERSIST><<<g, kBlock, 0, st>>>(a, b, h, n);
+    if (algo == 0) solve_soa_vec<kACA, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else solve_soa_vec<kSKS, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
     return (int)hipGetLastError();
 }
 
@@ -134,6 +135,8 @@ const SoaVariant kSoaVariants[] = {
     {"f32 G1 one-shot (shipped)", launch_soa<float, 1, false>},
     {"f32 G2 one-shot", launch_soa<float, 2, false>},
     {"f32 G1 persist", launch_soa<float, 1, true>},
+    {"f64 G1 one-shot plain (cached) ld/st", launch_soa<double, 1, false, false>},
+    {"f32 G1 one-shot plain (cached) ld/st", launch_soa<float, 1, false, false>},
 };
 
 }  // namespace
@@ -206,6 +209,53 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
+}
+
+__global__ void empty_kernel() {}
+
+// cal_ACA's timing loop (GPU_Runtime Test.cu:1183-1200) in native code: `loops` back-to-
+// back launches of the C-ABI solver from a C++ loop, bracketed by HIP events on
+// `stream`.  Returns microseconds per launch, or -(hipError_t) on failure.  algo 0 ACA,
+// 1 SKS; elem 4 (float) or 8 (double).
+double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
+                           int64_t n, int layout, int flags, int loops, void* stream) {
+    if (algo < 0 || algo > 2 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    auto launch = [&]() -> int {
+        if (algo == 2) {  // the floor: an empty kernel, raw launch, no checks
+            empty_kernel<<<1, kWave, 0, st>>>();
+            return 0;
+        }
+        if (elem == 4) {
+            const auto* s = static_cast<const float*>(src);
+            const auto* t = static_cast<const float*>(tar);
+            auto* h = static_cast<float*>(H);
+            return algo == 0 ? hg_aca_f32(s, t, h, n, layout, flags, stream)
+                             : hg_sks_f32(s, t, h, n, layout, flags, stream);
+        }
+        const auto* s = static_cast<const double*>(src);
+        const auto* t = static_cast<const double*>(tar);
+        auto* h = static_cast<double*>(H);
+        return algo == 0 ? hg_aca_f64(s, t, h, n, layout, flags, stream)
+                         : hg_sks_f64(s, t, h, n, layout, flags, stream);
+    };
+    hipEvent_t e0, e1;
+    if (hipEventCreate(&e0) != hipSuccess) return -1.0;
+    if (hipEventCreate(&e1) != hipSuccess) return -1.0;
+    int rc = 0;
+    for (int i = 0; i < 1 + loops / 8 && rc == 0; ++i) rc = launch();  // warm
+    if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = 1;
+    float ms = 0.f;
+    if (rc == 0) {
+        (void)hipEventRecord(e0, st);
+        for (int i = 0; i < loops && rc == 0; ++i) rc = launch();
+        (void)hipEventRecord(e1, st);
+        (void)hipEventSynchronize(e1);
+        (void)hipEventElapsedTime(&ms, e0, e1);
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return rc ? -(double)rc : (double)ms * 1e3 / loops;
 }
 
 }  // extern "C"
