@@ -184,15 +184,22 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
     constexpr int P = kRectP;
     const int64_t blocks = ceil_div(B, (int64_t)kBlock * P);
     if (blocks > 0x7fffffffLL) return kErrInvalid;
-    if (SCALAR && is_unit_ratio(dv) && aligned16(src) && aligned16(tar) && aligned16(H))
-        tensor_aca_rect_kernel<P, true, true, true>
-            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
-    else if (aligned16(src) && aligned16(tar) && aligned16(H))
-        tensor_aca_rect_kernel<P, true, SCALAR>
-            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
-    else
-        tensor_aca_rect_kernel<P, false, SCALAR>
-            <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    // 132 B actually move per problem (the whole 48-B src record is fetched); cache
+    // policy by size as launch_solver (tools/kbench_rect.py: 1 M 23.2 -> 21.4 us cached,
+    // 16 M 351 nt vs 397 cached)
+    const bool cached = B * 132 <= kMallResidentBytes;
+    const bool vec = aligned16(src) && aligned16(tar) && aligned16(H);
+    const unsigned g = (unsigned)blocks;
+#define HG_RECT(SQ, NT) \
+    tensor_aca_rect_kernel<P, true, SCALAR, SQ, NT><<<g, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv)
+    if (vec && SCALAR && is_unit_ratio(dv)) {
+        if (cached) HG_RECT(true, false); else HG_RECT(true, true);
+    } else if (vec) {
+        if (cached) HG_RECT(false, false); else HG_RECT(false, true);
+    } else {  // unaligned views: per-lane loads and stores
+        tensor_aca_rect_kernel<P, false, SCALAR><<<g, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+    }
+#undef HG_RECT
     return launch_status();
 }
 
@@ -297,12 +304,17 @@ int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* 
     const bool vec = hg::aligned16(corner) && hg::aligned16(offsets) && hg::aligned16(H);
     // width / height == 1 exactly iff the two are equal, finite and non-zero
     const bool square = width == height && width != 0.f && std::isfinite(width);
-#define HG_OFFSETS(V, SQ)                                                                     \
-    hg::tensor_aca_offsets_kernel<P, V, SQ><<<(unsigned)blocks, hg::kBlock, 0, s>>>(          \
+    const bool cached = B * 76 <= hg::kMallResidentBytes;  // policy by size, as launch_solver
+#define HG_OFFSETS(V, SQ, NT)                                                                 \
+    hg::tensor_aca_offsets_kernel<P, V, SQ, NT><<<(unsigned)blocks, hg::kBlock, 0, s>>>(      \
         corner, offsets, H, B, width, height)
-    if (vec && square) HG_OFFSETS(true, true);
-    else if (vec) HG_OFFSETS(true, false);
-    else HG_OFFSETS(false, false);  // unaligned views: per-lane loads and stores
+    if (vec && square) {
+        if (cached) HG_OFFSETS(true, true, false); else HG_OFFSETS(true, true, true);
+    } else if (vec) {
+        if (cached) HG_OFFSETS(true, false, false); else HG_OFFSETS(true, false, true);
+    } else {
+        HG_OFFSETS(false, false, true);  // unaligned views: per-lane loads and stores
+    }
 #undef HG_OFFSETS
     return hg::launch_status();
 }

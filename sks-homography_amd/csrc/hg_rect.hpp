@@ -20,7 +20,7 @@ namespace hg {
 // loads per lane (offsets 0 and 16 of the 48-B src record) issued before the DMA
 // wait.  H is written through the LDS-staged 16-B store.  Ragged/unaligned tiles
 // use per-lane loads and stores.
-template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false>
+template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false, bool NT = true>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -45,12 +45,12 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int64_t p = base + j * kWave + lane;
-            mx[j] = __builtin_nontemporal_load(src + p * 12 + 0);
-            my[j] = __builtin_nontemporal_load(src + p * 12 + 4);
+            mx[j] = NT ? __builtin_nontemporal_load(src + p * 12 + 0) : src[p * 12 + 0];
+            my[j] = NT ? __builtin_nontemporal_load(src + p * 12 + 4) : src[p * 12 + 4];
         }
         const char* const g[1] = {reinterpret_cast<const char*>(tar + base * 12)};
         char* const l[1] = {lds};
-        slabs_to_lds<kSlab, 1, true, true>(g, l, lane);
+        slabs_to_lds<kSlab, 1, true, NT>(g, l, lane);
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             float tr[12];
@@ -58,7 +58,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
             tensor_aca_rect_solve<SQUARE>(tr, mx[j], my[j], scale, div, h[j]);
         }
         wave_lds_sync();
-        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        store_rows9_staged<float, P, NT>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
         return;
     }
 #pragma unroll
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
 // Compact TensorACA: corner (B,2) + offsets (B,4,2) -> H (B,3,3) = 8 + 32 + 36 B per
 // problem instead of the (B,3,4) tensors' 48 + 48 + 36.  Full tiles: both slabs by
 // LDS-DMA (P = 1: 512 B of corners + 2 KiB of offsets per wave), staged 16-B H stores.
-template <int P, bool VEC, bool SQUARE>
+template <int P, bool VEC, bool SQUARE, bool NT = true>
 __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
     const float* __restrict__ corner, const float* __restrict__ offsets, float* __restrict__ H,
     int64_t B, float w, float h) {
@@ -128,8 +128,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
     char* lds = smem[wave];
     float hm[P][9];
     if (VEC && base + kTile <= B) {
-        dma_slab_issue<kCorner, true>(reinterpret_cast<const char*>(corner + base * 2), lds, lane);
-        dma_slab_issue<kOff, true>(reinterpret_cast<const char*>(offsets + base * 8),
+        dma_slab_issue<kCorner, NT>(reinterpret_cast<const char*>(corner + base * 2), lds, lane);
+        dma_slab_issue<kOff, NT>(reinterpret_cast<const char*>(offsets + base * 8),
                                    lds + kCorner, lane);
         dma_wait_sync();
 #pragma unroll
@@ -142,7 +142,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_kernel(
             tensor_aca_rect_solve<SQUARE>(tr, c[0], c[1], w, div, hm[j]);
         }
         wave_lds_sync();
-        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), hm, lds, lane);
+        store_rows9_staged<float, P, NT>(reinterpret_cast<char*>(H + base * 9), hm, lds, lane);
         return;
     }
 #pragma unroll

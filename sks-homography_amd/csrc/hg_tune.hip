@@ -206,6 +206,8 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
         case 3: tensor_aca_offsets_kernel<1, true, false><<<blocks(1), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
         case 4: tensor_aca_offsets_kernel<2, true, false><<<blocks(2), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
         case 5: tensor_aca_offsets_kernel<4, true, false><<<blocks(4), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
+        case 6: tensor_aca_rect_kernel<1, true, true, false, false><<<blocks(1), kBlock, 0, st>>>(src, tar, H, B, nullptr, nullptr, a, b); break;
+        case 7: tensor_aca_offsets_kernel<1, true, false, false><<<blocks(1), kBlock, 0, st>>>(src, tar, H, B, a, b); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
@@ -243,7 +245,8 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
     if (hipEventCreate(&e0) != hipSuccess) return -1.0;
     if (hipEventCreate(&e1) != hipSuccess) return -1.0;
     int rc = 0;
-    for (int i = 0; i < 1 + loops / 8 && rc == 0; ++i) rc = launch();  // warm
+    // warm as long as the timed run: after host-bound work the clocks need ~100 ms to ramp
+    for (int i = 0; i < loops && rc == 0; ++i) rc = launch();
     if (rc == 0 && hipStreamSynchronize(st) != hipSuccess) rc = 1;
     float ms = 0.f;
     if (rc == 0) {

@@ -18,7 +18,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 NAMES = ["rect P1 (shipped)", "rect P2", "rect P4", "offsets P1 (shipped)", "offsets P2",
-         "offsets P4"]
+         "offsets P4", "rect P1 cached", "offsets P1 cached"]
 
 
 def main():
@@ -42,8 +42,9 @@ def main():
         graphs, ok = {}, {}
         s = torch.cuda.Stream(dev)
         for v, name in enumerate(NAMES):
-            a, b = (src, tar) if v < 3 else (corner, offs)
-            wb = (128.0, 1.0) if v < 3 else (128.0, 128.0)
+            is_rect = name.startswith("rect")
+            a, b = (src, tar) if is_rect else (corner, offs)
+            wb = (128.0, 1.0) if is_rect else (128.0, 128.0)
 
             def launch(v=v, a=a, b=b, wb=wb):
                 rc = f(v, a.data_ptr(), b.data_ptr(), H.data_ptr(), B, wb[0], wb[1],
@@ -54,7 +55,7 @@ def main():
             launch()
             torch.cuda.synchronize()
             ok[name] = bool(torch.equal(H.view(torch.int32),
-                                        (want_r if v < 3 else want_o).view(torch.int32)))
+                                        (want_r if is_rect else want_o).view(torch.int32)))
             s.wait_stream(torch.cuda.current_stream(dev))
             with torch.cuda.stream(s):
                 g = torch.cuda.CUDAGraph()
