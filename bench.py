@@ -42,7 +42,7 @@ def parse():
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-extras", action="store_true", help="ACA headline only")
     ap.add_argument("--no-gather", action="store_true",
-                    help="N>1: skip the timed gather of every H block to rank 0")
+                    help="N>1: skip the timed split (scatter) / gather through rank 0")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
@@ -419,24 +419,53 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     }
 
 
-def gather_section(d: Dist, pkg, H, n: int, n_total: int, step_ms: float):
-    """SURVEY 8(e)'s second number: every rank's H block gathered to rank 0 (paired
-    send/recv; RCCL over xGMI, bound by rank 0's ingress), outside the timed steps.
-    Rank 0 then re-solves a slice of the last rank's block from regenerated inputs and
-    checks the gathered bits.  Over gloo (one-GPU rehearsal) the blocks go via the host."""
-    blk = H if d.backend == "nccl" else H.cpu()
-    small = blk[:1024].contiguous()
-    pkg.gather_blocks(small, 1024 * d.world, d.world, d.rank)  # open the p2p connections
+def split_gather_section(d: Dist, pkg, src, tar, H, n: int, n_total: int, step_ms: float):
+    """SURVEY 8(e)'s second number: the split / gather a caller whose batch lives on one
+    rank pays, outside the timed steps.  Split: rank 0 holds the whole (n_total, 8)
+    src/tar and scatter_blocks hands each rank its block (paired send/recv; RCCL over
+    xGMI, bound by rank 0's egress); every rank checks the bytes it received against the
+    block it generated itself.  Gather: every H block to rank 0 (ingress-bound); rank 0
+    re-solves a slice of the last rank's block and checks the gathered bits.  Over gloo
+    (one-GPU rehearsal) the blocks go through the host."""
+    host = d.backend != "nccl"
+    mv = (lambda t: t.cpu()) if host else (lambda t: t)  # noqa: E731
+    full_s = full_t = None
+    if d.rank == 0:
+        full_s = mv(pkg.fill_uniform(n_total * 8, SEED, 0, device=d.dev).view(n_total, 8))
+        full_t = mv(pkg.fill_uniform(n_total * 8, SEED, n_total * 8, device=d.dev).view(n_total, 8))
+    like = mv(src[:1])
+    warm = pkg.scatter_blocks(full_s[:1024 * d.world] if d.rank == 0 else None, 1024 * d.world,
+                              d.world, d.rank, like)  # open the p2p connections
+    del warm
+    torch.cuda.synchronize(d.dev)
+    d.barrier()
+    t0 = time.perf_counter()
+    got_s = pkg.scatter_blocks(full_s, n_total, d.world, d.rank, like)
+    got_t = pkg.scatter_blocks(full_t, n_total, d.world, d.rank, like)
+    torch.cuda.synchronize(d.dev)
+    d.barrier()
+    t_split = d.max(time.perf_counter() - t0)
+    ok = (torch.equal(got_s.to(d.dev).view(torch.int32), src.view(torch.int32)) and
+          torch.equal(got_t.to(d.dev).view(torch.int32), tar.view(torch.int32)))
+    split_ok = d.max(0.0 if ok else 1.0) == 0.0
+    del full_s, full_t, got_s, got_t
+
+    blk = mv(H)
+    pkg.gather_blocks(blk[:1024].contiguous(), 1024 * d.world, d.world, d.rank)
     torch.cuda.synchronize(d.dev)
     d.barrier()
     t0 = time.perf_counter()
     full = pkg.gather_blocks(blk, n_total, d.world, d.rank)
     torch.cuda.synchronize(d.dev)
     d.barrier()
-    secs = d.max(time.perf_counter() - t0)
-    out = {"gather_to_rank0_ms": round(secs * 1e3, 3), "gathered_bytes": n_total * 36,
-           "rank0_ingress_gbps": round((n_total - n) * 36 / secs / 1e9, 1),
-           "end_to_end_M_homographies_per_s": round(n_total / (secs + step_ms * 1e-3) / 1e6, 1)}
+    t_gather = d.max(time.perf_counter() - t0)
+    out = {"split_from_rank0_ms": round(t_split * 1e3, 3), "split_bytes": n_total * 64,
+           "rank0_egress_gbps": round((n_total - n) * 64 / t_split / 1e9, 1),
+           "split_verified": bool(split_ok),
+           "gather_to_rank0_ms": round(t_gather * 1e3, 3), "gathered_bytes": n_total * 36,
+           "rank0_ingress_gbps": round((n_total - n) * 36 / t_gather / 1e9, 1),
+           "end_to_end_M_homographies_per_s": round(
+               n_total / (t_split + step_ms * 1e-3 + t_gather) / 1e6, 1)}
     if d.rank == 0:
         lo, m = (d.world - 1) * n, min(n, 1 << 20)
         s = pkg.fill_uniform(m * 8, SEED, lo * 8, device=d.dev).view(m, 8)
@@ -612,7 +641,8 @@ def main():
 
     if d.world > 1 and not args.no_gather:
         run("aca")()
-        line["gather"] = gather_section(d, pkg, H, n, n_total, wall / args.steps * 1e3)
+        line["split_gather"] = split_gather_section(d, pkg, src, tar, H, n, n_total,
+                                                    wall / args.steps * 1e3)
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(min(n, 10_000_000))

@@ -9,7 +9,7 @@ Layers:
   csrc/                      HIP kernels for gfx950 + the C ABI + the sks:: API
   ops.py                     torch-facing wrappers, torch.ops.sks_amd.*
   reference_api.py           TensorACA_rect / ACA_vanilla / getInput / adjust mirrors
-  shard.py                   per-GPU block sharding, optional RCCL gather
+  shard.py                   per-GPU block sharding, optional RCCL split / gather
   ransac.py                  fused hypothesis sampling + solve + inlier scoring
 """
 from __future__ import annotations
@@ -22,7 +22,7 @@ from .ops import (aca, fill_uniform, sks, solve, stream_copy, tensor_aca_rect,
 from .ransac import RansacResult, fill_bits, ransac, read_points, sample_solve
 from .ransac import score as ransac_score
 from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
-from .shard import gather_blocks, shard_range
+from .shard import gather_blocks, scatter_blocks, shard_range
 
 BYTES_PER_PROBLEM = {"f32": 64 + 36, "f64": 128 + 72}   # algorithmic HBM bytes per H
 RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H
@@ -33,6 +33,6 @@ __all__ = [
     "fill_uniform", "sample_solve", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
     "read_points",
     "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
-    "gather_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
+    "gather_blocks", "scatter_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
     "HG_FLAG_NORMALIZE", "BYTES_PER_PROBLEM", "RECT_BYTES_PER_PROBLEM",
 ]

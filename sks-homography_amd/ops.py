@@ -121,9 +121,10 @@ Scalar = Union[float, int, torch.Tensor]
 
 
 def _dev_scalar(x, dev: torch.device) -> torch.Tensor:
-    """A batch-uniform scalar as a float32 tensor on `dev` (no copy when it already is
-    one -- the reference keeps scale/div in (1,)-shaped tensors, .py:33-35)."""
-    if isinstance(x, torch.Tensor) and x.dtype == torch.float32 and x.device == dev:
+    """A batch-uniform scalar as a float32 GPU tensor (no copy when it already is one --
+    the reference keeps scale/div in (1,)-shaped tensors, .py:33-35; the op checks that
+    it sits on the batch's device)."""
+    if type(x) is torch.Tensor and x.dtype is torch.float32 and x.is_cuda:
         return x
     return torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)[:1]
 
@@ -144,8 +145,7 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     Runs torch.ops.sks_amd.tensor_aca_rect (native, csrc/hg_torch_ops.cpp); with tensor
     scale/div and no ``out`` it is differentiable in all four inputs.
     """
-    _gpu_only(src)
-    _gpu_only(tar)
+    _gpu_only(tar)  # the op checks that src (and out) share tar's device
     if isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):
         sc, dv = _dev_scalar(scale, tar.device), _dev_scalar(div, tar.device)
         if out is None:
@@ -175,8 +175,7 @@ def tensor_aca_offsets(corner: torch.Tensor, offsets: torch.Tensor, width: float
     as building the (B,3,4) tensors and calling tensor_aca_rect(scale=width,
     div=width/height).  Returns the unnormalised (B,3,3) H; differentiable without
     ``out``."""
-    _gpu_only(corner)
-    _gpu_only(offsets)
+    _gpu_only(offsets)  # the op checks that corner (and out) share its device
     if out is None:
         return _OPS.tensor_aca_offsets.default(corner, offsets, float(width), float(height))
     return _OPS.tensor_aca_offsets.out(corner, offsets, float(width), float(height), out=out)

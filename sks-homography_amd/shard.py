@@ -4,9 +4,10 @@ Problems are independent, so a batch of N splits into
 contiguous rank-major blocks and every rank solves its own block with no data-path
 collective.  Inputs are generated on each rank from the counter-based stream
 (offset = the block's first element), so no scatter is needed either.  The only
-collective is the optional gather of all H blocks to one rank over RCCL
-(torch.distributed "nccl" == RCCL on ROCm), which is what a caller that wants every
-result in one place pays for -- reported separately by bench.py.
+collectives are the optional split / gather a caller with host- or rank-0-resident data
+needs: scatter_blocks hands each rank its block of one rank's batch, gather_blocks
+collects every H block on one rank, both as paired send/recv over RCCL
+(torch.distributed "nccl" == RCCL on ROCm) -- reported separately by bench.py.
 """
 from __future__ import annotations
 
@@ -54,3 +55,29 @@ def gather_blocks(block: torch.Tensor, n_total: int, world: int, rank: int, dst:
         for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, block.contiguous(), dst, group)]):
             w.wait()
     return None
+
+
+def scatter_blocks(full: Optional[torch.Tensor], n_total: int, world: int, rank: int,
+                   like: torch.Tensor, src: int = 0, group=None) -> torch.Tensor:
+    """Splits ``full`` ((n_total, ...) on rank ``src``; None elsewhere) into the contiguous
+    rank-major blocks of shard_range and returns this rank's block (shaped like
+    ``like``'s rows).  Paired send/recv: rank ``src``'s egress is the bound."""
+    import torch.distributed as dist
+
+    lo, hi = shard_range(n_total, world, rank)
+    if world == 1:
+        return full
+    if rank == src:
+        ops: List = []
+        for r in range(world):
+            rlo, rhi = shard_range(n_total, world, r)
+            if r != src and rhi > rlo:
+                ops.append(dist.P2POp(dist.isend, full[rlo:rhi].contiguous(), r, group))
+        for w in dist.batch_isend_irecv(ops) if ops else []:
+            w.wait()
+        return full[lo:hi]
+    block = torch.empty((hi - lo,) + tuple(like.shape[1:]), dtype=like.dtype, device=like.device)
+    if hi > lo:
+        for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, block, src, group)]):
+            w.wait()
+    return block

@@ -1,4 +1,5 @@
-"""Multi-GPU path on CPU: sharding arithmetic and the gather, world_size 2 over gloo."""
+"""Multi-GPU path on CPU: sharding arithmetic, the split (scatter) and the gather, world
+sizes 2 and 3 over gloo."""
 import os
 import socket
 
@@ -44,19 +45,26 @@ def _worker(rank, world, port, n_total, q):
     # stand-in for the rank's H block: a deterministic function of the global index
     block = torch.arange(lo, hi, dtype=torch.float32).repeat_interleave(9).view(-1, 9)
     full = pkg.gather_blocks(block, n_total, world, rank, dst=0)
+    # the split: rank 0's whole (n_total, 8) input -> each rank's contiguous block
+    src_full = (torch.arange(n_total * 8, dtype=torch.float32).view(n_total, 8)
+                if rank == 0 else None)
+    like = torch.empty((0, 8), dtype=torch.float32)
+    mine = pkg.scatter_blocks(src_full, n_total, world, rank, like, src=0)
+    scatter_ok = bool(torch.equal(mine, torch.arange(lo * 8, hi * 8, dtype=torch.float32)
+                                  .view(hi - lo, 8)))
     # max-over-ranks timing reduction used by bench.py
     t = torch.tensor([float(rank + 1)], dtype=torch.float64)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     if rank == 0:
         want = torch.arange(n_total, dtype=torch.float32).repeat_interleave(9).view(-1, 9)
-        q.put((bool(torch.equal(full, want)), float(t.item())))
+        q.put((bool(torch.equal(full, want)) and scatter_ok, float(t.item())))
     else:
-        q.put((full is None, float(t.item())))
+        q.put((full is None and scatter_ok, float(t.item())))
     dist.destroy_process_group()
 
 
 @pytest.mark.parametrize("world,n_total", [(2, 1001), (3, 10)])
-def test_gather_blocks_gloo(world, n_total):
+def test_scatter_gather_blocks_gloo(world, n_total):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
