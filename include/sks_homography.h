@@ -89,8 +89,9 @@ int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float*
 /* Backward of hg_tensor_aca_rect_f32 (the gradients ATen autograd gives the
  * reference's composed TensorACA_rect, Modules_Runtime_Test.py:294-302).  grad_H:
  * (B,3,3) dL/dH.  Writes grad_tar (B,3,4); grad_src (B,3,4, only [0][0] and [1][0]
- * non-zero) when non-NULL; grad_scale_div (B,2) per-problem partials of dL/dscale and
- * dL/ddiv when non-NULL (the caller sums them).  scale, div: device pointers. */
+ * non-zero) when non-NULL; grad_scale_div (2,B) per-problem partials -- row 0 of
+ * dL/dscale, row 1 of dL/ddiv -- when non-NULL (the caller sums each row).  scale, div:
+ * device pointers. */
 int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
                                     int64_t B, const float* scale, const float* div,
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
@@ -153,6 +154,12 @@ int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int
                      void* stream);
 int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, int flags,
                      void* stream);
+
+/* Deterministic sums of the rows of x (rows, cols), row-major, into out[rows]: a fixed
+ * two-level order (chunks of 4096 in order, folded by halving strides), so the bits do
+ * not depend on timing.  x is OVERWRITTEN (used as the scratch for the chunk sums).
+ * rows <= 65535.  Reduces hg_tensor_aca_rect_backward_f32's (2,B) partials. */
+int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stream);
 
 /* Device-to-device streaming copy (float4) used by bench.py as the measured
  * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */

@@ -153,6 +153,26 @@ __device__ __forceinline__ void dma_wait_sync() {
 // Writes a wave's 64*P rows of 9 T (36/72-B rows, not 16-B aligned per lane) to
 // the contiguous slab `out`: rows are staged in LDS at a 9-element stride (odd dword
 // stride: conflict-free ds_write_b32), then every lane stores consecutive 16-B chunks.
+// This wave's 64 rows of kFloats floats (row l = lane l's `v`) leave as ONE contiguous
+// slab: 16-B ds_writes of each row into LDS, then lane-consecutive 16-B global stores.
+// kFloats % 4 == 0 (32-B and 48-B rows: the backward's gradient records).
+template <int kFloats, bool NT>
+__device__ __forceinline__ void store_rows_staged(char* __restrict__ out, const float (&v)[kFloats],
+                                                  char* lds, int lane) {
+    static_assert(kFloats % 4 == 0, "rows of whole 16-B granules");
+#pragma unroll
+    for (int c = 0; c < kFloats / 4; ++c)
+        __builtin_memcpy(lds + (lane * kFloats + 4 * c) * 4, &v[4 * c], 16);
+    wave_lds_sync();
+    constexpr int kChunks = kWave * kFloats / 4;
+#pragma unroll
+    for (int c = 0; c < kChunks / kWave; ++c) {
+        const int chunk = c * kWave + lane;
+        st16<NT>(out + 16 * chunk, *reinterpret_cast<const u32x4*>(lds + 16 * chunk));
+    }
+    wave_lds_sync();
+}
+
 template <typename T, int P, bool NT>
 __device__ __forceinline__ void store_rows9_staged(char* __restrict__ out, const T (&h)[P][9],
                                                    char* lds, int lane) {

@@ -85,6 +85,50 @@ __global__ __launch_bounds__(kWave) void solve_one_kernel(Quad<T> q, T* __restri
     for (int k = 0; k < 9; ++k) H[k] = h[k];
 }
 
+// Deterministic row sums, in place (hg_sum_rows_f32).  Pass 1: block (c, r) sums chunk c
+// = x[r][c*kSumChunk, (c+1)*kSumChunk) -- thread t adds elements c*kSumChunk + t + 256 i,
+// i = 0, 1, ... in order (out-of-range elements count as +0), then the 256 sums fold by
+// halving strides (v[t] += v[t + s], s = 128 ... 1) -- and writes the chunk's sum over the
+// chunk's first element, which no other block reads.  Pass 2: one block per row folds
+// the chunk sums the same way.  Fixed order, so the result is bit-reproducible (and
+// restated in numpy by tests/test_gpu_parity.py).
+constexpr int kSumChunk = kBlock * 16;
+
+__device__ __forceinline__ float block_fold(float v, float* red) {
+    red[threadIdx.x] = v;
+    __syncthreads();
+#pragma unroll
+    for (int s = kBlock / 2; s > 0; s >>= 1) {
+        if (threadIdx.x < s) red[threadIdx.x] = red[threadIdx.x] + red[threadIdx.x + s];
+        __syncthreads();
+    }
+    return red[0];
+}
+
+__global__ __launch_bounds__(kBlock) void sum_rows_pass1(float* __restrict__ x, int64_t cols) {
+    __shared__ float red[kBlock];
+    float* row = x + (int64_t)blockIdx.y * cols;
+    const int64_t c0 = (int64_t)blockIdx.x * kSumChunk;
+    float v = 0.f;
+#pragma unroll
+    for (int i = 0; i < kSumChunk / kBlock; ++i) {
+        const int64_t e = c0 + threadIdx.x + (int64_t)i * kBlock;
+        v = v + (e < cols ? row[e] : 0.f);
+    }
+    const float sum = block_fold(v, red);  // ends with every read of the chunk done
+    if (threadIdx.x == 0) row[c0] = sum;
+}
+
+__global__ __launch_bounds__(kBlock) void sum_rows_pass2(const float* __restrict__ x, int64_t cols,
+                                                         int64_t chunks, float* __restrict__ out) {
+    __shared__ float red[kBlock];
+    const float* row = x + (int64_t)blockIdx.x * cols;
+    float v = 0.f;
+    for (int64_t c = threadIdx.x; c < chunks; c += kBlock) v = v + row[c * kSumChunk];
+    const float sum = block_fold(v, red);
+    if (threadIdx.x == 0) out[blockIdx.x] = sum;
+}
+
 // Streaming copy, 16 B per lane per iteration (bandwidth yardstick).
 __global__ __launch_bounds__(kBlock) void stream_copy_kernel(const u32x4* __restrict__ src,
                                                              u32x4* __restrict__ dst,
@@ -279,8 +323,31 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
     if (B == 0) return 0;
     if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const unsigned g = hg::generic_grid(B);
     const bool ws = grad_src != nullptr, wd = grad_scale_div != nullptr;
+    using hg::aligned16;
+    if (aligned16(src) && aligned16(tar) && aligned16(grad_H) && aligned16(grad_tar) &&
+        (!ws || aligned16(grad_src))) {
+        // staged form (tools/kbench_bwd.py); cache policy by size as the forward
+        const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
+        const bool nt = B * 232 > hg::kMallResidentBytes;
+#define HG_RB(A, Bf, NT)                                                                      \
+    hg::tensor_aca_rect_backward_staged<A, Bf, NT><<<g, hg::kBlock, 0, s>>>(                  \
+        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
+        if (nt) {
+            if (ws && wd) HG_RB(true, true, true);
+            else if (ws) HG_RB(true, false, true);
+            else if (wd) HG_RB(false, true, true);
+            else HG_RB(false, false, true);
+        } else {
+            if (ws && wd) HG_RB(true, true, false);
+            else if (ws) HG_RB(true, false, false);
+            else if (wd) HG_RB(false, true, false);
+            else HG_RB(false, false, false);
+        }
+#undef HG_RB
+        return hg::launch_status();
+    }
+    const unsigned g = hg::generic_grid(B);
 #define HG_RECT_BWD(A, Bf)                                                                    \
     hg::tensor_aca_rect_backward_kernel<A, Bf><<<g, hg::kBlock, 0, s>>>(                      \
         src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
@@ -327,6 +394,19 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
     if (B == 0) return 0;
     if (!corner || !offsets || !grad_H || !grad_offsets) return hg::kErrInvalid;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    using hg::aligned16;
+    if (aligned16(corner) && aligned16(offsets) && aligned16(grad_H) && aligned16(grad_offsets) &&
+        (reinterpret_cast<uintptr_t>(grad_corner) & 7u) == 0) {
+        const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
+        const bool nt = B * 116 > hg::kMallResidentBytes;
+#define HG_OB(C, NT)                                                                          \
+    hg::tensor_aca_offsets_backward_staged<C, NT><<<g, hg::kBlock, 0, s>>>(                   \
+        corner, offsets, grad_H, B, width, height, grad_offsets, grad_corner)
+        if (grad_corner) { if (nt) HG_OB(true, true); else HG_OB(true, false); }
+        else { if (nt) HG_OB(false, true); else HG_OB(false, false); }
+#undef HG_OB
+        return hg::launch_status();
+    }
     const unsigned g = hg::generic_grid(B);
     if (grad_corner)
         hg::tensor_aca_offsets_backward_kernel<true><<<g, hg::kBlock, 0, s>>>(
@@ -368,6 +448,19 @@ int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int
 int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, int flags,
                      void* stream) {
     return hg::launch_one<double>(algo, src, tar, H, flags, stream);
+}
+
+int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stream) {
+    if (rows < 0 || cols < 0) return hg::kErrInvalid;
+    if (rows == 0) return 0;
+    if (!out || (cols > 0 && !x) || rows > 65535) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t chunks = hg::ceil_div(cols, hg::kSumChunk);
+    if (chunks > 0x7fffffffLL) return hg::kErrInvalid;
+    if (chunks > 0)
+        hg::sum_rows_pass1<<<dim3((unsigned)chunks, (unsigned)rows), hg::kBlock, 0, s>>>(x, cols);
+    hg::sum_rows_pass2<<<(unsigned)rows, hg::kBlock, 0, s>>>(x, cols, chunks, out);
+    return hg::launch_status();
 }
 
 const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }

@@ -78,7 +78,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
 // ---------------------------------------------------------------------------
 // TensorACA rect backward: one lane per problem, grid-stride.  Writes dL/dtar
 // (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and the
-// per-problem (dL/dscale, dL/ddiv) partials (B,2) that the caller reduces.
+// per-problem dL/dscale and dL/ddiv partials as the rows of a (2,B) array the caller
+// reduces.
 template <bool WANT_SRC, bool WANT_SD>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
@@ -102,8 +103,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
         if constexpr (WANT_SD) {
-            gsd[p * 2 + 0] = gscale;
-            gsd[p * 2 + 1] = gdiv;
+            gsd[p] = gscale;      // (2,B): each row reduces as one contiguous run
+            gsd[B + p] = gdiv;
         }
     }
 }
@@ -189,6 +190,140 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
             g_corner[p * 2] = gmx + (((gt[0] + gt[1]) + gt[2]) + gt[3]);
             g_corner[p * 2 + 1] = gmy + (((gt[4] + gt[5]) + gt[6]) + gt[7]);
         }
+    }
+}
+
+// Staged forms of the two backward kernels (full 64-problem wave tiles, 16-B aligned
+// tensors): the tile's input slabs land in LDS by LDS-DMA, each lane reads its records
+// there, and the gradient rows leave as contiguous slabs (store_rows_staged) instead
+// of 48-B / 32-B per-lane strided accesses.  The ragged tail takes the per-lane code.
+// Same arithmetic (tensor_aca_rect_grad), same bits.
+template <bool WANT_SRC, bool WANT_SD, bool NT>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
+    const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float* __restrict__ gsrc, float* __restrict__ gtar, float* __restrict__ gsd) {
+    constexpr int kTar = kWave * 48, kG = kWave * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kTar + kG];
+    const float scale = scale_p[0], div = div_p[0];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    if (base >= B) return;
+    const int64_t p = base + lane;
+    char* lds = smem[wave];
+    if (base + kWave <= B) {
+        const float mx = NT ? __builtin_nontemporal_load(src + p * 12 + 0) : src[p * 12 + 0];
+        const float my = NT ? __builtin_nontemporal_load(src + p * 12 + 4) : src[p * 12 + 4];
+        dma_slab_issue<kTar, NT>(reinterpret_cast<const char*>(tar + base * 12), lds, lane);
+        dma_slab_issue<kG, NT>(reinterpret_cast<const char*>(gH + base * 9), lds + kTar, lane);
+        dma_wait_sync();
+        float tr[12], g[9], gt[12];
+        __builtin_memcpy(tr, lds + lane * 48, 48);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
+        float gmx, gmy, gscale, gdiv;
+        tensor_aca_rect_grad(tr, mx, my, scale, div, g, gt, gmx, gmy, gscale, gdiv);
+        wave_lds_sync();  // the staging below reuses the input bytes
+        store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
+        if constexpr (WANT_SRC) {
+            float gs[12];
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gs[k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
+            store_rows_staged<12, NT>(reinterpret_cast<char*>(gsrc + base * 12), gs, lds, lane);
+        }
+        if constexpr (WANT_SD) {
+            gsd[p] = gscale;
+            gsd[B + p] = gdiv;
+        }
+        return;
+    }
+    if (p < B) {
+        float tr[12], g[9], gt[12];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        float gmx, gmy, gscale, gdiv;
+        tensor_aca_rect_grad(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx, gmy,
+                             gscale, gdiv);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
+        if constexpr (WANT_SRC) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
+        }
+        if constexpr (WANT_SD) {
+            gsd[p] = gscale;
+            gsd[B + p] = gdiv;
+        }
+    }
+}
+
+template <bool WANT_CORNER, bool NT>
+__global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_staged(
+    const float* __restrict__ corner, const float* __restrict__ offsets,
+    const float* __restrict__ gH, int64_t B, float w, float h, float* __restrict__ g_off,
+    float* __restrict__ g_corner) {
+    constexpr int kC = kWave * 8, kO = kWave * 32, kG = kWave * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kC + kO + kG];
+    const float div = w / h;
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    if (base >= B) return;
+    const int64_t p = base + lane;
+    char* lds = smem[wave];
+    float off[8], tr[12], g[9], gt[12], mx, my;
+    const bool full = base + kWave <= B;
+    if (full) {
+        dma_slab_issue<kC, NT>(reinterpret_cast<const char*>(corner + base * 2), lds, lane);
+        dma_slab_issue<kO, NT>(reinterpret_cast<const char*>(offsets + base * 8), lds + kC, lane);
+        dma_slab_issue<kG, NT>(reinterpret_cast<const char*>(gH + base * 9), lds + kC + kO, lane);
+        dma_wait_sync();
+        float c[2];
+        __builtin_memcpy(c, lds + lane * 8, 8);
+        __builtin_memcpy(off, lds + kC + lane * 32, 32);
+#pragma unroll
+        for (int k = 0; k < 9; ++k)
+            g[k] = reinterpret_cast<const float*>(lds + kC + kO)[lane * 9 + k];
+        mx = c[0];
+        my = c[1];
+        wave_lds_sync();
+    } else {
+        if (p >= B) return;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) off[k] = offsets[p * 8 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        mx = corner[p * 2];
+        my = corner[p * 2 + 1];
+    }
+    rect_target_from_offsets(mx, my, w, h, off, tr);
+    float gmx, gmy, gsc, gdv;
+    tensor_aca_rect_grad(tr, mx, my, w, div, g, gt, gmx, gmy, gsc, gdv);
+    // tar[0][j] = x_j + off[j].x, tar[1][j] = y_j + off[j].y
+    float go[8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        go[2 * j] = gt[j];
+        go[2 * j + 1] = gt[4 + j];
+    }
+    float gc[2] = {gmx + (((gt[0] + gt[1]) + gt[2]) + gt[3]),
+                   gmy + (((gt[4] + gt[5]) + gt[6]) + gt[7])};
+    if (full) {
+        store_rows_staged<8, NT>(reinterpret_cast<char*>(g_off + base * 8), go, lds, lane);
+        if constexpr (WANT_CORNER) {
+            // 8-B rows: 512 B slab, written straight (lane-consecutive 8-B stores)
+            __builtin_memcpy(g_corner + p * 2, gc, 8);
+        }
+        return;
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) g_off[p * 8 + k] = go[k];
+    if constexpr (WANT_CORNER) {
+        g_corner[p * 2] = gc[0];
+        g_corner[p * 2 + 1] = gc[1];
     }
 }
 

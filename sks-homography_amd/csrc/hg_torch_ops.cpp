@@ -120,7 +120,7 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
     const at::Tensor scale = scale_.contiguous(), div = div_.contiguous();
     at::Tensor g_tar = at::empty({B, 3, 4}, tar.options());
     at::Tensor g_src = need_src ? at::empty({B, 3, 4}, tar.options()) : at::empty({0}, tar.options());
-    at::Tensor part = need_scale_div ? at::empty({B, 2}, tar.options()) : at::empty({0}, tar.options());
+    at::Tensor part = need_scale_div ? at::empty({2, B}, tar.options()) : at::empty({0}, tar.options());
     const c10::DeviceGuard guard(dev);
     hip_ok(hg_tensor_aca_rect_backward_f32(
                src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
@@ -128,8 +128,14 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
                need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
                need_scale_div && B ? part.data_ptr<float>() : nullptr, stream_of(tar)),
            "hg_tensor_aca_rect_backward_f32");
-    // per-problem partials summed on the device, deterministically
-    at::Tensor g_sd = need_scale_div ? part.sum(0) : part;
+    // per-problem partials summed on the device in a fixed order (hg_sum_rows_f32)
+    at::Tensor g_sd = part;
+    if (need_scale_div) {
+        g_sd = at::empty({2}, tar.options());
+        hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), 2, B, g_sd.data_ptr<float>(),
+                               stream_of(tar)),
+               "hg_sum_rows_f32");
+    }
     return {g_src, g_tar, g_sd};
 }
 

@@ -342,12 +342,12 @@ def test_rect_backward_kernel_vs_oracle(orc, oracle, pkg, dev):
             _bits(orc, g_tar, wt, f"grad_tar B={B}")
             _bits(orc, g_src, ws, f"grad_src B={B}")
             # per-problem partials, via the raw C ABI
-            part = torch.empty(B, 2, device=dev)
+            part = torch.empty(2, B, device=dev)
             gt2 = torch.empty(B, 3, 4, device=dev)
             pkg._lib.call("hg_tensor_aca_rect_backward_f32", sh.data_ptr(), th.data_ptr(),
                           gH.data_ptr(), B, s_t.data_ptr(), d_t.data_ptr(), None, gt2.data_ptr(),
                           part.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-            _bits(orc, part, wsd, f"scale/div partials B={B}")
+            _bits(orc, part.T, wsd, f"scale/div partials B={B}")
             _bits(orc, gt2, wt, f"grad_tar (no src) B={B}")
 
 
@@ -487,3 +487,57 @@ def test_config2_full_batch_equals_compiled_reference(orc, ref, pkg, dev):
     for algo in ("aca", "sks"):
         ref.time_batch(algo, s, t, H, 16, 1)  # threaded pass of the reference solver
         _bits(orc, pkg.solve(algo, src, tar), H, f"{algo} 10M vs reference")
+
+
+def _sum_rows_restated(x):
+    """numpy restatement of hg_sum_rows_f32's fixed order (hg_kernels.hip): chunks of
+    4096 summed per thread (t + 256 i, in order, from +0) then folded by halving strides;
+    the chunk sums the same way."""
+    def fold(v):
+        v = v.copy()
+        s = 128
+        while s:
+            v[:s] = v[:s] + v[s:2 * s]
+            s //= 2
+        return v[0]
+
+    out = []
+    for row in x.astype(np.float32):
+        cols = row.shape[0]
+        chunks = -(-cols // 4096)
+        parts = []
+        for c in range(chunks):
+            seg = np.zeros(4096, np.float32)
+            piece = row[c * 4096:(c + 1) * 4096]
+            seg[:piece.shape[0]] = piece
+            v = np.zeros(256, np.float32)
+            for i in range(16):
+                v = v + seg[i * 256:(i + 1) * 256]
+            parts.append(fold(v))
+        v = np.zeros(256, np.float32)
+        for c in range(0, chunks, 256):
+            blk = np.zeros(256, np.float32)
+            p = np.asarray(parts[c:c + 256], np.float32)
+            blk[:p.shape[0]] = p
+            v = v + blk  # +0 padding is exact: v starts at +0 and never becomes -0
+        out.append(fold(v))
+    return np.asarray(out, np.float32)
+
+
+@pytest.mark.parametrize("rows,cols", [(1, 0), (2, 1), (2, 4095), (2, 4096), (2, 4097),
+                                       (3, (1 << 20) + 3), (2, 2_000_000)])
+def test_sum_rows_fixed_order(orc, pkg, dev, rows, cols):
+    """hg_sum_rows_f32 (the reduction of the TensorACA scale/div gradient partials) is
+    bit-identical to its numpy restatement and to itself across runs."""
+    g = torch.Generator(device=dev).manual_seed(cols)
+    x = torch.randn(rows, cols, device=dev, generator=g) * 100
+    want = _sum_rows_restated(x.cpu().numpy())
+    outs = []
+    for _ in range(2):
+        out = torch.empty(rows, device=dev)
+        xx = x.clone()
+        pkg._lib.call("hg_sum_rows_f32", xx.data_ptr(), rows, cols, out.data_ptr(),
+                      torch.cuda.current_stream(dev).cuda_stream)
+        outs.append(out.cpu().numpy())
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    _bits(orc, outs[0], want, f"sum_rows {rows}x{cols}")

@@ -51,6 +51,7 @@ for step in $STEPS; do
         kbench_sample) run kbench_sample 300 python tools/kbench_sample.py ;;
         kbench_soa_small) run kbench_soa_small 300 python tools/kbench_soa_small.py ;;
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
+        kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;
         dist2)
             # rehearse the N>1 control path (barriers, max-over-ranks, one JSON line) with
             # 2 ranks sharing the one GPU over gloo; the real N>1 run uses RCCL
