@@ -369,6 +369,53 @@ int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_
     return (int)hipGetLastError();
 }
 
+// Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice
+// the arithmetic, half the waves.
+template <int UNROLL>
+__global__ __launch_bounds__(kBlock) void ransac_score_sgpr4_kernel(
+    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
+    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
+    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
+    f32x2 h[2][9];
+#pragma unroll
+    for (int q = 0; q < 2; ++q)
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            const int64_t a = p0 + 2 * q, b = a + 1;
+            h[q][k].x = a < n ? H[a * 9 + k] : 0.f;
+            h[q][k].y = b < n ? H[b * 9 + k] : 0.f;
+        }
+    const f32x2 t2v = {t2, t2};
+    i32x2 cnt[2] = {{0, 0}, {0, 0}};
+    auto pair = [&](float2 a, float2 b) {
+        const f32x2 x = {a.x, a.x}, y = {a.y, a.y}, nu = {-b.x, -b.x}, nv = {-b.y, -b.y};
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const f32x2 xs = __builtin_elementwise_fma(h[q][0], x, __builtin_elementwise_fma(h[q][1], y, h[q][2]));
+            const f32x2 ys = __builtin_elementwise_fma(h[q][3], x, __builtin_elementwise_fma(h[q][4], y, h[q][5]));
+            const f32x2 ws = __builtin_elementwise_fma(h[q][6], x, __builtin_elementwise_fma(h[q][7], y, h[q][8]));
+            const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
+            const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
+            const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
+            const f32x2 lim = t2v * (ws * ws);
+            const f32x2 zero = {0.f, 0.f};
+            cnt[q] -= (e2 <= lim) & (ws != zero);
+        }
+    };
+    uint32_t i = 0;
+    for (; i + UNROLL <= npool; i += UNROLL) {
+#pragma unroll
+        for (int u = 0; u < UNROLL; ++u) pair(pool_src[i + u], pool_tar[i + u]);
+    }
+    for (; i < npool; ++i) pair(pool_src[i], pool_tar[i]);
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+        const int64_t a = p0 + 2 * q;
+        if (a < n) counts[a] = (uint32_t)cnt[q].x;
+        if (a + 1 < n) counts[a + 1] = (uint32_t)cnt[q].y;
+    }
+}
+
 }  // namespace hg
 
 extern "C" {
@@ -409,6 +456,8 @@ int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
         case 2: hg::ransac_score2_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         case 3: hg::ransac_score_sgpr_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         case 4: hg::ransac_score_sgpr_kernel<8><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 5: hg::ransac_score_sgpr4_kernel<4><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 6: hg::ransac_score_sgpr4_kernel<8><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();

@@ -43,6 +43,10 @@ for step in $STEPS; do
                 -d "$OUT/pmc_fetch_$TAG" -o run -- python3 tools/pmc_run.py
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
                 -d "$OUT/pmc_write_$TAG" -o run -- python3 tools/pmc_run.py ;;
+        pmc_score)
+            run pmc_score 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES \
+                SQ_WAVE_CYCLES SQ_INSTS_VALU_FLOPS_FP32 GRBM_GUI_ACTIVE --kernel-trace \
+                --output-format csv -d "$OUT/pmc_score_$TAG" -o run -- python3 tools/pmc_score.py ;;
         kbench) run kbench 600 python tools/kbench.py ;;
         kbench_soa) run kbench_soa 600 python tools/kbench_soa.py ;;
         kbench_score) run kbench_score 600 python tools/kbench_score.py ;;

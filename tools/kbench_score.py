@@ -14,7 +14,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 
-NV = 5  # hg_tune_score variants (csrc/hg_ransac.hip)
+NV = 7  # hg_tune_score variants (csrc/hg_ransac.hip)
 
 
 def main():

@@ -1,0 +1,24 @@
+"""Workload for a VALU-counter pass over the RANSAC scorer (tools/gpu_round.sh pmc_score):
+1 M hypotheses x the 2540-pair wall pool, 3 launches."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+pkg = ge.load_package()
+dev = torch.device("cuda:0")
+g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+ps = torch.from_numpy(g["pool_src"]).to(dev)
+pt = torch.from_numpy(g["pool_tar"]).to(dev)
+n = 1 << 20
+idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
+H = pkg.sample_solve(ps, pt, idx)
+for _ in range(3):
+    pkg.ransac_score(H, ps, pt, 3.0)
+torch.cuda.synchronize()
+print("pmc_score done")
