@@ -95,6 +95,17 @@ def test_other_entry_validation(pkg):
                                                   None) == 1
     assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
                                                None) == 1
+    assert lib.hg_solve_one_f32(0, None, None, None, 1, None) == 1               # NULL points
+    assert lib.hg_solve_one_f64(2, None, None, None, 1, None) == 1               # algo 2
+    assert lib.hg_sum_rows_f32(None, -1, 5, None, None) == 1                      # rows < 0
+    assert lib.hg_sum_rows_f32(None, 0, 5, None, None) == 0                       # nothing to do
+    assert lib.hg_sum_rows_f32(None, 2, 5, None, None) == 1                       # NULL x / out
+    assert lib.hg_sum_rows_f32(None, 70000, 5, None, None) == 1                   # rows > 65535
+    assert lib.hg_sample_solve_f32(None, None, 0, None, None, 5, 0, 1, None) == 1  # npool 0
+    assert lib.hg_sample_solve_f32(None, None, 9, None, None, 5, 7, 1, None) == 1  # algo 7
+    assert lib.hg_ransac_score_f32(None, -1, None, None, 9, 1.0, None, None) == 1
+    assert lib.hg_fill_bits_u32(None, 5, 0, 0, None) == 1
+    assert lib.hg_fill_bits_u32(None, 0, 0, 0, None) == 0
     assert lib.hg_stream_copy(None, None, 17, None) == 1                          # not x16
     assert lib.hg_stream_copy(None, None, 0, None) == 0
     assert pkg.version().startswith("sks-homography-amd")
