@@ -312,25 +312,21 @@ def reference_layout(d: Dist, pkg):
         tar = pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(8, n).double()
         H = torch.empty((9, n), dtype=torch.float64, device=d.dev)
         algos = ("aca", "sks", "gpt", "ge") if n == 1_000_000 else ("aca", "sks")
-        for algo in algos:
-            if algo == "ge":  # the reference's GE is binary32 (GE.cpp); Table 8 ran it in f64
-                s32, t32, H32 = src.float(), tar.float(), H.float()
-                f = lambda: pkg.solve("ge", s32, t32, layout="soa", out=H32)  # noqa
-            else:
-                f = lambda: pkg.solve(algo, src, tar, normalize=False, layout="soa", out=H)  # noqa
+        for algo in algos:  # all four in binary64, as Table 8 (cal_Homo_GE is f64 too)
+            f = lambda: pkg.solve(algo, src, tar, normalize=False, layout="soa", out=H)  # noqa
             for _ in range(10):
                 f()
             _, ms1 = timed_region(d, f, 10)
             loops = max(10, min(5000, int(1000.0 / max(ms1, 1e-3))))  # ~1 s, like .cu:1188
             _, ms = timed_region(d, f, loops)
-            bpp = 100 if algo == "ge" else 200
+            bpp = 200
             rec = {"us_per_launch": round(ms * 1e3, 2), "launches": loops,
                    "achieved_gbps": round(n * bpp / (ms * 1e-3) / 1e9, 1),
                    "G_homographies_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
             if n == 1_000_000:
                 rec["table8_us"] = TABLE8_US[algo]
                 rec["speedup_vs_table8"] = round(TABLE8_US[algo] / (ms * 1e3), 2)
-            out[f"{algo}_{'f32' if algo == 'ge' else 'f64'}_soa_n{n}"] = rec
+            out[f"{algo}_f64_soa_n{n}"] = rec
         del src, tar, H
     return out
 

@@ -67,6 +67,12 @@ int hg_sks_f64(const double* src, const double* tar, double* H, int64_t n, int l
 int hg_ge_f32(const float* src, const float* tar, float* H, int64_t n, int layout, int flags,
               void* stream);
 
+/* RHO Gaussian elimination, binary64 -- the reference GPU harness's cal_Homo_GE
+ * (GPU_Runtime Test.cu:359-507: GE.cpp's statements in double), batched; Table 8's GE
+ * row.  H[8] is 1 by construction. */
+int hg_ge_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
+              int flags, void* stream);
+
 /* 8x8 LU with partial pivoting, binary64 -- the reference GPU harness's
  * getPerspectiveTransform baseline cal_Homo_GPT (GPU_Runtime Test.cu:301-357, helpers
  * :242-300), batched.  H[8] is 1 by construction. */

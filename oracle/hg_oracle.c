@@ -394,76 +394,85 @@ int oracle_ransac_score_f32(const float* H, int64_t n, const float* ps, const fl
 /* Restates cv::runKernel_GE ("C++ Codes/modules/GE.cpp:41-188", OpenCV rho.cpp
  * hFuncRefC), the reference's comparison baseline: elimination on
  * the 2 source rows (q) and 3 right-hand rows (m), pivot point P (index 2). */
-static void ge_one_f32(const float* s, const float* t, float* h) {
-    float xX[4], xY[4], yX[4], yY[4], q[2][4], m[3][8], a, b;
-    for (int i = 0; i < 4; ++i) {
-        xX[i] = s[2 * i] * t[2 * i];
-        xY[i] = s[2 * i] * t[2 * i + 1];
-        yX[i] = s[2 * i + 1] * t[2 * i];
-        yY[i] = s[2 * i + 1] * t[2 * i + 1];
-    }
-    for (int i = 0; i < 4; ++i) {
-        if (i == 2) {
-            q[0][2] = s[4]; q[1][2] = s[5];
-            m[0][2] = -xX[2]; m[0][6] = -xY[2];
-            m[1][2] = -yX[2]; m[1][6] = -yY[2];
-            m[2][2] = t[4]; m[2][6] = t[5];
-        } else {
-            q[0][i] = s[2 * i] - s[4];
-            q[1][i] = s[2 * i + 1] - s[5];
-            m[0][i] = xX[2] - xX[i]; m[0][4 + i] = xY[2] - xY[i];
-            m[1][i] = yX[2] - yX[i]; m[1][4 + i] = yY[2] - yY[i];
-            m[2][i] = t[2 * i] - t[4]; m[2][4 + i] = t[2 * i + 1] - t[5];
-        }
-    }
-    a = q[0][0]; b = q[0][1];
-    q[1][1] = q[1][1] * a - q[1][0] * b;
-    for (int r = 0; r < 3; ++r) {
-        m[r][1] = m[r][1] * a - m[r][0] * b;
-        m[r][5] = m[r][5] * a - m[r][4] * b;
-    }
-    b = q[0][3];
-    q[1][3] = q[1][3] * a - q[1][0] * b;
-    for (int r = 0; r < 3; ++r) {
-        m[r][3] = m[r][3] * a - m[r][0] * b;
-        m[r][7] = m[r][7] * a - m[r][4] * b;
-    }
-    a = q[1][1]; b = q[1][3];
-    for (int r = 0; r < 3; ++r) {
-        m[r][3] = m[r][3] * a - m[r][1] * b;
-        m[r][7] = m[r][7] * a - m[r][5] * b;
-    }
-    b = q[1][0];
-    q[0][0] = q[0][0] * a;
-    for (int r = 0; r < 3; ++r) {
-        m[r][0] = m[r][0] * a - m[r][1] * b;
-        m[r][4] = m[r][4] * a - m[r][5] * b;
-    }
-    a = 1.0f / q[0][0];
-    for (int r = 0; r < 3; ++r) { m[r][0] = m[r][0] * a; m[r][4] = m[r][4] * a; }
-    a = 1.0f / q[1][1];
-    for (int r = 0; r < 3; ++r) { m[r][1] = m[r][1] * a; m[r][5] = m[r][5] * a; }
-    a = q[0][2]; b = q[1][2];
-    for (int r = 0; r < 3; ++r) {
-        m[r][2] = m[r][2] - (m[r][0] * a + m[r][1] * b);
-        m[r][6] = m[r][6] - (m[r][4] * a + m[r][5] * b);
-    }
-    a = m[0][7];
-    m[1][7] = m[1][7] / a;
-    m[2][7] = m[2][7] / a;
-    for (int c = 0; c < 7; ++c) {
-        m[1][c] = m[1][c] - m[0][c] * m[1][7];
-        m[2][c] = m[2][c] - m[0][c] * m[2][7];
-    }
-    m[2][3] = m[2][3] / m[1][3];
-    for (int c = 0; c < 8; ++c)
-        if (c != 3) m[2][c] = m[2][c] - m[1][c] * m[2][3];
-    h[0] = m[2][0]; h[1] = m[2][1]; h[2] = m[2][2];
-    h[3] = m[2][4]; h[4] = m[2][5]; h[5] = m[2][6];
-    h[6] = m[2][7]; h[7] = m[2][3]; h[8] = 1.0f;
+/* The same statements in binary64 are the reference GPU harness's cal_Homo_GE
+ * ("GPU_Runtime Test.cu:359-507": identical statement sequence and output mapping,
+ * double literals) -- compared statement by statement with GE.cpp after type
+ * normalisation; nvcc is absent, so that form is pinned by construction, not by a run. */
+#define DEFINE_GE_ONE(NAME, T, ONE) \
+static void NAME(const T* s, const T* t, T* h) { \
+    T xX[4], xY[4], yX[4], yY[4], q[2][4], m[3][8], a, b; \
+    for (int i = 0; i < 4; ++i) { \
+        xX[i] = s[2 * i] * t[2 * i]; \
+        xY[i] = s[2 * i] * t[2 * i + 1]; \
+        yX[i] = s[2 * i + 1] * t[2 * i]; \
+        yY[i] = s[2 * i + 1] * t[2 * i + 1]; \
+    } \
+    for (int i = 0; i < 4; ++i) { \
+        if (i == 2) { \
+            q[0][2] = s[4]; q[1][2] = s[5]; \
+            m[0][2] = -xX[2]; m[0][6] = -xY[2]; \
+            m[1][2] = -yX[2]; m[1][6] = -yY[2]; \
+            m[2][2] = t[4]; m[2][6] = t[5]; \
+        } else { \
+            q[0][i] = s[2 * i] - s[4]; \
+            q[1][i] = s[2 * i + 1] - s[5]; \
+            m[0][i] = xX[2] - xX[i]; m[0][4 + i] = xY[2] - xY[i]; \
+            m[1][i] = yX[2] - yX[i]; m[1][4 + i] = yY[2] - yY[i]; \
+            m[2][i] = t[2 * i] - t[4]; m[2][4 + i] = t[2 * i + 1] - t[5]; \
+        } \
+    } \
+    a = q[0][0]; b = q[0][1]; \
+    q[1][1] = q[1][1] * a - q[1][0] * b; \
+    for (int r = 0; r < 3; ++r) { \
+        m[r][1] = m[r][1] * a - m[r][0] * b; \
+        m[r][5] = m[r][5] * a - m[r][4] * b; \
+    } \
+    b = q[0][3]; \
+    q[1][3] = q[1][3] * a - q[1][0] * b; \
+    for (int r = 0; r < 3; ++r) { \
+        m[r][3] = m[r][3] * a - m[r][0] * b; \
+        m[r][7] = m[r][7] * a - m[r][4] * b; \
+    } \
+    a = q[1][1]; b = q[1][3]; \
+    for (int r = 0; r < 3; ++r) { \
+        m[r][3] = m[r][3] * a - m[r][1] * b; \
+        m[r][7] = m[r][7] * a - m[r][5] * b; \
+    } \
+    b = q[1][0]; \
+    q[0][0] = q[0][0] * a; \
+    for (int r = 0; r < 3; ++r) { \
+        m[r][0] = m[r][0] * a - m[r][1] * b; \
+        m[r][4] = m[r][4] * a - m[r][5] * b; \
+    } \
+    a = ONE / q[0][0]; \
+    for (int r = 0; r < 3; ++r) { m[r][0] = m[r][0] * a; m[r][4] = m[r][4] * a; } \
+    a = ONE / q[1][1]; \
+    for (int r = 0; r < 3; ++r) { m[r][1] = m[r][1] * a; m[r][5] = m[r][5] * a; } \
+    a = q[0][2]; b = q[1][2]; \
+    for (int r = 0; r < 3; ++r) { \
+        m[r][2] = m[r][2] - (m[r][0] * a + m[r][1] * b); \
+        m[r][6] = m[r][6] - (m[r][4] * a + m[r][5] * b); \
+    } \
+    a = m[0][7]; \
+    m[1][7] = m[1][7] / a; \
+    m[2][7] = m[2][7] / a; \
+    for (int c = 0; c < 7; ++c) { \
+        m[1][c] = m[1][c] - m[0][c] * m[1][7]; \
+        m[2][c] = m[2][c] - m[0][c] * m[2][7]; \
+    } \
+    m[2][3] = m[2][3] / m[1][3]; \
+    for (int c = 0; c < 8; ++c) \
+        if (c != 3) m[2][c] = m[2][c] - m[1][c] * m[2][3]; \
+    h[0] = m[2][0]; h[1] = m[2][1]; h[2] = m[2][2]; \
+    h[3] = m[2][4]; h[4] = m[2][5]; h[5] = m[2][6]; \
+    h[6] = m[2][7]; h[7] = m[2][3]; h[8] = ONE; \
 }
 
+DEFINE_GE_ONE(ge_one_f32, float, 1.0f)
+DEFINE_GE_ONE(ge_one_f64, double, 1.0)
+
 DEFINE_BATCH(oracle_ge_f32, float, ge_one_f32, normalize_f32)
+DEFINE_BATCH(oracle_ge_f64, double, ge_one_f64, normalize_f64)
 
 /* ---------------------------------------------------- GPT-LU baseline ------ */
 /* Restates the reference GPU harness's cal_Homo_GPT ("GPU_Runtime Test.cu:301-357")

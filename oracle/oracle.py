@@ -40,7 +40,8 @@ class Oracle:
         lib = ctypes.CDLL(path)
         for name, fp in (("oracle_aca_f32", _f32p), ("oracle_sks_f32", _f32p),
                          ("oracle_aca_f64", _f64p), ("oracle_sks_f64", _f64p),
-                         ("oracle_ge_f32", _f32p), ("oracle_gpt_f64", _f64p)):
+                         ("oracle_ge_f32", _f32p), ("oracle_ge_f64", _f64p),
+                         ("oracle_gpt_f64", _f64p)):
             fn = getattr(lib, name)
             fn.argtypes = [fp, fp, fp, _i64, ctypes.c_int, ctypes.c_int]
             fn.restype = ctypes.c_int

@@ -28,6 +28,7 @@ SIGNATURES = {
     "hg_sks_f32": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
     "hg_sks_f64": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
     "hg_ge_f32": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_ge_f64": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
     "hg_gpt_f64": ([_vp, _vp, _vp, _i64, _int, _int, _vp], _int),
     "hg_tensor_aca_rect_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     "hg_tensor_aca_rect_f32_hostscalar": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,

@@ -300,6 +300,11 @@ int hg_ge_f32(const float* src, const float* tar, float* H, int64_t n, int layou
     return hg::dispatch<hg::kGE>(src, tar, H, n, layout, flags, stream);
 }
 
+int hg_ge_f64(const double* src, const double* tar, double* H, int64_t n, int layout, int flags,
+              void* stream) {
+    return hg::dispatch<hg::kGE>(src, tar, H, n, layout, flags, stream);
+}
+
 int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
                int flags, void* stream) {
     return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream);

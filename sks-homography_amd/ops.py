@@ -75,8 +75,8 @@ def _as_problems(x: torch.Tensor, layout: str) -> torch.Tensor:
 def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = True,
           layout: str = "aos", out: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Batched 4-point homography, ``algo`` in {"aca", "sks", "ge", "gpt"}.  "ge" and
-    "gpt" are the reference's comparison baselines: RHO Gaussian elimination (f32,
-    cv::runKernel_GE) and 8x8 pivoted LU (f64, cal_Homo_GPT).
+    "gpt" are the reference's comparison baselines: RHO Gaussian elimination (f32 as
+    cv::runKernel_GE, f64 as cal_Homo_GE) and 8x8 pivoted LU (f64, cal_Homo_GPT).
 
     AoS: src/tar (n,8) or (n,4,2) -> H (n,9); SoA: (8,n) -> (9,n).
     ``normalize=True`` returns H/H[8] exactly as sks::runKernel_* (ACA_SKS.cpp:94-98);
@@ -85,8 +85,6 @@ def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = Tru
     if algo not in ("aca", "sks", "ge", "gpt"):
         raise ValueError(f"algo must be 'aca', 'sks', 'ge' or 'gpt', got {algo!r}")
     dev = _require_device(src, tar)
-    if algo == "ge" and src.dtype != torch.float32:
-        raise TypeError("the GE baseline (cv::runKernel_GE) is float32 only")
     if algo == "gpt" and src.dtype != torch.float64:
         raise TypeError("the GPT-LU baseline (cal_Homo_GPT) is float64 only")
     if src.dtype not in _DTYPES or tar.dtype != src.dtype:

@@ -433,6 +433,26 @@ def test_ge_random_1m_vs_oracle(orc, oracle, pkg, dev):
 
 
 @pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_ge_f64_baseline_vs_oracle(orc, oracle, pkg, dev, layout):
+    """cal_Homo_GE's binary64 GE (GPU_Runtime Test.cu:359-507), bit-exact against the
+    restatement, incl. the edge-case fixture; parity vs the .cu itself is by statement
+    comparison with GE.cpp (nvcc absent)."""
+    rng = np.random.default_rng(21)
+    n = 300_001
+    g = load_golden("cpp_edge.npz")
+    s = np.concatenate([rng.uniform(0, 1024, (n, 8)), g["src_f64"]])
+    t = np.concatenate([rng.uniform(0, 1024, (n, 8)), g["tar_f64"]])
+    src, tar = _t(s, dev), _t(t, dev)
+    want = oracle.solve("ge", s, t, normalize=False)
+    if layout == "soa":
+        H = pkg.solve("ge", src.T.contiguous(), tar.T.contiguous(), normalize=False,
+                      layout="soa").T
+    else:
+        H = pkg.solve("ge", src, tar, normalize=False)
+    _bits(orc, H, want, f"ge f64 {layout}")
+
+
+@pytest.mark.parametrize("layout", ["aos", "soa"])
 def test_gpt_lu_baseline_vs_oracle(orc, oracle, pkg, dev, layout):
     """The reference GPU harness's pivoted-LU baseline (cal_Homo_GPT), f64, bit-exact
     against the restatement; includes the golden edge cases (pivoting on zeros/NaN)."""

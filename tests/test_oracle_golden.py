@@ -194,3 +194,13 @@ def test_oracle_gpt_lu_vs_lapack(oracle):
         want = np.linalg.solve(A, b)
         np.testing.assert_allclose(H[i, :8], want, rtol=1e-7, atol=1e-9 * np.abs(want).max())
         assert H[i, 8] == 1.0
+
+
+def test_oracle_ge_f64_tracks_reference_f32(orc, oracle):
+    """The binary64 GE restatement (cal_Homo_GE) agrees with the reference's binary32
+    GE.cpp to f32 accuracy on the uniform fixture (same statements, wider type)."""
+    g = load_golden("cpp_uniform.npz")
+    h64 = oracle.solve("ge", g["src_f32"].astype(np.float64), g["tar_f32"].astype(np.float64))
+    h32 = g["ge_f32"].astype(np.float64)
+    rel = np.abs(h64 - h32) / np.maximum(np.abs(h64), 1e-12)
+    assert np.median(rel) < 1e-5
