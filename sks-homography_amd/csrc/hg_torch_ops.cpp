@@ -243,6 +243,31 @@ at::Tensor call_rect(const at::Tensor& src, const at::Tensor& tar, const at::Ten
     return op.call(src, tar, scale, div);
 }
 
+// The backward ops are reached through the dispatcher too, so tracing (fake tensors,
+// AOT autograd) sees their Meta kernels instead of a raw launch.
+std::tuple<at::Tensor, at::Tensor, at::Tensor> call_rect_backward(
+    const at::Tensor& src, const at::Tensor& tar, const at::Tensor& grad, const at::Tensor& scale,
+    const at::Tensor& div, bool need_src, bool need_sd) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::tensor_aca_rect_backward", "")
+                         .typed<std::tuple<at::Tensor, at::Tensor, at::Tensor>(
+                             const at::Tensor&, const at::Tensor&, const at::Tensor&,
+                             const at::Tensor&, const at::Tensor&, bool, bool)>();
+    return op.call(src, tar, grad, scale, div, need_src, need_sd);
+}
+
+std::tuple<at::Tensor, at::Tensor> call_offsets_backward(const at::Tensor& corner,
+                                                         const at::Tensor& offsets,
+                                                         const at::Tensor& grad, double w,
+                                                         double h, bool need_corner) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::tensor_aca_offsets_backward", "")
+                         .typed<std::tuple<at::Tensor, at::Tensor>(
+                             const at::Tensor&, const at::Tensor&, const at::Tensor&, double,
+                             double, bool)>();
+    return op.call(corner, offsets, grad, w, h, need_corner);
+}
+
 class RectFunction : public torch::autograd::Function<RectFunction> {
    public:
     static at::Tensor forward(AutogradContext* ctx, const at::Tensor& src, const at::Tensor& tar,
@@ -258,7 +283,7 @@ class RectFunction : public torch::autograd::Function<RectFunction> {
         const bool need_src = ctx->needs_input_grad(0);
         const bool need_sd = ctx->needs_input_grad(2) || ctx->needs_input_grad(3);
         auto [g_src, g_tar, g_sd] =
-            rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd);
+            call_rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd);
         at::Tensor none;
         return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none,
                 ctx->needs_input_grad(2) ? g_sd.slice(0, 0, 1).reshape(scale.sizes()) : none,
@@ -304,7 +329,7 @@ class OffsetsFunction : public torch::autograd::Function<OffsetsFunction> {
         const auto saved = ctx->get_saved_variables();
         const bool need_c = ctx->needs_input_grad(0);
         auto [g_off, g_cor] =
-            offsets_backward(saved[0], saved[1], grads[0].contiguous(),
+            call_offsets_backward(saved[0], saved[1], grads[0].contiguous(),
                              ctx->saved_data["w"].toDouble(), ctx->saved_data["h"].toDouble(),
                              need_c);
         at::Tensor none;

@@ -105,3 +105,27 @@ def test_square_specialisation_same_bits(orc, oracle, pkg, dev, wh):
                              torch.tensor([div], device=dev))
     assert orc.same_bits(Hh.cpu().numpy(), Hd.cpu().numpy()).all()
     assert orc.same_bits(Hh.cpu().numpy(), want).all()
+
+
+def test_native_ops_pass_torch_opcheck(pkg, dev):
+    """torch.library.opcheck over the native operators (csrc/hg_torch_ops.cpp): schema,
+    Meta/fake-tensor kernels, autograd registration and AOT dispatch agree with the real
+    GPU kernels."""
+    B = 1000
+    torch.manual_seed(0)
+    _, _, src, tar, scale, div = pkg.adjust(dev, B)
+    corner = src[:, 0:2, 0].contiguous()
+    offs = (tar[:, 0:2, :] - src[:, 0:2, :]).transpose(1, 2).contiguous()
+    ops = torch.ops.sks_amd
+    tests = ("test_schema", "test_autograd_registration", "test_faketensor",
+             "test_aot_dispatch_dynamic")
+    offs_g = offs.clone().requires_grad_(True)
+    tar_g = tar.clone().requires_grad_(True)
+    torch.library.opcheck(ops.tensor_aca_offsets.default, (corner, offs_g, 128.0, 128.0),
+                          test_utils=tests)
+    torch.library.opcheck(ops.tensor_aca_rect.default, (src, tar_g, scale, div), test_utils=tests)
+    q = torch.rand(B, 4, 2, device=dev) * 100
+    torch.library.opcheck(ops.aca.default, (q, q + 1.5, True),
+                          test_utils=("test_schema", "test_faketensor"))
+    torch.library.opcheck(ops.sks.default, (q, q + 1.5, False),
+                          test_utils=("test_schema", "test_faketensor"))
