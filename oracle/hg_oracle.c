@@ -15,11 +15,17 @@
  *   rect_one   <- TensorACA_rect "PyTorch Codes/Modules_Runtime_Test.py:286-309"
  *                 (spec "Matlab Codes/ACA_rect.m:22-38"), evaluated the way ATen's
  *                 CPU kernels evaluate it (cross product with one fused multiply-add
- *                 per component, left-to-right 3-term sum, every other op rounded).
+ *                 per component, left-to-right 3-term sum, every other op rounded),
+ *                 and its reverse-mode gradient (rect_grad)
+ *   ge_one     <- cv::runKernel_GE "C++ Codes/modules/GE.cpp:41-188" (binary32) and
+ *                 the harness's cal_Homo_GE "GPU_Runtime Test.cu:359-507" (binary64)
+ *   gpt_one    <- cal_Homo_GPT "GPU_Runtime Test.cu:242-357" (binary64)
+ *   fill_*, ransac_score <- the counter generators and the inlier test of the
+ *                 RANSAC extension (no reference code to pin)
  *
- * Parity is PINNED: tests/test_oracle_golden.py checks every function here
+ * Parity is PINNED (where noted otherwise in DESIGN.md section 3, by restatement): tests/test_oracle_golden.py checks every function here
  * against tests/golden/*.npz, which tools/make_golden.py produced by running the
- * reference's own C++ (compiled from /root/reference, oracle/Makefile) and the
+ * reference's own C++ (compiled from /root/reference by oracle/build.sh) and the
  * reference's own PyTorch statements (executed from /root/reference).
  *
  * Numerics contract (why this file must be compiled with -ffp-contract=off and
