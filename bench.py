@@ -598,10 +598,32 @@ def main():
         for _ in range(100):
             f_os()
         _, ms_os = timed_region(d, f_os, 1000)
+        # the torch-composed deep-homography path from the same corner + offsets: build
+        # the (B,3,4) target as getTar/adjust do (.py:19-37), then TensorACA_rect's ATen ops
+        s64 = src_h  # the batch's static (B,3,4) rectangle, as above
+
+        def f_ot():
+            t = s64.clone()
+            t[:, 0:2, :] += o64.transpose(1, 2)
+            return torch_tensor_aca_rect(s64, t, scale, div)
+
+        for _ in range(100):
+            f_ot()
+        _, ms_ot = timed_region(d, f_ot, 1000)
+        g_os = graph_of(d, f_os, 100)
+        g_ot = graph_of(d, f_ot, 100)
+        _, ms_gos = timed_region(d, g_os.replay, 20)
+        _, ms_got = timed_region(d, g_ot.replay, 20)
+        del g_os, g_ot
         del corner, offs, Ho
         rb = pkg.RECT_BYTES_PER_PROBLEM
         line["tensor_aca_offsets"] = {
             "batch": args.rect_batch, "us_per_call": round(ms_os * 1e3, 3),
+            "torch_composed_us_per_call": round(ms_ot * 1e3, 3),
+            "speedup_vs_torch": round(ms_ot / ms_os, 2),
+            "graph_us_per_call": round(ms_gos * 1e3 / 100, 3),
+            "torch_composed_graph_us_per_call": round(ms_got * 1e3 / 100, 3),
+            "graph_speedup_vs_torch": round(ms_got / ms_gos, 2),
             "large_batch": big, "large_us_per_call": round(ms_ob * 1e3, 2),
             "large_achieved_gbps": round(big * 76 / (ms_ob * 1e-3) / 1e9, 1),
             "large_frac": round(big * 76 / (ms_ob * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
