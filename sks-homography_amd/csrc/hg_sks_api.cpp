@@ -62,6 +62,8 @@ int solve_one(T* src, T* tar, T* result) {
     const bool ds = is_device_pointer(src), dt = is_device_pointer(tar);
     const bool dr = is_device_pointer(result);
     if (ds && dt && dr) {
+        // device data may come from work the caller queued on the legacy default stream:
+        // launching there keeps that order (a private stream would race it)
         int rc = F(src, tar, result, 1, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, nullptr);
         if (rc) return rc;
         return (int)hipStreamSynchronize(nullptr);
