@@ -139,6 +139,35 @@ const SoaVariant kSoaVariants[] = {
     {"f32 G1 one-shot plain (cached) ld/st", launch_soa<float, 1, false, false>},
 };
 
+// The HBM ceilings either side of a copy: read-only (every 16-B load folded into a
+// per-lane XOR, one dword out per lane) and write-only (a constant).
+template <int U>
+__global__ __launch_bounds__(kBlock) void read_only(const u32x4* __restrict__ src,
+                                                    uint32_t* __restrict__ sink, int64_t n16) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) {
+            const u32x4 v = ld16<true>(src + i);
+            acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+        }
+    }
+    sink[(int64_t)blockIdx.x * kBlock + threadIdx.x] = acc;
+}
+
+template <int U>
+__global__ __launch_bounds__(kBlock) void write_only(u32x4* __restrict__ dst, int64_t n16) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    const u32x4 v = {1u, 2u, 3u, 4u};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) st16<true>(dst + i, v);
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -157,7 +186,8 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
                                         reinterpret_cast<hipStream_t>(stream));
 }
 
-// variant 0: U=4 nt, 1: U=8 nt, 2: U=4 plain, 3: LDS-DMA (bytes % 32 KiB == 0)
+// variant 0: U=4 nt, 1: U=8 nt, 2: U=4 plain, 3: LDS-DMA (bytes % 32 KiB == 0),
+// 4: read-only U=4 (dst receives bytes/64 B of XOR sinks), 5: write-only U=4 (src unused)
 int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* stream) {
     if (bytes <= 0 || (bytes & 15)) return (int)hipErrorInvalidValue;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -172,6 +202,8 @@ int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* s
             if (bytes % 32768) return (int)hipErrorInvalidValue;
             copy_dma<<<(unsigned)(bytes / 32768), kBlock, 0, st>>>((const char*)src, (char*)dst, bytes);
             break;
+        case 4: read_only<4><<<(unsigned)((n16 + 1023) / 1024), kBlock, 0, st>>>(s, reinterpret_cast<uint32_t*>(dst), n16); break;
+        case 5: write_only<4><<<(unsigned)((n16 + 1023) / 1024), kBlock, 0, st>>>(d, n16); break;
         default: return (int)hipErrorInvalidValue;
     }
     return (int)hipGetLastError();
