@@ -13,6 +13,8 @@
 #include <torch/autograd.h>
 #include <torch/library.h>
 
+#include <vector>
+
 #include "sks_homography.h"
 
 namespace {
@@ -230,6 +232,67 @@ at::Tensor quad(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
     return out;
 }
 
+// ------------------------------------------------------------------ the general batch solve
+// algo 0 ACA, 1 SKS, 2 RHO-GE, 3 GPT-LU (f64 only); layout 0 AoS (n,8)|(n,4,2) -> (n,9),
+// 1 SoA (8,n) -> (9,n).  What ops.solve() calls.
+using SolveF32 = int (*)(const float*, const float*, float*, int64_t, int, int, void*);
+using SolveF64 = int (*)(const double*, const double*, double*, int64_t, int, int, void*);
+constexpr SolveF32 kSolveF32[4] = {hg_aca_f32, hg_sks_f32, hg_ge_f32, nullptr};
+constexpr SolveF64 kSolveF64[4] = {hg_aca_f64, hg_sks_f64, hg_ge_f64, hg_gpt_f64};
+
+std::vector<int64_t> solve_shape(const at::Tensor& src, const at::Tensor& tar, int64_t layout) {
+    TORCH_CHECK(layout == 0 || layout == 1, "sks_amd::solve: layout must be 0 (AoS) or 1 (SoA)");
+    if (layout == 0) {
+        for (const auto* p : {&src, &tar})
+            TORCH_CHECK((p->dim() == 2 && p->size(1) == 8) ||
+                            (p->dim() == 3 && p->size(1) == 4 && p->size(2) == 2),
+                        "sks_amd::solve: AoS problems must be (n,8) or (n,4,2), got ", p->sizes());
+        TORCH_CHECK(src.size(0) == tar.size(0), "sks_amd::solve: src/tar batch sizes differ");
+        return {src.size(0), 9};
+    }
+    for (const auto* p : {&src, &tar})
+        TORCH_CHECK(p->dim() == 2 && p->size(0) == 8, "sks_amd::solve: SoA problems must be (8,n), got ",
+                    p->sizes());
+    TORCH_CHECK(src.size(1) == tar.size(1), "sks_amd::solve: src/tar batch sizes differ");
+    return {9, src.size(1)};
+}
+
+at::Tensor& solve_out(const at::Tensor& src_, const at::Tensor& tar_, int64_t algo,
+                      bool normalize, int64_t layout, at::Tensor& out) {
+    const at::Device dev = tar_.device();
+    TORCH_CHECK(src_.is_cuda() && tar_.is_cuda() && out.is_cuda(),
+                "sks_amd::solve: GPU tensors only (no CPU path)");
+    TORCH_CHECK(src_.device() == dev && out.device() == dev, "sks_amd::solve: devices differ");
+    const auto dt = tar_.scalar_type();
+    TORCH_CHECK((dt == at::kFloat || dt == at::kDouble) && src_.scalar_type() == dt &&
+                    out.scalar_type() == dt,
+                "sks_amd::solve: src/tar/out must all be float32 or all float64");
+    TORCH_CHECK(algo >= 0 && algo <= 3, "sks_amd::solve: algo must be 0..3");
+    TORCH_CHECK(!(algo == 3 && dt == at::kFloat), "sks_amd::solve: GPT-LU is float64 only");
+    const auto shape = solve_shape(src_, tar_, layout);
+    TORCH_CHECK(out.sizes() == at::IntArrayRef(shape) && out.is_contiguous(),
+                "sks_amd::solve: out must be a contiguous ", at::IntArrayRef(shape), " tensor");
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
+    const int64_t n = layout == 0 ? shape[0] : shape[1];
+    const int flags = normalize ? HG_FLAG_NORMALIZE : 0;
+    const int lay = layout == 0 ? HG_LAYOUT_AOS : HG_LAYOUT_SOA;
+    const c10::DeviceGuard guard(dev);
+    const int rc = dt == at::kFloat
+                       ? kSolveF32[algo](src.data_ptr<float>(), tar.data_ptr<float>(),
+                                         out.data_ptr<float>(), n, lay, flags, stream_of(tar))
+                       : kSolveF64[algo](src.data_ptr<double>(), tar.data_ptr<double>(),
+                                         out.data_ptr<double>(), n, lay, flags, stream_of(tar));
+    hip_ok(rc, "sks_amd::solve");
+    return out;
+}
+
+at::Tensor solve(const at::Tensor& src, const at::Tensor& tar, int64_t algo, bool normalize,
+                 int64_t layout) {
+    at::Tensor out = at::empty(solve_shape(src, tar, layout), tar.options());
+    solve_out(src, tar, algo, normalize, layout, out);
+    return out;
+}
+
 // ------------------------------------------------------------------ Meta (shapes only)
 at::Tensor meta_b33(const at::Tensor& t) { return at::empty({t.size(0), 3, 3}, t.options()); }
 
@@ -353,6 +416,9 @@ TORCH_LIBRARY(sks_amd, m) {
     m.def("aca.out(Tensor src, Tensor tar, bool normalize=False, *, Tensor(a!) out) -> Tensor(a!)");
     m.def("sks(Tensor src, Tensor tar, bool normalize=False) -> Tensor");
     m.def("sks.out(Tensor src, Tensor tar, bool normalize=False, *, Tensor(a!) out) -> Tensor(a!)");
+    m.def("solve(Tensor src, Tensor tar, int algo, bool normalize, int layout) -> Tensor");
+    m.def("solve.out(Tensor src, Tensor tar, int algo, bool normalize, int layout, *, "
+          "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect(Tensor src, Tensor tar, Tensor scale, Tensor div) -> Tensor");
     m.def("tensor_aca_rect.out(Tensor src, Tensor tar, Tensor scale, Tensor div, *, "
           "Tensor(a!) out) -> Tensor(a!)");
@@ -369,6 +435,8 @@ TORCH_LIBRARY(sks_amd, m) {
 }
 
 TORCH_LIBRARY_IMPL(sks_amd, CUDA, m) {
+    m.impl("solve", solve);
+    m.impl("solve.out", solve_out);
     m.impl("aca", quad<0>);
     m.impl("aca.out", quad_out<0>);
     m.impl("sks", quad<1>);
@@ -384,6 +452,9 @@ TORCH_LIBRARY_IMPL(sks_amd, CUDA, m) {
 }
 
 TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
+    m.impl("solve", [](const at::Tensor& s, const at::Tensor& t, int64_t, bool, int64_t layout) {
+        return at::empty(solve_shape(s, t, layout), t.options());
+    });
     m.impl("aca", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
     m.impl("sks", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
     m.impl("tensor_aca_rect", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&,

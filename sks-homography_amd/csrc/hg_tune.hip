@@ -253,11 +253,23 @@ __global__ void empty_kernel() {}
 // 1 SKS; elem 4 (float) or 8 (double).
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream) {
-    if (algo < 0 || algo > 2 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
+    if (algo < 0 || algo > 4 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     auto launch = [&]() -> int {
         if (algo == 2) {  // the floor: an empty kernel, raw launch, no checks
             empty_kernel<<<1, kWave, 0, st>>>();
+            return 0;
+        }
+        if (algo == 3) {  // the floor plus the error query every C-ABI call makes
+            empty_kernel<<<1, kWave, 0, st>>>();
+            return (int)hipGetLastError();
+        }
+        if (algo == 4) {  // the SoA f64 ACA kernel launched raw (no checks, no query)
+            const auto* s = static_cast<const double*>(src);
+            const auto* t = static_cast<const double*>(tar);
+            auto* h = static_cast<double*>(H);
+            solve_soa_vec<kACA, false, double, 1, false, false>
+                <<<(unsigned)soa_grid<1, false>(n / 2), kBlock, 0, st>>>(s, t, h, n);
             return 0;
         }
         if (elem == 4) {

@@ -16,7 +16,6 @@ from typing import Optional, Union
 import torch
 
 from . import _lib
-from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA
 
 _DTYPES = {torch.float32: "f32", torch.float64: "f64"}
 
@@ -57,19 +56,8 @@ def _guard(dev: torch.device):
     return torch.cuda.device(dev)
 
 
-def _as_problems(x: torch.Tensor, layout: str) -> torch.Tensor:
-    """AoS accepts (n,8) or (n,4,2) (the ACA_vanilla layout, .py:312); SoA (8,n)."""
-    if layout == "aos":
-        if x.dim() == 3 and x.shape[1:] == (4, 2):
-            x = x.reshape(x.shape[0], 8)
-        if x.dim() != 2 or x.shape[1] != 8:
-            raise ValueError(f"AoS problems must be (n,8) or (n,4,2), got {tuple(x.shape)}")
-    elif layout == "soa":
-        if x.dim() != 2 or x.shape[0] != 8:
-            raise ValueError(f"SoA problems must be (8,n), got {tuple(x.shape)}")
-    else:
-        raise ValueError(f"layout must be 'aos' or 'soa', got {layout!r}")
-    return x.contiguous()
+_ALGO_ID = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
+_LAYOUT_ID = {"aos": 0, "soa": 1}
 
 
 def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = True,
@@ -80,31 +68,24 @@ def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = Tru
 
     AoS: src/tar (n,8) or (n,4,2) -> H (n,9); SoA: (8,n) -> (9,n).
     ``normalize=True`` returns H/H[8] exactly as sks::runKernel_* (ACA_SKS.cpp:94-98);
-    False returns H up to scale as cal_Homo_* / ACA_vanilla do.
+    False returns H up to scale as cal_Homo_* / ACA_vanilla do.  Runs the native
+    torch.ops.sks_amd.solve (shape/dtype checks there; no CPU path).
     """
-    if algo not in ("aca", "sks", "ge", "gpt"):
+    algo_id = _ALGO_ID.get(algo)
+    if algo_id is None:
         raise ValueError(f"algo must be 'aca', 'sks', 'ge' or 'gpt', got {algo!r}")
-    dev = _require_device(src, tar)
-    if algo == "gpt" and src.dtype != torch.float64:
-        raise TypeError("the GPT-LU baseline (cal_Homo_GPT) is float64 only")
-    if src.dtype not in _DTYPES or tar.dtype != src.dtype:
+    lay = _LAYOUT_ID.get(layout)
+    if lay is None:
+        raise ValueError(f"layout must be 'aos' or 'soa', got {layout!r}")
+    _gpu_only(src)
+    _gpu_only(tar)
+    if src.dtype not in _DTYPES or tar.dtype is not src.dtype:
         raise TypeError(f"src/tar must both be float32 or float64, got {src.dtype}/{tar.dtype}")
-    src = _as_problems(src, layout)
-    tar = _as_problems(tar, layout)
-    if src.shape != tar.shape:
-        raise ValueError(f"src {tuple(src.shape)} and tar {tuple(tar.shape)} differ")
-    n = src.shape[0] if layout == "aos" else src.shape[1]
-    shape = (n, 9) if layout == "aos" else (9, n)
+    if algo_id == 3 and src.dtype is not torch.float64:
+        raise TypeError("the GPT-LU baseline (cal_Homo_GPT) is float64 only")
     if out is None:
-        out = torch.empty(shape, dtype=src.dtype, device=dev)
-    elif out.shape != shape or out.dtype != src.dtype or not out.is_contiguous() or out.device != dev:
-        raise ValueError(f"out must be a contiguous {shape} {src.dtype} tensor on {dev}")
-    fn = f"hg_{algo}_{_DTYPES[src.dtype]}"
-    with _guard(dev):
-        _lib.call(fn, src.data_ptr(), tar.data_ptr(), out.data_ptr(), n,
-                  HG_LAYOUT_AOS if layout == "aos" else HG_LAYOUT_SOA,
-                  HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
-    return out
+        return _OPS.solve.default(src, tar, algo_id, normalize, lay)
+    return _OPS.solve.out(src, tar, algo_id, normalize, lay, out=out)
 
 
 def aca(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torch.Tensor:

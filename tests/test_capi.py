@@ -147,7 +147,7 @@ def test_native_torch_ops_registered(pkg):
     import torch
     ops = torch.ops.sks_amd
     want = {
-        "aca": ["default", "out"], "sks": ["default", "out"],
+        "solve": ["default", "out"], "aca": ["default", "out"], "sks": ["default", "out"],
         "tensor_aca_rect": ["default", "out", "scalar", "scalar_out"],
         "tensor_aca_rect_backward": ["default"],
         "tensor_aca_offsets": ["default", "out"], "tensor_aca_offsets_backward": ["default"],
@@ -158,6 +158,8 @@ def test_native_torch_ops_registered(pkg):
     assert ops.tensor_aca_rect(m(5, 3, 4), m(5, 3, 4), m(1), m(1)).shape == (5, 3, 3)
     assert ops.tensor_aca_offsets(m(5, 2), m(5, 4, 2), 1.0, 2.0).shape == (5, 3, 3)
     assert ops.aca(m(5, 4, 2), m(5, 4, 2), True).shape == (5, 3, 3)
+    assert ops.solve(m(5, 8), m(5, 8), 1, True, 0).shape == (5, 9)
+    assert ops.solve(m(8, 7), m(8, 7), 2, False, 1).shape == (9, 7)
     g = ops.tensor_aca_rect_backward(m(5, 3, 4), m(5, 3, 4), m(5, 3, 3), m(1), m(1), True, False)
     assert [tuple(x.shape) for x in g] == [(5, 3, 4), (5, 3, 4), (0,)]
     with pytest.raises(NotImplementedError):

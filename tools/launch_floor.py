@@ -20,7 +20,12 @@ st = torch.cuda.current_stream().cuda_stream
 s = torch.rand(8, 2048, dtype=torch.float64, device=dev)
 H = torch.empty(9, 2048, dtype=torch.float64, device=dev)
 for rep in range(2):
-    row = {"empty": round(loop(2, 8, 0, 0, 0, 0, 1, 0, 20000, st), 2)}
+    row = {"empty": round(loop(2, 8, 0, 0, 0, 0, 1, 0, 20000, st), 2),
+           "empty+getlasterror": round(loop(3, 8, 0, 0, 0, 0, 1, 0, 20000, st), 2)}
+    a = torch.rand(8, 1000, dtype=torch.float64, device=dev)
+    h = torch.empty(9, 1000, dtype=torch.float64, device=dev)
+    row["aca1000_raw"] = round(loop(4, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000, 1, 0,
+                                    20000, st), 2)
     for n in (1, 2, 3, 4, 10, 1000):
         for algo in (0, 1):
             # SoA views of n problems inside the (8, 2048) buffer need stride n: use fresh tensors
