@@ -266,7 +266,7 @@ def table8_sweep(d: Dist, pkg):
     small N on both GPUs.  `python`: the same through pkg.solve.  `graph`: device time per
     launch from a HIP graph of 100 launches."""
     import ctypes
-    loop = pkg.lib().hg_tune_launch_loop
+    loop = pkg._lib.tune().hg_tune_launch_loop
     loop.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p,
                      ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                      ctypes.c_void_p]

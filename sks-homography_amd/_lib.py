@@ -12,6 +12,7 @@ import threading
 HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_amd.so")
 TORCH_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_torch.so")
+TUNE_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_tune.so")
 
 HG_LAYOUT_AOS = 0
 HG_LAYOUT_SOA = 1
@@ -81,6 +82,21 @@ def lib() -> ctypes.CDLL:
                 fn.restype = restype
             _lib = handle
     return _lib
+
+
+_tune = None
+
+
+def tune() -> ctypes.CDLL:
+    """The kernel-variant / timing-loop library (include/sks_homography_tune.h) used by
+    tools/ and tests; not part of the product path."""
+    global _tune
+    if _tune is None:
+        lib()  # the product library first (the tune library links it)
+        if not os.path.exists(TUNE_LIB_PATH):
+            raise ImportError(f"{TUNE_LIB_PATH} not built: run build()")
+        _tune = ctypes.CDLL(TUNE_LIB_PATH)
+    return _tune
 
 
 def call(name: str, *args) -> None:

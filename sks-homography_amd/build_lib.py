@@ -20,9 +20,13 @@ BUILD = os.path.join(HERE, "build")
 LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsks_homography_amd.so")
 TORCH_LIB = os.path.join(LIB_DIR, "libsks_homography_torch.so")
+TUNE_LIB = os.path.join(LIB_DIR, "libsks_homography_tune.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
-SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_tune.hip", "hg_sks_api.cpp"]
+SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_sks_api.cpp"]
+# kernel-variant sweeps and timing loops (tools/, tests): a separate library so the product
+# library carries only the shipped kernels
+TUNE_SOURCES = ["hg_tune.hip"]
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
@@ -47,11 +51,11 @@ def build(verbose: bool = False, force: bool = False) -> str:
     cc = hipcc()
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
     headers += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
-    objs = []
-    for src in SOURCES:
+    objs, tune_objs = [], []
+    for src in SOURCES + TUNE_SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
-        objs.append(obj)
+        (tune_objs if src in TUNE_SOURCES else objs).append(obj)
         if not force and not _stale(obj, [path] + headers):
             continue
         cmd = [cc, *COMMON, "-c", path, "-o", obj]
@@ -64,6 +68,12 @@ def build(verbose: bool = False, force: bool = False) -> str:
         subprocess.run(cmd, check=True)
     if force or _stale(LIB, objs):
         cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        if verbose:
+            print(" ".join(cmd))
+        subprocess.run(cmd, check=True)
+    if force or _stale(TUNE_LIB, tune_objs + [LIB]):
+        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", TUNE_LIB, *tune_objs,
+               f"-L{LIB_DIR}", "-lsks_homography_amd", "-Wl,-rpath,$ORIGIN"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -7,461 +7,12 @@
 //   hg_ransac_score_f32   H (n,9) x pool (npool) -> inlier count per hypothesis
 //
 // The scorer is the one compute-bound kernel here: every (hypothesis, point) pair
-// costs ~13 VALU ops and no HBM traffic (the pool sits in LDS, H in VGPRs), so its
-// roofline is the FP32 VALU rate, not HBM.
-#include <hip/hip_runtime.h>
-
-#include <cstdint>
-
-#include "hg_aos.hpp"
-#include "hg_solvers.hpp"
-#include "sks_homography.h"
-
-#pragma clang fp contract(off)
-
-namespace hg {
-
-constexpr uint64_t kBitsMul = 0xA0761D6478BD642Full;
-
-__global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __restrict__ out,
-                                                           int64_t count, uint64_t seed,
-                                                           uint64_t offset) {
-    const uint64_t base = seed * kBitsMul + offset;
-    const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride)
-        out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
-}
-
-// Fused sampler + solver.  A wave owns 64*P hypotheses: its 16-B index rows arrive by
-// LDS-DMA (P = 2: 2 KiB), each lane gathers its 4 correspondences from the pool
-// (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
-// LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
-// does (.cu:56-59, modulo bias and duplicates included).
-template <int ALGO, bool NORM, int P>
-__global__ __launch_bounds__(kBlock) void sample_solve_kernel(
-    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
-    constexpr int kTile = kWave * P;
-    constexpr int kIdx = kTile * 16;
-    constexpr int kLds = kIdx > kTile * 36 ? kIdx : kTile * 36;
-    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kLds];
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
-    if (base >= n) return;
-    char* lds = smem[wave];
-    const bool full = base + kTile <= n;
-    uint4 r[P];
-    if (full) {
-        dma_slab_issue<kIdx, true>(reinterpret_cast<const char*>(idx + base), lds, lane);
-        dma_wait_sync();
-#pragma unroll
-        for (int j = 0; j < P; ++j) r[j] = *reinterpret_cast<const uint4*>(lds + (j * kWave + lane) * 16);
-        wave_lds_sync();
-    } else {
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int64_t p = base + j * kWave + lane;
-            r[j] = p < n ? idx[p] : make_uint4(0, 0, 0, 0);
-        }
-    }
-    float h[P][9];
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const uint32_t id[4] = {r[j].x % npool, r[j].y % npool, r[j].z % npool, r[j].w % npool};
-        float s[8], t[8];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
-            s[2 * k] = a.x; s[2 * k + 1] = a.y;
-            t[2 * k] = b.x; t[2 * k + 1] = b.y;
-        }
-        solve<ALGO, NORM>(s, t, h[j]);
-    }
-    if (full) {
-        store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
-        return;
-    }
-#pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const int64_t p = base + j * kWave + lane;
-        if (p < n) {
-#pragma unroll
-            for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
-        }
-    }
-}
-
-// r mod d for every 32-bit r and d >= 1 by one 64-bit multiply and a high multiply
-// (Lemire, Kaser & Kurz, "Faster remainder by direct computation", 2019), with
-// M = floor((2^64 - 1) / d) + 1 computed once on the host.  Equals r % d exactly.
-__device__ __forceinline__ uint32_t fastmod_u32(uint32_t r, uint64_t M, uint32_t d) {
-    return (uint32_t)__umul64hi(M * (uint64_t)r, (uint64_t)d);
-}
-
-inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
-
-// The same sampler with the pool staged in LDS once per block: {x, y, u, v} 16-B
-// records, so a hypothesis gathers with 4 ds_read_b128 instead of 8 scattered global
-// loads through the texture path (the bound of sample_solve_kernel: 47 G hyp/s, 30 % of
-// HBM).  Persistent grid sized to the resident blocks; each wave walks its tiles with
-// the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
-// and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
-// staging to fit the block's LDS (checked on the host).
-template <int ALGO, bool NORM, int P>
-__global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
-    const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
-    constexpr int kTile = kWave * P;
-    constexpr int kStage = kTile * 36;
-    extern __shared__ __attribute__((aligned(16))) char dyn[];
-    float4* pool = reinterpret_cast<float4*>(dyn);
-    const int lane = threadIdx.x & (kWave - 1);
-    const int wave = threadIdx.x / kWave;
-    char* stage = dyn + (size_t)npool * 16 + (size_t)wave * kStage;
-    for (uint32_t i = threadIdx.x; i < npool; i += kBlock) {
-        const float2 a = pool_src[i], b = pool_tar[i];
-        pool[i] = make_float4(a.x, a.y, b.x, b.y);
-    }
-    __syncthreads();
-
-    const int64_t tiles = (n + kTile - 1) / kTile;
-    const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock;
-    int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave;
-    auto load = [&](int64_t tile, u32x4 (&r)[P]) {
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const int64_t p = tile * kTile + j * kWave + lane;
-            r[j] = p < n ? ld16<true>(reinterpret_cast<const char*>(idx + p)) : u32x4{0, 0, 0, 0};
-        }
-    };
-    u32x4 cur[P];
-    if (t < tiles) load(t, cur);
-    for (; t < tiles; t += stride) {
-        u32x4 nxt[P]{};
-        if (t + stride < tiles) load(t + stride, nxt);
-        float h[P][9];
-#pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const uint32_t id[4] = {fastmod_u32(cur[j].x, magic, npool),
-                                    fastmod_u32(cur[j].y, magic, npool),
-                                    fastmod_u32(cur[j].z, magic, npool),
-                                    fastmod_u32(cur[j].w, magic, npool)};
-            float s[8], tt[8];
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 q = pool[id[k]];
-                s[2 * k] = q.x; s[2 * k + 1] = q.y;
-                tt[2 * k] = q.z; tt[2 * k + 1] = q.w;
-            }
-            solve<ALGO, NORM>(s, tt, h[j]);
-        }
-        const int64_t base = t * kTile;
-        if (base + kTile <= n) {
-            store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, stage, lane);
-        } else {
-#pragma unroll
-            for (int j = 0; j < P; ++j) {
-                const int64_t p = base + j * kWave + lane;
-                if (p < n) {
-#pragma unroll
-                    for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < P; ++j) cur[j] = nxt[j];
-    }
-}
-
-// LDS bytes of sample_solve_lds_kernel<P> for a pool of npool points.
-template <int P>
-constexpr size_t sample_lds_bytes(uint32_t npool) {
-    return (size_t)npool * 16 + (size_t)kWavesPerBlock * kWave * P * 36;
-}
-constexpr size_t kSampleLdsMax = 64 * 1024;  // per-block dynamic LDS without opt-in
-
-// Inlier test of one (hypothesis, correspondence) pair, division-free:
-//   (x', y', w') = H (x, y, 1),  inlier <=> w' != 0 and
-//   (x' - u w')^2 + (y' - v w')^2 <= t^2 w'^2        [== |(x'/w', y'/w') - (u, v)|^2 <= t^2]
-// with this exact FMA placement (restated in oracle/hg_oracle.c).
-__device__ __forceinline__ bool is_inlier(const float (&h)[9], float4 q, float t2) {
-    const float xs = __builtin_fmaf(h[0], q.x, __builtin_fmaf(h[1], q.y, h[2]));
-    const float ys = __builtin_fmaf(h[3], q.x, __builtin_fmaf(h[4], q.y, h[5]));
-    const float ws = __builtin_fmaf(h[6], q.x, __builtin_fmaf(h[7], q.y, h[8]));
-    const float ex = __builtin_fmaf(-q.z, ws, xs);
-    const float ey = __builtin_fmaf(-q.w, ws, ys);
-    const float e2 = __builtin_fmaf(ex, ex, ey * ey);
-    const float lim = t2 * (ws * ws);
-    return (e2 <= lim) & (ws != 0.f);
-}
-
-// One lane per hypothesis; the block streams the pool through LDS in chunks of
-// kChunk points {x, y, u, v} (every lane reads the same point: an LDS broadcast).
-constexpr int kScoreChunk = 2048;  // 32 KiB of LDS per block
-
-__global__ __launch_bounds__(kBlock) void ransac_score_kernel(
-    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
-    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) float4 pts[kScoreChunk];
-    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
-    float h[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) h[k] = p < n ? H[p * 9 + k] : 0.f;
-    uint32_t cnt = 0;
-    for (uint32_t c0 = 0; c0 < npool; c0 += kScoreChunk) {
-        const uint32_t m = npool - c0 < (uint32_t)kScoreChunk ? npool - c0 : kScoreChunk;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += kBlock) {
-            const float2 a = pool_src[c0 + i], b = pool_tar[c0 + i];
-            pts[i] = make_float4(a.x, a.y, b.x, b.y);
-        }
-        __syncthreads();
-        uint32_t i = 0;
-        for (; i + 4 <= m; i += 4) {
-#pragma unroll
-            for (int u = 0; u < 4; ++u) cnt += is_inlier(h, pts[i + u], t2) ? 1u : 0u;
-        }
-        for (; i < m; ++i) cnt += is_inlier(h, pts[i], t2) ? 1u : 0u;
-    }
-    if (p < n) counts[p] = cnt;
-}
-
-// Two hypotheses per lane, evaluated as packed pairs (v_pk_fma_f32 / v_pk_mul_f32:
-// one instruction serves both), every LDS point read shared by both.  Same per-pair
-// arithmetic (and bits) as is_inlier.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-
-template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void ransac_score2_kernel(
-    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
-    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
-    __shared__ __attribute__((aligned(16))) float4 pts[kScoreChunk];
-    // lane owns hypotheses p0 = 2*gid and p0 + 1 (adjacent rows: one 72-B read)
-    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
-    f32x2 h[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        h[k].x = p0 < n ? H[p0 * 9 + k] : 0.f;
-        h[k].y = p0 + 1 < n ? H[(p0 + 1) * 9 + k] : 0.f;
-    }
-    const f32x2 t2v = {t2, t2};
-    i32x2 cnt = {0, 0};
-    for (uint32_t c0 = 0; c0 < npool; c0 += kScoreChunk) {
-        const uint32_t m = npool - c0 < (uint32_t)kScoreChunk ? npool - c0 : kScoreChunk;
-        __syncthreads();
-        for (uint32_t i = threadIdx.x; i < m; i += kBlock) {
-            const float2 a = pool_src[c0 + i], b = pool_tar[c0 + i];
-            pts[i] = make_float4(a.x, a.y, b.x, b.y);
-        }
-        __syncthreads();
-        auto pair = [&](float4 q) {
-            const f32x2 x = {q.x, q.x}, y = {q.y, q.y}, nu = {-q.z, -q.z}, nv = {-q.w, -q.w};
-            const f32x2 xs = __builtin_elementwise_fma(h[0], x, __builtin_elementwise_fma(h[1], y, h[2]));
-            const f32x2 ys = __builtin_elementwise_fma(h[3], x, __builtin_elementwise_fma(h[4], y, h[5]));
-            const f32x2 ws = __builtin_elementwise_fma(h[6], x, __builtin_elementwise_fma(h[7], y, h[8]));
-            const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
-            const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
-            const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
-            const f32x2 lim = t2v * (ws * ws);
-            const f32x2 zero = {0.f, 0.f};
-            cnt -= (e2 <= lim) & (ws != zero);   // vector compares yield -1 / 0
-        };
-        uint32_t i = 0;
-        for (; i + UNROLL <= m; i += UNROLL) {
-#pragma unroll
-            for (int u = 0; u < UNROLL; ++u) pair(pts[i + u]);
-        }
-        for (; i < m; ++i) pair(pts[i]);
-    }
-    if (p0 < n) counts[p0] = (uint32_t)cnt.x;
-    if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
-}
-
-// Pool points through the scalar unit instead of LDS: every lane of a wave needs the
-// same point, so the loads are wave-uniform -- s_load into SGPRs that the packed VALU
-// ops read directly.  No LDS (occupancy is then set by VGPRs alone), no block barriers,
-// no chunking; the pool (16 B per pair) streams through the scalar cache / L2.
-template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void ransac_score_sgpr_kernel(
-    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
-    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
-    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 2;
-    f32x2 h[9];
-#pragma unroll
-    for (int k = 0; k < 9; ++k) {
-        h[k].x = p0 < n ? H[p0 * 9 + k] : 0.f;
-        h[k].y = p0 + 1 < n ? H[(p0 + 1) * 9 + k] : 0.f;
-    }
-    const f32x2 t2v = {t2, t2};
-    i32x2 cnt = {0, 0};
-    auto pair = [&](float2 a, float2 b) {
-        const f32x2 x = {a.x, a.x}, y = {a.y, a.y}, nu = {-b.x, -b.x}, nv = {-b.y, -b.y};
-        const f32x2 xs = __builtin_elementwise_fma(h[0], x, __builtin_elementwise_fma(h[1], y, h[2]));
-        const f32x2 ys = __builtin_elementwise_fma(h[3], x, __builtin_elementwise_fma(h[4], y, h[5]));
-        const f32x2 ws = __builtin_elementwise_fma(h[6], x, __builtin_elementwise_fma(h[7], y, h[8]));
-        const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
-        const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
-        const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
-        const f32x2 lim = t2v * (ws * ws);
-        const f32x2 zero = {0.f, 0.f};
-        cnt -= (e2 <= lim) & (ws != zero);
-    };
-    uint32_t i = 0;
-    for (; i + UNROLL <= npool; i += UNROLL) {
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) pair(pool_src[i + u], pool_tar[i + u]);
-    }
-    for (; i < npool; ++i) pair(pool_src[i], pool_tar[i]);
-    if (p0 < n) counts[p0] = (uint32_t)cnt.x;
-    if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
-}
-
-int cu_count() {
-    static int cus = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 256;
-        return v > 0 ? v : 256;
-    }();
-    return cus;
-}
-
-// variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
-// P = 1 / 2 (falls back to 0 when the pool does not fit).
-int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
-                        const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
-    constexpr int kShippedP = 2;
-    int use_p = variant == -1 ? kShippedP : variant;
-    const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
-    if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
-    if (use_p == 0) {
-        constexpr int P = 2;
-        const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
-        if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
-        const unsigned g = (unsigned)blocks;
-#define HG_SS(A, N) sample_solve_kernel<A, N, P><<<g, kBlock, 0, s>>>(ps, pt, npool, ix, H, n)
-        if (algo == 0) { if (norm) HG_SS(kACA, true); else HG_SS(kACA, false); }
-        else { if (norm) HG_SS(kSKS, true); else HG_SS(kSKS, false); }
-#undef HG_SS
-        return (int)hipGetLastError();
-    }
-    // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
-    const int64_t tiles = (n + (int64_t)kWave * use_p - 1) / ((int64_t)kWave * use_p);
-    const int64_t want = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
-    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
-    const int64_t cap = per_cu * cu_count();
-    const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = fastmod_magic(npool);
-#define HG_SL(PP, A, N) \
-    sample_solve_lds_kernel<A, N, PP><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
-    if (use_p == 1) {
-        if (algo == 0) { if (norm) HG_SL(1, kACA, true); else HG_SL(1, kACA, false); }
-        else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
-    } else {
-        if (algo == 0) { if (norm) HG_SL(2, kACA, true); else HG_SL(2, kACA, false); }
-        else { if (norm) HG_SL(2, kSKS, true); else HG_SL(2, kSKS, false); }
-    }
-#undef HG_SL
-    return (int)hipGetLastError();
-}
-
-// Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice
-// the arithmetic, half the waves.
-template <int UNROLL>
-__global__ __launch_bounds__(kBlock) void ransac_score_sgpr4_kernel(
-    const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
-    const float2* __restrict__ pool_tar, uint32_t npool, float t2, uint32_t* __restrict__ counts) {
-    const int64_t p0 = ((int64_t)blockIdx.x * kBlock + threadIdx.x) * 4;
-    f32x2 h[2][9];
-#pragma unroll
-    for (int q = 0; q < 2; ++q)
-#pragma unroll
-        for (int k = 0; k < 9; ++k) {
-            const int64_t a = p0 + 2 * q, b = a + 1;
-            h[q][k].x = a < n ? H[a * 9 + k] : 0.f;
-            h[q][k].y = b < n ? H[b * 9 + k] : 0.f;
-        }
-    const f32x2 t2v = {t2, t2};
-    i32x2 cnt[2] = {{0, 0}, {0, 0}};
-    auto pair = [&](float2 a, float2 b) {
-        const f32x2 x = {a.x, a.x}, y = {a.y, a.y}, nu = {-b.x, -b.x}, nv = {-b.y, -b.y};
-#pragma unroll
-        for (int q = 0; q < 2; ++q) {
-            const f32x2 xs = __builtin_elementwise_fma(h[q][0], x, __builtin_elementwise_fma(h[q][1], y, h[q][2]));
-            const f32x2 ys = __builtin_elementwise_fma(h[q][3], x, __builtin_elementwise_fma(h[q][4], y, h[q][5]));
-            const f32x2 ws = __builtin_elementwise_fma(h[q][6], x, __builtin_elementwise_fma(h[q][7], y, h[q][8]));
-            const f32x2 ex = __builtin_elementwise_fma(nu, ws, xs);
-            const f32x2 ey = __builtin_elementwise_fma(nv, ws, ys);
-            const f32x2 e2 = __builtin_elementwise_fma(ex, ex, ey * ey);
-            const f32x2 lim = t2v * (ws * ws);
-            const f32x2 zero = {0.f, 0.f};
-            cnt[q] -= (e2 <= lim) & (ws != zero);
-        }
-    };
-    uint32_t i = 0;
-    for (; i + UNROLL <= npool; i += UNROLL) {
-#pragma unroll
-        for (int u = 0; u < UNROLL; ++u) pair(pool_src[i + u], pool_tar[i + u]);
-    }
-    for (; i < npool; ++i) pair(pool_src[i], pool_tar[i]);
-#pragma unroll
-    for (int q = 0; q < 2; ++q) {
-        const int64_t a = p0 + 2 * q;
-        if (a < n) counts[a] = (uint32_t)cnt[q].x;
-        if (a + 1 < n) counts[a + 1] = (uint32_t)cnt[q].y;
-    }
-}
-
-}  // namespace hg
+// costs ~9 wave64 VALU instructions and no HBM traffic (the pool streams through the
+// scalar cache, H sits in VGPRs), so its roofline is the FP32 VALU rate, not HBM.
+// Kernels: hg_ransac.hpp.
+#include "hg_ransac.hpp"
 
 extern "C" {
-
-// Sampler variants for tools/kbench_sample.py (0 global gather, 1 / 2 LDS pool P1 / P2);
-// same argument checks as hg_sample_solve_f32.
-int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
-                   const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
-    if (n <= 0 || npool == 0 || variant < 0 || variant > 2 || (algo != 0 && algo != 1))
-        return (int)hipErrorInvalidValue;
-    if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
-        (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
-        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
-        return (int)hipErrorInvalidValue;
-    return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
-                                   reinterpret_cast<const float2*>(pool_tar), npool,
-                                   reinterpret_cast<const uint4*>(idx), H, n, algo,
-                                   (flags & HG_FLAG_NORMALIZE) != 0,
-                                   reinterpret_cast<hipStream_t>(stream));
-}
-
-// Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
-// 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4), 3 / 4 = two
-// per lane packed, pool through scalar loads (unroll 4 / 8).
-int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
-                  const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
-                  void* stream) {
-    if (n <= 0 || !H || !counts) return (int)hipErrorInvalidValue;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const float t2 = thresh * thresh;
-    const auto* ps = reinterpret_cast<const float2*>(pool_src);
-    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
-    const int64_t b1 = (n + hg::kBlock - 1) / hg::kBlock;
-    const int64_t b2 = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
-    switch (variant) {
-        case 0: hg::ransac_score_kernel<<<(unsigned)b1, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 1: hg::ransac_score2_kernel<1><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 2: hg::ransac_score2_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 3: hg::ransac_score_sgpr_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 4: hg::ransac_score_sgpr_kernel<8><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 5: hg::ransac_score_sgpr4_kernel<4><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        case 6: hg::ransac_score_sgpr4_kernel<8><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
-        default: return (int)hipErrorInvalidValue;
-    }
-    return (int)hipGetLastError();
-}
 
 int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset, void* stream) {
     if (count < 0) return (int)hipErrorInvalidValue;

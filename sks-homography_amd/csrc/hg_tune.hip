@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hg_aos.hpp"
+#include "hg_ransac.hpp"
 #include "hg_rect.hpp"
 #include "hg_soa.hpp"
 #include "sks_homography.h"
@@ -303,6 +304,49 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
     (void)hipEventDestroy(e0);
     (void)hipEventDestroy(e1);
     return rc ? -(double)rc : (double)ms * 1e3 / loops;
+}
+
+// Sampler variants for tools/kbench_sample.py (0 global gather, 1 / 2 LDS pool P1 / P2);
+// same argument checks as hg_sample_solve_f32.
+int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
+                   const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 2 || (algo != 0 && algo != 1))
+        return (int)hipErrorInvalidValue;
+    if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
+        (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
+        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return (int)hipErrorInvalidValue;
+    return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
+                                   reinterpret_cast<const float2*>(pool_tar), npool,
+                                   reinterpret_cast<const uint4*>(idx), H, n, algo,
+                                   (flags & HG_FLAG_NORMALIZE) != 0,
+                                   reinterpret_cast<hipStream_t>(stream));
+}
+
+// Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
+// 1 = two per lane packed (unroll 1), 2 = two per lane packed (unroll 4), 3 / 4 = two
+// per lane packed, pool through scalar loads (unroll 4 / 8).
+int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
+                  const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
+                  void* stream) {
+    if (n <= 0 || !H || !counts) return (int)hipErrorInvalidValue;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const float t2 = thresh * thresh;
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const int64_t b1 = (n + hg::kBlock - 1) / hg::kBlock;
+    const int64_t b2 = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
+    switch (variant) {
+        case 0: hg::ransac_score_kernel<<<(unsigned)b1, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 1: hg::ransac_score2_kernel<1><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 2: hg::ransac_score2_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 3: hg::ransac_score_sgpr_kernel<4><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 4: hg::ransac_score_sgpr_kernel<8><<<(unsigned)b2, hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 5: hg::ransac_score_sgpr4_kernel<4><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        case 6: hg::ransac_score_sgpr4_kernel<8><<<(unsigned)((n + 4 * hg::kBlock - 1) / (4 * hg::kBlock)), hg::kBlock, 0, s>>>(H, n, ps, pt, npool, t2, counts); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
 }
 
 }  // extern "C"

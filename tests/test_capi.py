@@ -13,8 +13,8 @@ from conftest import ROOT
 INCLUDE = os.path.join(ROOT, "include")
 
 
-def _c_decls():
-    text = open(os.path.join(INCLUDE, "sks_homography.h")).read()
+def _c_decls(header="sks_homography.h"):
+    text = open(os.path.join(INCLUDE, header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(hg_\w+)\s*\(", text)))
 
@@ -31,6 +31,17 @@ def test_library_exports_every_c_symbol(pkg):
     for name in _c_decls():
         assert hasattr(lib, name), f"{name} declared in sks_homography.h but not exported"
     assert set(_c_decls()) == set(pkg._lib.SIGNATURES), "ctypes table out of sync with header"
+
+
+def test_tune_library_exports_its_header(pkg):
+    """include/sks_homography_tune.h (kernel-variant sweeps, timing loops) is served by
+    lib/libsks_homography_tune.so; the product library carries none of it."""
+    tune, lib = pkg._lib.tune(), pkg.lib()
+    decls = _c_decls("sks_homography_tune.h")
+    assert decls
+    for name in decls:
+        assert hasattr(tune, name), f"{name} declared in sks_homography_tune.h but not exported"
+        assert not hasattr(lib, name), f"{name} leaked into the product library"
 
 
 def test_cpp_api_links_against_library(pkg):

@@ -61,7 +61,7 @@ def test_ransac_end_to_end(oracle, pkg, dev):
 
 def _tune_sample(pkg):
     import ctypes
-    f = pkg.lib().hg_tune_sample
+    f = pkg._lib.tune().hg_tune_sample
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     f.restype = ctypes.c_int

@@ -16,7 +16,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 def main():
     pkg = ge.load_package()
-    f = pkg.lib().hg_tune_copy
+    f = pkg._lib.tune().hg_tune_copy
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
     f.restype = ctypes.c_int
     dev = torch.device("cuda:0")

@@ -25,7 +25,7 @@ def main():
     rounds = int(os.environ.get("KB_ROUNDS", 7))
     iters = int(os.environ.get("KB_ITERS", 30))
     pkg = ge.load_package()
-    lib = pkg.lib()
+    lib = pkg._lib.tune()
     lib.hg_tune_num_variants.restype = ctypes.c_int
     lib.hg_tune_variant_name.restype = ctypes.c_char_p
     lib.hg_tune_variant_name.argtypes = [ctypes.c_int]

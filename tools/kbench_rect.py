@@ -23,7 +23,7 @@ NAMES = ["rect P1 (shipped)", "rect P2", "rect P4", "offsets P1 (shipped)", "off
 
 def main():
     pkg = ge.load_package()
-    lib = pkg.lib()
+    lib = pkg._lib.tune()
     f = lib.hg_tune_rect
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                   ctypes.c_float, ctypes.c_float, ctypes.c_void_p]

@@ -21,7 +21,7 @@ NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2"}
 
 def main():
     pkg = ge.load_package()
-    f = pkg.lib().hg_tune_sample
+    f = pkg._lib.tune().hg_tune_sample
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     f.restype = ctypes.c_int

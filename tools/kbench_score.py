@@ -19,7 +19,7 @@ NV = 7  # hg_tune_score variants (csrc/hg_ransac.hip)
 
 def main():
     pkg = ge.load_package()
-    lib = pkg.lib()
+    lib = pkg._lib.tune()
     lib.hg_tune_score.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_uint32, ctypes.c_float,
                                   ctypes.c_void_p, ctypes.c_void_p]

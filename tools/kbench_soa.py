@@ -19,7 +19,7 @@ def main():
     n = int(os.environ.get("KB_N", 10_000_000))
     rounds, iters = 5, 20
     pkg = ge.load_package()
-    lib = pkg.lib()
+    lib = pkg._lib.tune()
     lib.hg_tune_num_soa_variants.restype = ctypes.c_int
     lib.hg_tune_soa_variant_name.restype = ctypes.c_char_p
     lib.hg_tune_soa_variant_name.argtypes = [ctypes.c_int]

@@ -16,7 +16,7 @@ import __graft_entry__ as ge  # noqa: E402
 
 def main():
     pkg = ge.load_package()
-    lib = pkg.lib()
+    lib = pkg._lib.tune()
     lib.hg_tune_soa_variant_name.restype = ctypes.c_char_p
     lib.hg_tune_soa_variant_name.argtypes = [ctypes.c_int]
     f = lib.hg_tune_soa
