@@ -169,6 +169,31 @@ __global__ __launch_bounds__(kBlock) void write_only(u32x4* __restrict__ dst, in
     }
 }
 
+__global__ void empty_kernel() {}
+__global__ void store_one_kernel(uint32_t* p) {
+    if (threadIdx.x == 0) p[0] = 1u;
+}
+// one lane per problem, plain loads/stores (the latency probe's generic form)
+template <int ALGO, bool NORM, typename T, bool SOA>
+__global__ __launch_bounds__(kBlock) void solve_generic_t(const T* __restrict__ src,
+                                                          const T* __restrict__ tar,
+                                                          T* __restrict__ H, int64_t n) {
+    const int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (p >= n) return;
+    T s[8], t[8], h[9];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s[k] = SOA ? src[(int64_t)k * n + p] : src[p * 8 + k];
+        t[k] = SOA ? tar[(int64_t)k * n + p] : tar[p * 8 + k];
+    }
+    solve<ALGO, NORM>(s, t, h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        if (SOA) H[(int64_t)k * n + p] = h[k];
+        else H[p * 9 + k] = h[k];
+    }
+}
+
 }  // namespace
 
 extern "C" {
@@ -246,15 +271,13 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
     return (int)hipGetLastError();
 }
 
-__global__ void empty_kernel() {}
-
 // cal_ACA's timing loop (GPU_Runtime Test.cu:1183-1200) in native code: `loops` back-to-
 // back launches of the C-ABI solver from a C++ loop, bracketed by HIP events on
 // `stream`.  Returns microseconds per launch, or -(hipError_t) on failure.  algo 0 ACA,
 // 1 SKS; elem 4 (float) or 8 (double).
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream) {
-    if (algo < 0 || algo > 4 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
+    if (algo < 0 || algo > 7 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     auto launch = [&]() -> int {
         if (algo == 2) {  // the floor: an empty kernel, raw launch, no checks
@@ -264,6 +287,25 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
         if (algo == 3) {  // the floor plus the error query every C-ABI call makes
             empty_kernel<<<1, kWave, 0, st>>>();
             return (int)hipGetLastError();
+        }
+        if (algo == 5 || algo == 6) {  // raw, non-temporal stores / one-dword kernel
+            if (algo == 6) {
+                store_one_kernel<<<1, kWave, 0, st>>>(static_cast<uint32_t*>(H));
+                return 0;
+            }
+            const auto* s = static_cast<const double*>(src);
+            const auto* t = static_cast<const double*>(tar);
+            auto* h = static_cast<double*>(H);
+            solve_soa_vec<kACA, false, double, 1, false, true>
+                <<<(unsigned)soa_grid<1, false>(n / 2), kBlock, 0, st>>>(s, t, h, n);
+            return 0;
+        }
+        if (algo == 7) {  // raw generic (one lane per problem, plain accesses)
+            const auto* s = static_cast<const double*>(src);
+            const auto* t = static_cast<const double*>(tar);
+            auto* h = static_cast<double*>(H);
+            solve_generic_t<kACA, false, double, true><<<(unsigned)((n + kBlock - 1) / kBlock), kBlock, 0, st>>>(s, t, h, n);
+            return 0;
         }
         if (algo == 4) {  // the SoA f64 ACA kernel launched raw (no checks, no query)
             const auto* s = static_cast<const double*>(src);

@@ -26,6 +26,11 @@ for rep in range(2):
     h = torch.empty(9, 1000, dtype=torch.float64, device=dev)
     row["aca1000_raw"] = round(loop(4, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000, 1, 0,
                                     20000, st), 2)
+    row["aca1000_raw_nt"] = round(loop(5, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000, 1, 0,
+                                       20000, st), 2)
+    row["store_one"] = round(loop(6, 8, 0, 0, h.data_ptr(), 0, 1, 0, 20000, st), 2)
+    row["aca1000_generic_raw"] = round(loop(7, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000,
+                                            1, 0, 20000, st), 2)
     for n in (1, 2, 3, 4, 10, 1000):
         for algo in (0, 1):
             # SoA views of n problems inside the (8, 2048) buffer need stride n: use fresh tensors
