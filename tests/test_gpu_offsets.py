@@ -129,3 +129,16 @@ def test_native_ops_pass_torch_opcheck(pkg, dev):
                           test_utils=("test_schema", "test_faketensor"))
     torch.library.opcheck(ops.sks.default, (q, q + 1.5, False),
                           test_utils=("test_schema", "test_faketensor"))
+
+
+def test_fit_offsets_example(pkg, dev):
+    """examples/fit_offsets.py: gradient descent through the compact TensorACA op and its
+    HIP backward recovers known corner offsets (the deep-homography training signal)."""
+    import importlib.util
+    import os
+    from conftest import ROOT
+    spec = importlib.util.spec_from_file_location("fit_offsets",
+                                                  os.path.join(ROOT, "examples", "fit_offsets.py"))
+    mod = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(mod)
+    assert mod.fit(batch=2048, steps=300) < 0.5
