@@ -172,7 +172,9 @@ def graph_of(d: Dist, fn, calls: int):
     with torch.cuda.stream(s):
         fn()  # warm the allocator on the capture stream
         g = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(g, stream=s):
+        # thread-local capture: under RCCL (N > 1) the process group's watchdog thread
+        # queries events while we capture, which a global-mode capture would reject
+        with torch.cuda.graph(g, stream=s, capture_error_mode="thread_local"):
             for _ in range(calls):
                 fn()
     torch.cuda.current_stream(d.dev).wait_stream(s)
