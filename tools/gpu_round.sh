@@ -35,7 +35,13 @@ for step in $STEPS; do
         bench) run bench 600 python bench.py ;;
         prof)
             run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
-                -d "$OUT/prof_$TAG" -o run -- python3 bench.py --no-cpu ;;
+                -d "$OUT/prof_$TAG" -o run -- python3 bench.py --no-cpu
+            # the per-launch trace (~50 K launches) is reduced here and compressed, so the
+            # session's output stays under gpurun's 64 MiB copy-back limit
+            grep '^{' "$OUT/prof.log" > "$OUT/prof_$TAG/bench_line.json" || true
+            python3 tools/prof_agree.py "$OUT/prof_$TAG/run_kernel_trace.csv" \
+                "$OUT/prof_$TAG/bench_line.json" "$OUT/prof_$TAG/prof_agreement.json" > /dev/null || true
+            gzip -f "$OUT/prof_$TAG/run_kernel_trace.csv" || true ;;
         pmc)
             # HBM traffic: separate passes (FETCH_SIZE and WRITE_SIZE can't share one), no
             # tracing domains; a fixed short dispatch list (tools/pmc_run.py)
