@@ -561,3 +561,30 @@ def test_sum_rows_fixed_order(orc, pkg, dev, rows, cols):
         outs.append(out.cpu().numpy())
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
     _bits(orc, outs[0], want, f"sum_rows {rows}x{cols}")
+
+
+def test_concurrent_streams(orc, oracle, pkg, dev):
+    """Launches on four streams at once (each its own batch, algorithm and layout) finish
+    with the oracle's bits: no shared state between calls (thread-safe per
+    stream)."""
+    n = 200_003
+    jobs = []
+    for k, (algo, layout) in enumerate((("aca", "aos"), ("sks", "aos"), ("aca", "soa"),
+                                        ("sks", "soa"))):
+        src = pkg.fill_uniform(n * 8, 100 + k, 0, device=dev).view(n, 8)
+        tar = pkg.fill_uniform(n * 8, 100 + k, n * 8, device=dev).view(n, 8)
+        if layout == "soa":
+            src, tar = src.T.contiguous(), tar.T.contiguous()
+        jobs.append((algo, layout, src, tar, torch.cuda.Stream(dev)))
+    torch.cuda.synchronize(dev)
+    outs = []
+    for algo, layout, src, tar, st in jobs:
+        with torch.cuda.stream(st):
+            outs.append(pkg.solve(algo, src, tar, normalize=True, layout=layout))
+    torch.cuda.synchronize(dev)
+    for (algo, layout, src, tar, _), H in zip(jobs, outs):
+        s, t = src.cpu().numpy(), tar.cpu().numpy()
+        if layout == "soa":
+            s, t, H = s.T, t.T, H.T
+        _bits(orc, H, oracle.solve(algo, np.ascontiguousarray(s), np.ascontiguousarray(t)),
+              f"{algo} {layout} on its own stream")
