@@ -69,6 +69,11 @@ for step in $STEPS; do
             run dist2 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 20 \
                 --warmup 2 --no-extras --dist-backend gloo ;;
+        dist4)
+            # four ranks over gloo on the one GPU (the split / gather with 3 peers)
+            run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
+                --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 4 --steps 10 \
+                --warmup 2 --no-extras --dist-backend gloo ;;
         torchrun1)
             run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 50 \
