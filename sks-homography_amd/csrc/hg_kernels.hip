@@ -182,7 +182,13 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
         constexpr int V = 16 / sizeof(T);
         if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H)) {
             const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
-            if (cached)
+            if (sizeof(T) == 8 && !cached) {
+                // f64 beyond the MALL: the LDS-DMA tile form, 0-4 % ahead of the register
+                // form box to box (tools/kbench_soa.py, profiles/r01/kbench_soa_dma.json)
+                const int64_t tile = (int64_t)kWave * V * kWavesPerBlock;
+                solve_soa_dma<ALGO, NORM, T, true>
+                    <<<(unsigned)((n + tile - 1) / tile), kBlock, 0, s>>>(src, tar, H, n);
+            } else if (cached)
                 solve_soa_vec<ALGO, NORM, T, kSoaG, false, false><<<g, kBlock, 0, s>>>(src, tar, H, n);
             else
                 solve_soa_vec<ALGO, NORM, T, kSoaG, false, true><<<g, kBlock, 0, s>>>(src, tar, H, n);

@@ -59,6 +59,75 @@ __global__ __launch_bounds__(kBlock) void solve_soa_vec(const T* __restrict__ sr
     }
 }
 
+// Experiment (hg_tune.hip): the AoS kernel's tile form for SoA -- a wave's 64*V problems
+// are 16 component-row slabs of 1 KiB each, all landed in LDS by LDS-DMA behind one
+// wait, then read per lane from LDS; H rows leave as 1 KiB lane-consecutive stores.
+// Needs n % V == 0 and 16-B aligned bases.  The ragged last tile goes per lane.
+template <int ALGO, bool NORM, typename T, bool NT>
+__global__ __launch_bounds__(kBlock) void solve_soa_dma(const T* __restrict__ src,
+                                                        const T* __restrict__ tar,
+                                                        T* __restrict__ H, int64_t n) {
+    constexpr int V = 16 / sizeof(T);
+    constexpr int kTile = kWave * V;
+    constexpr int kRow = kWave * 16;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][16 * kRow];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kTile;
+    if (base >= n) return;
+    char* lds = smem[wave];
+    if (base + kTile <= n) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            dma_slab_issue<kRow, NT>(reinterpret_cast<const char*>(src + (int64_t)k * n + base),
+                                     lds + k * kRow, lane);
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+            dma_slab_issue<kRow, NT>(reinterpret_cast<const char*>(tar + (int64_t)k * n + base),
+                                     lds + (8 + k) * kRow, lane);
+        dma_wait_sync();
+        T s[8][V], t[8][V];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            __builtin_memcpy(s[k], lds + k * kRow + lane * 16, 16);
+            __builtin_memcpy(t[k], lds + (8 + k) * kRow + lane * 16, 16);
+        }
+        T h[V][9];
+#pragma unroll
+        for (int v = 0; v < V; ++v) {
+            T sv[8], tv[8];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) { sv[k] = s[k][v]; tv[k] = t[k][v]; }
+            solve<ALGO, NORM>(sv, tv, h[v]);
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            T o[V];
+#pragma unroll
+            for (int v = 0; v < V; ++v) o[v] = h[v][k];
+            u32x4 w;
+            __builtin_memcpy(&w, o, 16);
+            st16<NT>(H + (int64_t)k * n + base + lane * V, w);
+        }
+        return;
+    }
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        const int64_t p = base + lane * V + v;
+        if (p < n) {
+            T sv[8], tv[8], h[9];
+#pragma unroll
+            for (int k = 0; k < 8; ++k) {
+                sv[k] = src[(int64_t)k * n + p];
+                tv[k] = tar[(int64_t)k * n + p];
+            }
+            solve<ALGO, NORM>(sv, tv, h);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) H[(int64_t)k * n + p] = h[k];
+        }
+    }
+}
+
 template <int G, bool PERSIST>
 inline int64_t soa_grid(int64_t groups, int per_cu = 8) {
     const int64_t chunks = (groups + (int64_t)kBlock * G - 1) / ((int64_t)kBlock * G);

@@ -123,6 +123,21 @@ int launch_soa(int algo, const void* s, const void* t, void* H, int64_t n, int p
     return (int)hipGetLastError();
 }
 
+template <typename T>
+int launch_soa_dma(int algo, const void* s, const void* t, void* H, int64_t n, int,
+                   hipStream_t st) {
+    constexpr int V = 16 / sizeof(T);
+    if (n % V) return (int)hipErrorInvalidValue;
+    const int64_t tile = (int64_t)kWave * V * kWavesPerBlock;
+    const unsigned g = (unsigned)((n + tile - 1) / tile);
+    const T* a = (const T*)s;
+    const T* b = (const T*)t;
+    T* h = (T*)H;
+    if (algo == 0) solve_soa_dma<kACA, false, T, true><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else solve_soa_dma<kSKS, false, T, true><<<g, kBlock, 0, st>>>(a, b, h, n);
+    return (int)hipGetLastError();
+}
+
 struct SoaVariant {
     const char* name;
     int (*launch)(int, const void*, const void*, void*, int64_t, int, hipStream_t);
@@ -138,6 +153,8 @@ const SoaVariant kSoaVariants[] = {
     {"f32 G1 persist", launch_soa<float, 1, true>},
     {"f64 G1 one-shot plain (cached) ld/st", launch_soa<double, 1, false, false>},
     {"f32 G1 one-shot plain (cached) ld/st", launch_soa<float, 1, false, false>},
+    {"f64 LDS-DMA tile nt", launch_soa_dma<double>},
+    {"f32 LDS-DMA tile nt", launch_soa_dma<float>},
 };
 
 // The HBM ceilings either side of a copy: read-only (every 16-B load folded into a

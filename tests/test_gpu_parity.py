@@ -588,3 +588,17 @@ def test_concurrent_streams(orc, oracle, pkg, dev):
             s, t, H = s.T, t.T, H.T
         _bits(orc, H, oracle.solve(algo, np.ascontiguousarray(s), np.ascontiguousarray(t)),
               f"{algo} {layout} on its own stream")
+
+
+@pytest.mark.parametrize("algo", ["aca", "sks"])
+def test_soa_f64_beyond_mall_vs_oracle(orc, oracle, pkg, dev, algo):
+    """f64 SoA batches past the cache-policy threshold take the LDS-DMA tile kernel; a
+    ragged size (not a multiple of the 512-problem block tile) checks its tail path."""
+    n = 1_234_566
+    rng = np.random.default_rng(n)
+    s = rng.uniform(0, 1024, (8, n))
+    t = rng.uniform(0, 1024, (8, n))
+    for norm in (False, True):
+        H = pkg.solve(algo, _t(s, dev), _t(t, dev), normalize=norm, layout="soa")
+        _bits(orc, H, oracle.solve(algo, s, t, normalize=norm, layout="soa"),
+              f"{algo} f64 SoA n={n} norm={norm}")
