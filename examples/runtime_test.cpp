@@ -1,0 +1,154 @@
+// runtime_test.cpp -- the reference GPU harness's flow ("C++ Codes/Runtime Test/GPU_Runtime
+// Test/GPU_Runtime Test.cu": read_points, random 4-point draws from the correspondence
+// file, cal_ACA / cal_SKS / cal_GPT / cal_GE timing loops) as a native C++ caller of the
+// MI355X C ABI.  For each batch size N it gathers N random 4-subsets of the file's
+// correspondences into the harness's SoA binary64 layout ((8,N) src / tar, (9,N) H), then
+// times back-to-back launches the way cal_ACA does (one calibration launch, loops sized
+// from it, event-timed mean) and checks ACA against the GE baseline.
+//
+//   runtime_test <points.txt> [max_N] [seconds_per_case]
+//
+// Build (tests/test_gpu_cpp_api.py does):
+//   g++ -std=c++17 -O2 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__
+//       examples/runtime_test.cpp -Lsks-homography_amd/lib -lsks_homography_amd
+//       -L/opt/rocm/lib -lamdhip64 -o runtime_test
+#include <hip/hip_runtime_api.h>
+
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstdlib>
+#include <fstream>
+#include <random>
+#include <string>
+#include <vector>
+
+#include "sks_homography.h"
+
+namespace {
+
+#define CHECK(call)                                                                  \
+    do {                                                                             \
+        const int rc_ = (int)(call);                                                 \
+        if (rc_ != 0) {                                                              \
+            std::fprintf(stderr, "%s:%d: %s -> error %d\n", __FILE__, __LINE__, #call, \
+                         rc_);                                                       \
+            std::exit(1);                                                            \
+        }                                                                            \
+    } while (0)
+
+// The reference's point-file format (CPU_Runtime Test/utils.cpp:6-21): a count line,
+// then "x1 y1 x2 y2" per correspondence.
+bool read_points(const std::string& path, std::vector<double>& p1, std::vector<double>& p2) {
+    std::ifstream in(path);
+    long count = 0;
+    if (!(in >> count) || count <= 0) return false;
+    p1.resize(2 * count);
+    p2.resize(2 * count);
+    for (long i = 0; i < count; ++i) {
+        float x1, y1, x2, y2;  // the reference parses with %f (binary32)
+        if (!(in >> x1 >> y1 >> x2 >> y2)) return false;
+        p1[2 * i] = x1; p1[2 * i + 1] = y1;
+        p2[2 * i] = x2; p2[2 * i + 1] = y2;
+    }
+    return true;
+}
+
+using SolveF64 = int (*)(const double*, const double*, double*, int64_t, int, int, void*);
+
+// cal_ACA's statistic: one launch to calibrate, loops = budget / that time, mean per launch.
+double time_launches(SolveF64 fn, const double* s, const double* t, double* h, int64_t n,
+                     double budget_ms) {
+    hipEvent_t e0, e1;
+    CHECK(hipEventCreate(&e0));
+    CHECK(hipEventCreate(&e1));
+    float ms = 0.f;
+    CHECK(hipEventRecord(e0, nullptr));
+    CHECK(fn(s, t, h, n, HG_LAYOUT_SOA, 0, nullptr));
+    CHECK(hipEventRecord(e1, nullptr));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    int loops = (int)(budget_ms / (ms > 1e-3f ? ms : 1e-3f));
+    loops = loops < 10 ? 10 : (loops > 200000 ? 200000 : loops);
+    for (int i = 0; i < loops; ++i) CHECK(fn(s, t, h, n, HG_LAYOUT_SOA, 0, nullptr));  // warm
+    CHECK(hipEventRecord(e0, nullptr));
+    for (int i = 0; i < loops; ++i) CHECK(fn(s, t, h, n, HG_LAYOUT_SOA, 0, nullptr));
+    CHECK(hipEventRecord(e1, nullptr));
+    CHECK(hipEventSynchronize(e1));
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    CHECK(hipEventDestroy(e0));
+    CHECK(hipEventDestroy(e1));
+    return (double)ms * 1e3 / loops;  // microseconds
+}
+
+}  // namespace
+
+int main(int argc, char** argv) {
+    if (argc < 2) {
+        std::fprintf(stderr, "usage: %s <points.txt> [max_N] [seconds_per_case]\n", argv[0]);
+        return 2;
+    }
+    const int64_t max_n = argc > 2 ? std::atoll(argv[2]) : 1000000;
+    const double budget_ms = (argc > 3 ? std::atof(argv[3]) : 0.2) * 1e3;
+    std::vector<double> p1, p2;
+    if (!read_points(argv[1], p1, p2)) {
+        std::fprintf(stderr, "cannot read %s\n", argv[1]);
+        return 2;
+    }
+    const int64_t npool = (int64_t)p1.size() / 2;
+    std::printf("%lld correspondences from %s (%s)\n", (long long)npool, argv[1], hg_version());
+
+    std::mt19937 rng(11);  // the harness draws 4 random indices per hypothesis (.cu:52-78)
+    std::uniform_int_distribution<int64_t> pick(0, npool - 1);
+    int failures = 0;
+    for (int64_t n = 1; n <= max_n; n *= 10) {
+        std::vector<double> hs(8 * n), ht(8 * n);
+        for (int64_t i = 0; i < n; ++i)
+            for (int k = 0; k < 4; ++k) {
+                const int64_t j = pick(rng);
+                hs[(2 * k) * n + i] = p1[2 * j];
+                hs[(2 * k + 1) * n + i] = p1[2 * j + 1];
+                ht[(2 * k) * n + i] = p2[2 * j];
+                ht[(2 * k + 1) * n + i] = p2[2 * j + 1];
+            }
+        double *ds, *dt, *dh, *dg;
+        CHECK(hipMalloc(&ds, 8 * n * sizeof(double)));
+        CHECK(hipMalloc(&dt, 8 * n * sizeof(double)));
+        CHECK(hipMalloc(&dh, 9 * n * sizeof(double)));
+        CHECK(hipMalloc(&dg, 9 * n * sizeof(double)));
+        CHECK(hipMemcpy(ds, hs.data(), 8 * n * sizeof(double), hipMemcpyHostToDevice));
+        CHECK(hipMemcpy(dt, ht.data(), 8 * n * sizeof(double), hipMemcpyHostToDevice));
+        const struct { const char* name; SolveF64 fn; double* out; } cases[] = {
+            {"cal_Homo_ACA", hg_aca_f64, dh}, {"cal_Homo_SKS", hg_sks_f64, dg},
+            {"cal_Homo_GPT", hg_gpt_f64, dg}, {"cal_Homo_GE ", hg_ge_f64, dg}};
+        for (const auto& c : cases) {
+            const double us = time_launches(c.fn, ds, dt, c.out, n, budget_ms);
+            std::printf("%s N=%-8lld %10.3f us per launch  %8.2f G H/s\n", c.name, (long long)n,
+                        us, n / us * 1e-3);
+        }
+        // ACA (unnormalised) against GE (H[8] = 1) after normalising: same homography
+        std::vector<double> ha(9 * n), hg(9 * n);
+        CHECK(hipMemcpy(ha.data(), dh, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
+        CHECK(hipMemcpy(hg.data(), dg, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
+        int64_t agree = 0, finite = 0;
+        for (int64_t i = 0; i < n; ++i) {
+            const double w = ha[8 * n + i];
+            bool ok = std::isfinite(w) && w != 0.0, fin = ok;
+            double num = 0.0, den = 0.0;
+            for (int k = 0; k < 9 && ok; ++k) {
+                const double a = ha[k * n + i] / w, g = hg[k * n + i];
+                if (!std::isfinite(a) || !std::isfinite(g)) { ok = false; fin = false; break; }
+                num += (a - g) * (a - g);
+                den += g * g;
+            }
+            finite += fin;
+            agree += ok && num <= 1e-12 * den;
+        }
+        std::printf("  ACA vs GE: %lld of %lld finite solutions agree to 1e-6 relative\n",
+                    (long long)agree, (long long)finite);
+        if (finite > 0 && agree < finite * 99 / 100) ++failures;
+        CHECK(hipFree(ds)); CHECK(hipFree(dt)); CHECK(hipFree(dh)); CHECK(hipFree(dg));
+        std::printf("----------------------------------------------------------\n");
+    }
+    return failures ? 1 : 0;
+}

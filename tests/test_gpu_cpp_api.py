@@ -22,3 +22,30 @@ def test_cpp_dropin_program(pkg, dev, tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "dropin ok" in r.stdout
+
+
+def test_cpp_runtime_harness(pkg, dev, tmp_path):
+    """examples/runtime_test.cpp -- the reference GPU harness's flow in native C++ over the
+    C ABI: reads the reference's point-file format (written here from the committed
+    orig_pts_wall.txt fixture), draws random 4-subsets, times ACA/SKS/GPT/GE per N and
+    checks ACA against GE."""
+    import numpy as np
+    from conftest import load_golden
+    g = load_golden("cpp_wall.npz")
+    pts = tmp_path / "pts.txt"
+    with open(pts, "w") as f:
+        f.write(f"{g['pool_src'].shape[0]}\n")
+        for a, b in zip(g["pool_src"], g["pool_tar"]):
+            f.write(" ".join(np.format_float_positional(v, unique=True)
+                             for v in (a[0], a[1], b[0], b[1])) + "\n")
+    libdir = os.path.dirname(pkg._lib.LIB_PATH)
+    exe = tmp_path / "runtime_test"
+    subprocess.run(["g++", "-std=c++17", "-O2", f"-I{ROOT}/include", "-I/opt/rocm/include",
+                    "-D__HIP_PLATFORM_AMD__", f"{ROOT}/examples/runtime_test.cpp",
+                    f"-L{libdir}", "-lsks_homography_amd", f"-Wl,-rpath,{libdir}",
+                    "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-o", str(exe)],
+                   check=True)
+    r = subprocess.run([str(exe), str(pts), "100000", "0.05"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "cal_Homo_ACA N=100000" in r.stdout and "cal_Homo_GE  N=100000" in r.stdout
