@@ -194,6 +194,14 @@ def main():
              ge=ref.solve("ge", ws, wt))
     manifest.append("cpp_wall.npz: 1024 4-subsets of orig_pts_wall.txt (reference data file), "
                     "pool + indices kept for the fused sampler; reference C++ outputs")
+    with open(os.path.join(OUT, "orig_pts_wall_restated.txt"), "w") as f:
+        f.write(f"{ps.shape[0]}\n")
+        for a, b in zip(ps, pt):
+            f.write(" ".join(np.format_float_positional(v, unique=True)
+                             for v in (a[0], a[1], b[0], b[1])) + "\n")
+    manifest.append("orig_pts_wall_restated.txt: the pool of cpp_wall.npz written back in the "
+                    "reference's point-file format (count line, then x1 y1 x2 y2; shortest "
+                    "round-trip decimals) -- input for examples/runtime_test.cpp")
 
     # 3. edge cases, f32 and f64
     es, et = edge_problems()
