@@ -196,6 +196,8 @@ def test_read_points_matches_reference_format(pkg, tmp_path):
     rs, rt = pkg.read_points(str(path))
     assert rs.dtype == np.float32 and rs.shape == ps.shape
     assert np.array_equal(rs, ps) and np.array_equal(rt, pt)
+    fs, ft = pkg.read_points(os.path.join(ROOT, "tests", "golden", "orig_pts_wall_restated.txt"))
+    assert np.array_equal(fs, ps) and np.array_equal(ft, pt)
     bad = tmp_path / "short.txt"
     bad.write_text("3\n1 2 3 4\n")
     with pytest.raises(ValueError):
