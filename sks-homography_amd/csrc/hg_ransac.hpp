@@ -102,8 +102,8 @@ inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
 // the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
 // and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
 // staging to fit the block's LDS (checked on the host).
-template <int ALGO, bool NORM, int P>
-__global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
+template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock>
+__global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
     constexpr int kTile = kWave * P;
@@ -113,15 +113,15 @@ __global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
     char* stage = dyn + (size_t)npool * 16 + (size_t)wave * kStage;
-    for (uint32_t i = threadIdx.x; i < npool; i += kBlock) {
+    for (uint32_t i = threadIdx.x; i < npool; i += WPB * kWave) {
         const float2 a = pool_src[i], b = pool_tar[i];
         pool[i] = make_float4(a.x, a.y, b.x, b.y);
     }
     __syncthreads();
 
     const int64_t tiles = (n + kTile - 1) / kTile;
-    const int64_t stride = (int64_t)gridDim.x * kWavesPerBlock;
-    int64_t t = (int64_t)blockIdx.x * kWavesPerBlock + wave;
+    const int64_t stride = (int64_t)gridDim.x * WPB;
+    int64_t t = (int64_t)blockIdx.x * WPB + wave;
     auto load = [&](int64_t tile, u32x4 (&r)[P]) {
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -129,11 +129,14 @@ __global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
             r[j] = p < n ? ld16<true>(reinterpret_cast<const char*>(idx + p)) : u32x4{0, 0, 0, 0};
         }
     };
-    u32x4 cur[P];
+    // index rows of the next PF tiles stay in flight while this tile is solved
+    static_assert(PF == 1 || PF == 2, "prefetch depth 1 or 2");
+    u32x4 cur[P], ahead[P]{};
     if (t < tiles) load(t, cur);
+    if (PF == 2 && t + stride < tiles) load(t + stride, ahead);
     for (; t < tiles; t += stride) {
         u32x4 nxt[P]{};
-        if (t + stride < tiles) load(t + stride, nxt);
+        if (t + PF * stride < tiles) load(t + PF * stride, nxt);
         float h[P][9];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -164,16 +167,59 @@ __global__ __launch_bounds__(kBlock) void sample_solve_lds_kernel(
             }
         }
 #pragma unroll
-        for (int j = 0; j < P; ++j) cur[j] = nxt[j];
+        for (int j = 0; j < P; ++j) {
+            if constexpr (PF == 2) {
+                cur[j] = ahead[j];
+                ahead[j] = nxt[j];
+            } else {
+                cur[j] = nxt[j];
+            }
+        }
     }
 }
 
-// LDS bytes of sample_solve_lds_kernel<P> for a pool of npool points.
-template <int P>
+// LDS bytes of sample_solve_lds_kernel<P, *, WPB> for a pool of npool points.
+template <int P, int WPB = kWavesPerBlock>
 constexpr size_t sample_lds_bytes(uint32_t npool) {
-    return (size_t)npool * 16 + (size_t)kWavesPerBlock * kWave * P * 36;
+    return (size_t)npool * 16 + (size_t)WPB * kWave * P * 36;
 }
-constexpr size_t kSampleLdsMax = 64 * 1024;  // per-block dynamic LDS without opt-in
+constexpr size_t kSampleLdsMax = 64 * 1024;      // per-block dynamic LDS without opt-in
+constexpr size_t kSampleLdsOptIn = 160 * 1024;   // gfx950: a workgroup may take the whole LDS
+
+// Allows a kernel more than 64 KiB of dynamic LDS (once per instantiation).
+template <typename K>
+inline bool lds_opt_in(K kernel) {
+    static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
+                                               hipFuncAttributeMaxDynamicSharedMemorySize,
+                                               (int)kSampleLdsOptIn) == hipSuccess;
+    return ok;
+}
+
+// Variant sweep helper: the LDS-pool sampler with WPB waves per block (tools/kbench_sample.py).
+template <int P, int WPB>
+inline int launch_sample_wide(const float2* ps, const float2* pt, uint32_t npool,
+                              const uint4* ix, float* H, int64_t n, int algo, bool norm,
+                              hipStream_t s, int cus) {
+    const size_t lds = sample_lds_bytes<P, WPB>(npool);
+    if (lds > kSampleLdsOptIn) return (int)hipErrorInvalidValue;
+    const int64_t tiles = (n + (int64_t)kWave * P - 1) / ((int64_t)kWave * P);
+    const int64_t want = (tiles + WPB - 1) / WPB;
+    int64_t per_cu = (int64_t)kSampleLdsOptIn / (int64_t)lds;
+    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+    const int64_t cap = per_cu * cus;
+    const unsigned g = (unsigned)(want < cap ? want : cap);
+    const uint64_t magic = ~0ull / npool + 1;
+#define HG_SW(A, N)                                                                            \
+    do {                                                                                       \
+        auto k = sample_solve_lds_kernel<A, N, P, 1, WPB>;                                     \
+        if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;           \
+        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n);                         \
+    } while (0)
+    if (algo == 0) { if (norm) HG_SW(kACA, true); else HG_SW(kACA, false); }
+    else { if (norm) HG_SW(kSKS, true); else HG_SW(kSKS, false); }
+#undef HG_SW
+    return (int)hipGetLastError();
+}
 
 // Inlier test of one (hypothesis, correspondence) pair, division-free:
 //   (x', y', w') = H (x, y, 1),  inlier <=> w' != 0 and
@@ -324,11 +370,13 @@ inline int cu_count() {
 }
 
 // variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
-// P = 1 / 2 (falls back to 0 when the pool does not fit).
+// P = 1 / 2; 3 = LDS-pool P = 2 with the index rows two tiles ahead (falls back to 0
+// when the pool does not fit).
 inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
                         const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
     constexpr int kShippedP = 2;
-    int use_p = variant == -1 ? kShippedP : variant;
+    const bool pf2 = variant == 3;
+    int use_p = variant == -1 ? kShippedP : (pf2 ? 2 : variant);
     const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
     if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
     if (use_p == 0) {
@@ -355,9 +403,15 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
     if (use_p == 1) {
         if (algo == 0) { if (norm) HG_SL(1, kACA, true); else HG_SL(1, kACA, false); }
         else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
-    } else {
+    } else if (!pf2) {
         if (algo == 0) { if (norm) HG_SL(2, kACA, true); else HG_SL(2, kACA, false); }
         else { if (norm) HG_SL(2, kSKS, true); else HG_SL(2, kSKS, false); }
+    } else {
+#define HG_SL2(A, N) \
+    sample_solve_lds_kernel<A, N, 2, 2><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
+        if (algo == 0) { if (norm) HG_SL2(kACA, true); else HG_SL2(kACA, false); }
+        else { if (norm) HG_SL2(kSKS, true); else HG_SL2(kSKS, false); }
+#undef HG_SL2
     }
 #undef HG_SL
     return (int)hipGetLastError();

@@ -369,12 +369,23 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
 // same argument checks as hg_sample_solve_f32.
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
-    if (n <= 0 || npool == 0 || variant < 0 || variant > 2 || (algo != 0 && algo != 1))
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 6 || (algo != 0 && algo != 1))
         return (int)hipErrorInvalidValue;
     if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
         (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
         (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
         return (int)hipErrorInvalidValue;
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const auto* ix = reinterpret_cast<const uint4*>(idx);
+    const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (variant) {  // wider blocks: more waves share one LDS copy of the pool
+        case 4: return hg::launch_sample_wide<1, 8>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
+        case 5: return hg::launch_sample_wide<1, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
+        case 6: return hg::launch_sample_wide<2, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
+        default: break;
+    }
     return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
                                    reinterpret_cast<const float2*>(pool_tar), npool,
                                    reinterpret_cast<const uint4*>(idx), H, n, algo,

@@ -16,7 +16,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
-NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2"}
+NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2", 3: "LDS pool P2 prefetch 2",
+         4: "LDS pool P1, 8 waves/block", 5: "LDS pool P1, 16 waves/block",
+         6: "LDS pool P2, 16 waves/block"}
 
 
 def main():
