@@ -666,6 +666,8 @@ def main():
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(min(n, 10_000_000))
+        # the speed-up is quoted against the multi-threaded host baseline
+        line["cpu_baseline"]["gpu_speedup"] = round(line["value"] / line["cpu_baseline"]["value"], 1)
     if d.rank == 0:
         print(json.dumps(line), flush=True)
     d.close()
