@@ -3,9 +3,11 @@
 //
 // The four single-problem functions keep the reference's exact signatures and
 // output semantics (normalised H, H[8] == 1, bit-identical values).  The pointers
-// may be host memory (staged through a per-thread device scratch, like the
-// reference's one-call-per-homography use in CPU_Runtime Test/main.cpp:87-114) or
-// device memory (solved in place).  The call is synchronous, as the reference's is.
+// may be host memory -- the reference's one-call-per-homography use in
+// CPU_Runtime Test/main.cpp:87-114: the 16 values ride in the kernel launch
+// (hg_solve_one_*) and H comes back through per-thread mapped host memory on a
+// per-thread stream -- or device memory (solved in place, on the legacy default
+// stream).  The call is synchronous, as the reference's is, and thread-safe.
 // Returns 0 on success (the reference always returns 0, ACA_SKS.cpp:101), or the
 // hipError_t of a failed copy/launch.
 //

@@ -1,7 +1,9 @@
 /*
- * sks_homography_tune.h -- kernel-variant launcher used by tools/kbench.py to pick
- * the shipped AoS memory schedule.  Not part of the drop-in boundary
- * (include/sks_homography.h); every variant produces the same bits.
+ * sks_homography_tune.h -- kernel-variant launchers and timing loops for tools/ and
+ * bench.py (lib/libsks_homography_tune.so): the sweeps that picked each shipped
+ * kernel's memory schedule, the HBM ceiling streams, and cal_ACA's launch loop
+ * (GPU_Runtime Test.cu:1166-1206) in native code.  Not part of the drop-in boundary
+ * (include/sks_homography.h); every solver variant produces the shipped kernel's bits.
  */
 #ifndef SKS_HOMOGRAPHY_TUNE_H
 #define SKS_HOMOGRAPHY_TUNE_H
