@@ -142,3 +142,32 @@ def test_fit_offsets_example(pkg, dev):
     mod = importlib.util.module_from_spec(spec)
     spec.loader.exec_module(mod)
     assert mod.fit(batch=2048, steps=300) < 0.5
+
+
+def test_rect_and_offsets_edge_values_vs_oracle(orc, oracle, pkg, dev):
+    """Degenerate and extreme TensorACA inputs (coincident corners, zero-area targets,
+    +-Inf, NaN, 1e30, subnormals) propagate exactly as the restatement of the reference
+    statements does (no guards), forward and backward."""
+    rng = np.random.default_rng(3)
+    B = 4096 + 13
+    corner = np.floor(rng.uniform(10, 30, (B, 2))).astype(np.float32)
+    offs = rng.uniform(-16, 16, (B, 4, 2)).astype(np.float32)
+    specials = np.array([0.0, -0.0, np.inf, -np.inf, np.nan, 1e30, -1e30, 1e-40, -128.0],
+                        np.float32)
+    for i in range(0, B, 7):  # sprinkle special values into offsets and corners
+        offs[i, rng.integers(0, 4), rng.integers(0, 2)] = specials[i % len(specials)]
+        if i % 5 == 0:
+            corner[i, rng.integers(0, 2)] = specials[(i // 5) % len(specials)]
+    offs[1] = -np.array([[0, 0], [128, 0], [0, 128], [128, 128]], np.float32)  # all corners -> M
+    dc, do = torch.from_numpy(corner).to(dev), torch.from_numpy(offs).to(dev)
+    for w, h in ((128.0, 128.0), (64.0, 48.0)):
+        src, tar = _build_h(corner, offs, w, h)
+        div = float(np.float32(w) / np.float32(h))
+        want = oracle.tensor_aca_rect(src, tar, w, div)
+        assert orc.same_bits(pkg.tensor_aca_offsets(dc, do, w, h).cpu().numpy(), want).all()
+        Hr = pkg.tensor_aca_rect(torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev), w, div)
+        assert orc.same_bits(Hr.cpu().numpy(), want).all()
+        gH = torch.from_numpy(rng.standard_normal((B, 3, 3)).astype(np.float32)).to(dev)
+        g_off, _ = pkg.tensor_aca_offsets_backward(dc, do, gH, w, h, True)
+        _, wt, _ = oracle.tensor_aca_rect_backward(src, tar, gH.cpu().numpy(), w, div)
+        assert orc.same_bits(g_off.cpu().numpy(), np.stack([wt[:, 0, :], wt[:, 1, :]], 2)).all()
