@@ -91,3 +91,26 @@ def test_sample_solve_variants_vs_oracle(orc, oracle, pkg, dev, npool, variant):
             s, t = oracle.sample_problems(ps, pt, idx.cpu().numpy().view(np.uint32))
             ok = orc.same_bits(H.cpu().numpy(), oracle.solve("aca" if algo == 0 else "sks", s, t))
             assert ok.all(), f"variant {variant} npool {npool} n {n}: {(~ok).sum()} differ"
+
+
+def test_score_special_values_vs_oracle(oracle, pkg, dev):
+    """Hypotheses and pool points with NaN / +-Inf / 0 / huge entries: the division-free
+    inlier test gives the restatement's counts exactly (w' = 0 never counts)."""
+    rng = np.random.default_rng(8)
+    npool, n = 777, 5003
+    ps = rng.uniform(0, 1000, (npool, 2)).astype(np.float32)
+    pt = rng.uniform(0, 1000, (npool, 2)).astype(np.float32)
+    H = rng.standard_normal((n, 9)).astype(np.float32)
+    H[:, 8] = 1.0
+    specials = np.array([np.nan, np.inf, -np.inf, 0.0, -0.0, 1e30, 1e-40], np.float32)
+    H[::11, 6:9] = 0.0                                   # w' == 0 for every point
+    for i in range(0, n, 5):
+        H[i, rng.integers(0, 9)] = specials[i % len(specials)]
+    for i in range(0, npool, 9):
+        ps[i, rng.integers(0, 2)] = specials[i % len(specials)]
+    H[7] = [1, 0, 0, 0, 1, 0, 0, 0, 1]                   # identity: inliers where src == tar
+    pt[::3] = ps[::3]
+    for thresh in (0.0, 2.0):
+        got = pkg.ransac_score(torch.from_numpy(H).to(dev), torch.from_numpy(ps).to(dev),
+                               torch.from_numpy(pt).to(dev), thresh).cpu().numpy().view(np.uint32)
+        np.testing.assert_array_equal(got, oracle.ransac_score(H, ps, pt, thresh))
