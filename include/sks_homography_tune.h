@@ -47,6 +47,11 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream);
 
+/* binary64 AoS sweep: 0 P1 nt LDS-DMA (shipped), 1 P2 nt LDS-DMA, 2 P1 nt register-staged,
+ * 3 P1 LDS-DMA default policy. */
+int hg_tune_aos_f64(int algo, int variant, const double* src, const double* tar, double* H,
+                    int64_t n, void* stream);
+
 int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream);

@@ -266,6 +266,29 @@ int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, f
                                      reinterpret_cast<hipStream_t>(stream));
 }
 
+// binary64 AoS sweep (tools/kbench_f64.py): 0 = P1 nt LDS-DMA (shipped), 1 = P2 nt LDS-DMA,
+// 2 = P1 nt register-staged loads, 3 = P1 LDS-DMA default cache policy.
+int hg_tune_aos_f64(int algo, int variant, const double* src, const double* tar, double* H,
+                    int64_t n, void* stream) {
+    if (n <= 0 || (algo != 0 && algo != 1)) return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+#define HG_F64(P, FL)                                                                          \
+    do {                                                                                       \
+        const unsigned g = (unsigned)aos_grid<double, P, FL>(n);                               \
+        if (algo == 0) solve_aos<kACA, true, double, P, FL><<<g, kBlock, 0, st>>>(src, tar, H, n); \
+        else solve_aos<kSKS, true, double, P, FL><<<g, kBlock, 0, st>>>(src, tar, H, n);       \
+    } while (0)
+    switch (variant) {
+        case 0: HG_F64(1, kNtLoad | kNtStore | kLdsLoad | kLdsDma); break;
+        case 1: HG_F64(2, kNtLoad | kNtStore | kLdsLoad | kLdsDma); break;
+        case 2: HG_F64(1, kNtLoad | kNtStore | kLdsLoad); break;
+        case 3: HG_F64(1, kLdsLoad | kLdsDma); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HG_F64
+    return (int)hipGetLastError();
+}
+
 // TensorACA tile sweep (tools/kbench_rect.py).  Variants 0-2: rect form (host scalars
 // scale = a, div = b), P = 1 / 2 / 4 problems per lane; 3-5: compact form (src = corner,
 // tar = offsets, a = width, b = height), P = 1 / 2 / 4.  16-B aligned inputs only.

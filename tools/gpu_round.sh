@@ -63,6 +63,7 @@ for step in $STEPS; do
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
         kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;
         hbm_ceilings) run hbm_ceilings 300 python tools/hbm_ceilings.py ;;
+        kbench_f64) run kbench_f64 300 python tools/kbench_f64.py ;;
         dist2)
             # rehearse the N>1 control path (barriers, max-over-ranks, one JSON line) with
             # 2 ranks sharing the one GPU over gloo; the real N>1 run uses RCCL
