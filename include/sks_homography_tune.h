@@ -47,6 +47,11 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream);
 
+/* Row-stream probe: RI input / RO output rows of row_bytes at pitch_bytes; variant 0 (16,9),
+ * 1 (16,8), 2 (8,4), 3 (4,2), 4 (2,1), 5 (16,9) with 4 chunks per lane, 6 (32,16). */
+int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
+                    int64_t pitch_bytes, void* stream);
+
 /* binary64 AoS sweep: 0 P1 nt LDS-DMA (shipped), 1 P2 nt LDS-DMA, 2 P1 nt register-staged,
  * 3 P1 LDS-DMA default policy. */
 int hg_tune_aos_f64(int algo, int variant, const double* src, const double* tar, double* H,

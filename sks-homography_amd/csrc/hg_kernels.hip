@@ -161,9 +161,17 @@ constexpr int kAosFlags = kNtLoad | kNtStore | kLdsLoad | kLdsDma;
 constexpr int kAosCachedFlags = kLdsLoad | kLdsDma;
 constexpr int64_t kMallResidentBytes = 200000000;
 constexpr int kRectP = 1;  // TensorACA problems per lane (tools/kbench_rect.py, profiles/r01/kbench_rect.json)
-constexpr int kSoaG = 1;  // 16-B groups per lane (SoA path)
+// SoA: the narrow form (one problem per lane, element-wide row accesses; hg_soa.hpp
+// solve_soa_narrow) everywhere -- 3-5 % ahead of the 16-B register and LDS-DMA forms at
+// 10 M, 10-20 % ahead at N <= 10 K -- except MALL-resident binary64 batches of
+// kSoaWideMinN problems and up, where the 16-B register form (kSoaG groups per lane)
+// leads (tools/kbench_soa.py, tools/kbench_soa_small.py; profiles/r01/kbench_soa*.json).
+constexpr int kSoaG = 1;
+constexpr int64_t kSoaWideMinN = 32768;
 
 inline bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+template <int A>
+inline bool aligned_to(const void* p) { return (reinterpret_cast<uintptr_t>(p) & (A - 1)) == 0; }
 
 inline int64_t ceil_div(int64_t a, int64_t b) { return (a + b - 1) / b; }
 
@@ -180,18 +188,22 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
     const bool cached = n <= kMallResidentBytes / (25 * (int64_t)sizeof(T));  // 25 values/problem
     if (layout == HG_LAYOUT_SOA) {
         constexpr int V = 16 / sizeof(T);
-        if (n % V == 0 && aligned16(src) && aligned16(tar) && aligned16(H)) {
+        if (sizeof(T) == 8 && cached && n >= kSoaWideMinN && n % V == 0 && aligned16(src) &&
+            aligned16(tar) && aligned16(H)) {
+            // binary64, MALL-resident, mid-size: the 16-B register form (8 % ahead at 100 K)
             const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
-            if (sizeof(T) == 8 && !cached) {
-                // f64 beyond the MALL: the LDS-DMA tile form, 0-4 % ahead of the register
-                // form box to box (tools/kbench_soa.py, profiles/r01/kbench_soa_dma.json)
-                const int64_t tile = (int64_t)kWave * V * kWavesPerBlock;
-                solve_soa_dma<ALGO, NORM, T, true>
-                    <<<(unsigned)((n + tile - 1) / tile), kBlock, 0, s>>>(src, tar, H, n);
-            } else if (cached)
-                solve_soa_vec<ALGO, NORM, T, kSoaG, false, false><<<g, kBlock, 0, s>>>(src, tar, H, n);
+            solve_soa_vec<ALGO, NORM, T, kSoaG, false, false><<<g, kBlock, 0, s>>>(src, tar, H, n);
+        } else if (aligned_to<sizeof(T)>(src) && aligned_to<sizeof(T)>(tar) &&
+                   aligned_to<sizeof(T)>(H)) {
+            // one problem per lane, one element-wide access per component row
+            const int64_t blocks = ceil_div(n, kBlock);
+            if (blocks > 0x7fffffffLL) return kErrInvalid;
+            if (cached)
+                solve_soa_narrow<ALGO, NORM, T, sizeof(T), false>
+                    <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
             else
-                solve_soa_vec<ALGO, NORM, T, kSoaG, false, true><<<g, kBlock, 0, s>>>(src, tar, H, n);
+                solve_soa_narrow<ALGO, NORM, T, sizeof(T), true>
+                    <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
         } else
             solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
     } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {

@@ -128,6 +128,71 @@ __global__ __launch_bounds__(kBlock) void solve_soa_dma(const T* __restrict__ sr
     }
 }
 
+// Narrow-access form: a lane owns V = W/sizeof(T) consecutive problems and moves each
+// component row with ONE W-byte access (W = 4 / 8), so a wave-instruction touches 64*W
+// contiguous bytes of a row.  Fewer live VGPRs than the 16-B form (inputs 16*V dwords'
+// worth), hence more waves in flight per SIMD.  n % V == 0 and W-aligned bases.
+template <int W, bool NT>
+__device__ __forceinline__ void ldw(const void* p, void* dst) {
+    if constexpr (W == 4) {
+        const unsigned v = NT ? __builtin_nontemporal_load(reinterpret_cast<const unsigned*>(p))
+                              : *reinterpret_cast<const unsigned*>(p);
+        __builtin_memcpy(dst, &v, 4);
+    } else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        const u32x2 v = NT ? __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(p))
+                           : *reinterpret_cast<const u32x2*>(p);
+        __builtin_memcpy(dst, &v, 8);
+    }
+}
+
+template <int W, bool NT>
+__device__ __forceinline__ void stw(void* p, const void* src) {
+    if constexpr (W == 4) {
+        unsigned v;
+        __builtin_memcpy(&v, src, 4);
+        if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<unsigned*>(p));
+        else *reinterpret_cast<unsigned*>(p) = v;
+    } else {
+        typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+        u32x2 v;
+        __builtin_memcpy(&v, src, 8);
+        if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<u32x2*>(p));
+        else *reinterpret_cast<u32x2*>(p) = v;
+    }
+}
+
+template <int ALGO, bool NORM, typename T, int W, bool NT = true>
+__global__ __launch_bounds__(kBlock) void solve_soa_narrow(const T* __restrict__ src,
+                                                           const T* __restrict__ tar,
+                                                           T* __restrict__ H, int64_t n) {
+    constexpr int V = W / sizeof(T);
+    static_assert(V >= 1 && V * sizeof(T) == W, "W must be a multiple of sizeof(T)");
+    const int64_t q = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (q >= n / V) return;
+    T s[8][V], t[8][V];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        ldw<W, NT>(src + (int64_t)k * n + q * V, s[k]);
+        ldw<W, NT>(tar + (int64_t)k * n + q * V, t[k]);
+    }
+    T h[V][9];
+#pragma unroll
+    for (int v = 0; v < V; ++v) {
+        T sv[8], tv[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) { sv[k] = s[k][v]; tv[k] = t[k][v]; }
+        solve<ALGO, NORM>(sv, tv, h[v]);
+    }
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        T o[V];
+#pragma unroll
+        for (int v = 0; v < V; ++v) o[v] = h[v][k];
+        stw<W, NT>(H + (int64_t)k * n + q * V, o);
+    }
+}
+
 template <int G, bool PERSIST>
 inline int64_t soa_grid(int64_t groups, int per_cu = 8) {
     const int64_t chunks = (groups + (int64_t)kBlock * G - 1) / ((int64_t)kBlock * G);

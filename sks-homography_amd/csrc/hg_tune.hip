@@ -138,6 +138,20 @@ int launch_soa_dma(int algo, const void* s, const void* t, void* H, int64_t n, i
     return (int)hipGetLastError();
 }
 
+template <typename T, int W, bool NT = true>
+int launch_soa_narrow(int algo, const void* s, const void* t, void* H, int64_t n, int,
+                      hipStream_t st) {
+    constexpr int V = W / sizeof(T);
+    if (n % V) return (int)hipErrorInvalidValue;
+    const unsigned g = (unsigned)((n / V + kBlock - 1) / kBlock);
+    const T* a = (const T*)s;
+    const T* b = (const T*)t;
+    T* h = (T*)H;
+    if (algo == 0) solve_soa_narrow<kACA, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else solve_soa_narrow<kSKS, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    return (int)hipGetLastError();
+}
+
 struct SoaVariant {
     const char* name;
     int (*launch)(int, const void*, const void*, void*, int64_t, int, hipStream_t);
@@ -155,6 +169,11 @@ const SoaVariant kSoaVariants[] = {
     {"f32 G1 one-shot plain (cached) ld/st", launch_soa<float, 1, false, false>},
     {"f64 LDS-DMA tile nt", launch_soa_dma<double>},
     {"f32 LDS-DMA tile nt", launch_soa_dma<float>},
+    {"f32 narrow W4 (1 problem per lane)", launch_soa_narrow<float, 4>},
+    {"f32 narrow W8 (2 problems per lane)", launch_soa_narrow<float, 8>},
+    {"f64 narrow W8 (1 problem per lane)", launch_soa_narrow<double, 8>},
+    {"f64 narrow W8 plain (cached) ld/st", launch_soa_narrow<double, 8, false>},
+    {"f32 narrow W4 plain (cached) ld/st", launch_soa_narrow<float, 4, false>},
 };
 
 // The HBM ceilings either side of a copy: read-only (every 16-B load folded into a
@@ -183,6 +202,27 @@ __global__ __launch_bounds__(kBlock) void write_only(u32x4* __restrict__ dst, in
     for (int u = 0; u < U; ++u) {
         const int64_t i = base + (int64_t)u * kBlock;
         if (i < n16) st16<true>(dst + i, v);
+    }
+}
+
+// Row-stream probe (tools/soa_streams.py): RI input rows and RO output rows of row16
+// 16-B chunks each, at a row pitch of pitch16 chunks; a lane reads chunk q of every input
+// row (U chunks per lane, kBlock apart) and writes their XOR to chunk q of every output
+// row -- the SoA solver's access pattern with the arithmetic taken out.
+template <int RI, int RO, int U>
+__global__ __launch_bounds__(kBlock) void row_streams(const u32x4* __restrict__ in,
+                                                      u32x4* __restrict__ out, int64_t row16,
+                                                      int64_t pitch16) {
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t q = base + (int64_t)u * kBlock;
+        if (q >= row16) break;
+        u32x4 acc = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int k = 0; k < RI; ++k) acc ^= ld16<true>(in + k * pitch16 + q);
+#pragma unroll
+        for (int k = 0; k < RO; ++k) st16<true>(out + k * pitch16 + q, acc + (uint32_t)k);
     }
 }
 
@@ -264,6 +304,33 @@ int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, f
         return (int)hipErrorInvalidValue;
     return kVariants[variant].launch(algo, src, tar, H, n, per_cu > 0 ? per_cu : 8,
                                      reinterpret_cast<hipStream_t>(stream));
+}
+
+// Row-stream probe: variant -> (RI, RO, U); see row_streams.  in / out hold RI / RO rows
+// of row_bytes at a pitch of pitch_bytes (both multiples of 16).
+int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
+                    int64_t pitch_bytes, void* stream) {
+    if (row_bytes <= 0 || (row_bytes & 15) || (pitch_bytes & 15) || pitch_bytes < row_bytes)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t r16 = row_bytes / 16, p16 = pitch_bytes / 16;
+    const auto* s = reinterpret_cast<const u32x4*>(in);
+    auto* d = reinterpret_cast<u32x4*>(out);
+#define HG_RS(RI, RO, U)                                                                          \
+    row_streams<RI, RO, U><<<(unsigned)((r16 + kBlock * U - 1) / (kBlock * U)), kBlock, 0, st>>>( \
+        s, d, r16, p16)
+    switch (variant) {
+        case 0: HG_RS(16, 9, 1); break;   // SoA f32/f64 solver pattern
+        case 1: HG_RS(16, 8, 1); break;
+        case 2: HG_RS(8, 4, 1); break;
+        case 3: HG_RS(4, 2, 1); break;
+        case 4: HG_RS(2, 1, 1); break;
+        case 5: HG_RS(16, 9, 4); break;   // 4 KiB per wave per row
+        case 6: HG_RS(32, 16, 1); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+#undef HG_RS
+    return (int)hipGetLastError();
 }
 
 // binary64 AoS sweep (tools/kbench_f64.py): 0 = P1 nt LDS-DMA (shipped), 1 = P2 nt LDS-DMA,

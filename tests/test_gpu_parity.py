@@ -592,8 +592,8 @@ def test_concurrent_streams(orc, oracle, pkg, dev):
 
 @pytest.mark.parametrize("algo", ["aca", "sks"])
 def test_soa_f64_beyond_mall_vs_oracle(orc, oracle, pkg, dev, algo):
-    """f64 SoA batches past the cache-policy threshold take the LDS-DMA tile kernel; a
-    ragged size (not a multiple of the 512-problem block tile) checks its tail path."""
+    """f64 SoA batches past the cache-policy threshold take the non-temporal narrow kernel;
+    a ragged size checks the partial last block."""
     n = 1_234_566
     rng = np.random.default_rng(n)
     s = rng.uniform(0, 1024, (8, n))
@@ -602,3 +602,24 @@ def test_soa_f64_beyond_mall_vs_oracle(orc, oracle, pkg, dev, algo):
         H = pkg.solve(algo, _t(s, dev), _t(t, dev), normalize=norm, layout="soa")
         _bits(orc, H, oracle.solve(algo, s, t, normalize=norm, layout="soa"),
               f"{algo} f64 SoA n={n} norm={norm}")
+
+
+@pytest.mark.parametrize("dtype,n", [
+    (torch.float32, 1), (torch.float32, 7), (torch.float32, 4096), (torch.float32, 100_001),
+    (torch.float32, 2_000_003),
+    (torch.float64, 1), (torch.float64, 33), (torch.float64, 32_768), (torch.float64, 100_000),
+    (torch.float64, 1_000_001), (torch.float64, 1_000_004)])
+def test_soa_dispatch_regimes_vs_oracle(orc, oracle, pkg, dev, dtype, n):
+    """Every SoA kernel the dispatcher picks (hg_kernels.hip launch_solver): narrow with the
+    default policy (MALL-resident), narrow non-temporal (beyond it), the 16-B register form
+    for MALL-resident binary64 batches from kSoaWideMinN up -- on both sides of each
+    threshold, ragged and even sizes."""
+    npdt = np.float32 if dtype == torch.float32 else np.float64
+    rng = np.random.default_rng(n)
+    s = rng.uniform(0, 1024, (8, n)).astype(npdt)
+    t = rng.uniform(0, 1024, (8, n)).astype(npdt)
+    for algo in ("aca", "sks"):
+        for norm in (False, True):
+            H = pkg.solve(algo, _t(s, dev), _t(t, dev), normalize=norm, layout="soa")
+            _bits(orc, H, oracle.solve(algo, s, t, normalize=norm, layout="soa"),
+                  f"{algo} {dtype} SoA n={n} norm={norm}")
