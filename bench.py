@@ -401,6 +401,17 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     for _ in range(3):
         f_big()
     _, ms_big = timed_region(d, f_big, 10)
+    # the two-launch form a caller of the reference pipeline runs (draws, then gather+solve)
+    # against the seeded fused sampler (draws made in the kernel: 36 B per hypothesis)
+    f_two = lambda: pkg.sample_solve(ps, pt, pkg.fill_bits(big * 4, SEED, 0, d.dev).view(big, 4))  # noqa: E731
+    f_seed = lambda: pkg.sample_solve_seeded(ps, pt, big, SEED, 0)  # noqa: E731
+    for _ in range(3):
+        f_two()
+        f_seed()
+    _, ms_two = timed_region(d, f_two, 10)
+    _, ms_seed = timed_region(d, f_seed, 10)
+    seeded_same = bool(torch.equal(pkg.sample_solve_seeded(ps, pt, hyps, SEED, 0).view(torch.int32),
+                                   H.view(torch.int32)))
     del idx_b
     return {
         "hypotheses": hyps, "pool": int(ps.shape[0]), "thresh_px": thresh,
@@ -411,6 +422,14 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
                                "G_hyp_per_s": round(big / (ms_big * 1e-3) / 1e9, 2),
                                "achieved_gbps": round(big * 52 / (ms_big * 1e-3) / 1e9, 1),
                                "frac": round(big * 52 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
+        "sample_solve_seeded_large": {
+            "hypotheses": big, "us": round(ms_seed * 1e3, 2),
+            "G_hyp_per_s": round(big / (ms_seed * 1e-3) / 1e9, 2),
+            "achieved_gbps": round(big * 36 / (ms_seed * 1e-3) / 1e9, 1),
+            "frac": round(big * 36 / (ms_seed * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "draws_then_indexed_us": round(ms_two * 1e3, 2),
+            "speedup_vs_two_launch": round(ms_two / ms_seed, 2),
+            "bit_identical_to_indexed": seeded_same},
         "score_ms": round(ms_score, 3),
         "score_G_pairs_per_s": round(pairs / (ms_score * 1e-3) / 1e9, 1),
         "best_inliers": int(counts.max().item()),

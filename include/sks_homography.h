@@ -142,6 +142,15 @@ int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t n
                         const uint32_t* idx, float* H, int64_t n, int algo, int flags,
                         void* stream);
 
+/* The fused sampler with the draws made in the kernel: equals
+ * hg_fill_bits_u32(idx, 4*n, seed, offset) followed by hg_sample_solve_f32(..., idx, ...),
+ * bit for bit, without the (n,4) index array (cuRAND + get_rand_list + cal_Homo_ACA/SKS,
+ * GPU_Runtime Test.cu:1443-1451, :52-78, :81-240, as one launch).  H: (n,9), 16-B
+ * aligned; pools 8-B aligned. */
+int hg_sample_solve_seeded_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
+                               uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
+                               int flags, void* stream);
+
 /* Inlier count per hypothesis: counts[h] = #{i : w' != 0 and
  * (x' - u w')^2 + (y' - v w')^2 <= thresh^2 w'^2}, (x',y',w') = H_h (x_i, y_i, 1),
  * (u_i, v_i) = pool_tar[i] -- the squared reprojection error against thresh, without

@@ -19,7 +19,7 @@ from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib
 from .ops import (aca, fill_uniform, sks, solve, stream_copy, tensor_aca_rect,
                   tensor_aca_rect_autograd, tensor_aca_rect_backward,
                   tensor_aca_offsets, tensor_aca_offsets_backward)
-from .ransac import RansacResult, fill_bits, ransac, read_points, sample_solve
+from .ransac import RansacResult, fill_bits, ransac, read_points, sample_solve, sample_solve_seeded
 from .ransac import score as ransac_score
 from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
 from .shard import gather_blocks, scatter_blocks, shard_range
@@ -30,7 +30,7 @@ RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H (SURV
 __all__ = [
     "aca", "sks", "solve", "tensor_aca_rect", "tensor_aca_rect_autograd",
     "tensor_aca_rect_backward", "tensor_aca_offsets", "tensor_aca_offsets_backward",
-    "fill_uniform", "sample_solve", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
+    "fill_uniform", "sample_solve", "sample_solve_seeded", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
     "read_points",
     "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
     "gather_blocks", "scatter_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",

@@ -43,6 +43,8 @@ SIGNATURES = {
                              ctypes.c_float, _vp], _int),
     "hg_fill_bits_u32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _int),
     "hg_sample_solve_f32": ([_vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _int, _vp], _int),
+    "hg_sample_solve_seeded_f32": ([_vp, _vp, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint64,
+                                    _vp, _i64, _int, _int, _vp], _int),
     "hg_ransac_score_f32": ([_vp, _i64, _vp, _vp, ctypes.c_uint32, ctypes.c_float, _vp, _vp],
                             _int),
     "hg_solve_one_f32": ([_int, _vp, _vp, _vp, _int, _vp], _int),

@@ -4,6 +4,7 @@
 //
 //   hg_fill_bits_u32      counter-based 32-bit draws (4 per hypothesis)
 //   hg_sample_solve_f32   idx (n,4) -> gather 4 correspondences from the pool -> H (n,9)
+//   hg_sample_solve_seeded_f32   the same with the draws made in the kernel (no idx)
 //   hg_ransac_score_f32   H (n,9) x pool (npool) -> inlier count per hypothesis
 //
 // The scorer is the one compute-bound kernel here: every (hypothesis, point) pair
@@ -40,6 +41,23 @@ int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t n
                                    reinterpret_cast<const uint4*>(idx), H, n, algo,
                                    (flags & HG_FLAG_NORMALIZE) != 0,
                                    reinterpret_cast<hipStream_t>(stream));
+}
+
+int hg_sample_solve_seeded_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
+                               uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
+                               int flags, void* stream) {
+    if (n < 0 || npool == 0 || (algo != 0 && algo != 1) || (flags & ~HG_FLAG_NORMALIZE))
+        return (int)hipErrorInvalidValue;
+    if (n == 0) return 0;
+    if (!pool_src || !pool_tar || !H) return (int)hipErrorInvalidValue;
+    if ((reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
+        (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
+        return (int)hipErrorInvalidValue;
+    return hg::launch_sample_seeded(reinterpret_cast<const float2*>(pool_src),
+                                    reinterpret_cast<const float2*>(pool_tar), npool,
+                                    seed * hg::kBitsMul + offset, H, n, algo,
+                                    (flags & HG_FLAG_NORMALIZE) != 0,
+                                    reinterpret_cast<hipStream_t>(stream));
 }
 
 int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,

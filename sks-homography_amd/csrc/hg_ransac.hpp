@@ -26,15 +26,30 @@ static __global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __re
         out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
 }
 
+// The 4 draws of hypothesis p: row p of the (n,4) index array, or -- SEEDED -- the same
+// four words generated in place, out[4p .. 4p+3] of fill_bits_kernel with
+// base = seed * kBitsMul + offset (so a seeded launch equals fill_bits + an indexed one,
+// bit for bit, without the 16 B per hypothesis of index traffic).
+template <bool SEEDED>
+__device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, int64_t p) {
+    if constexpr (SEEDED) {
+        const uint64_t b = bits_base + 4 * (uint64_t)p;
+        return u32x4{(uint32_t)(mix64(b) >> 32), (uint32_t)(mix64(b + 1) >> 32),
+                     (uint32_t)(mix64(b + 2) >> 32), (uint32_t)(mix64(b + 3) >> 32)};
+    } else {
+        return ld16<true>(reinterpret_cast<const char*>(idx + p));
+    }
+}
+
 // Fused sampler + solver.  A wave owns 64*P hypotheses: its 16-B index rows arrive by
 // LDS-DMA (P = 2: 2 KiB), each lane gathers its 4 correspondences from the pool
 // (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
 // LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
 // does (.cu:56-59, modulo bias and duplicates included).
-template <int ALGO, bool NORM, int P>
+template <int ALGO, bool NORM, int P, bool SEEDED = false>
 __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
+    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n, uint64_t bits_base = 0) {
     constexpr int kTile = kWave * P;
     constexpr int kIdx = kTile * 16;
     constexpr int kLds = kIdx > kTile * 36 ? kIdx : kTile * 36;
@@ -46,7 +61,13 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     char* lds = smem[wave];
     const bool full = base + kTile <= n;
     uint4 r[P];
-    if (full) {
+    if constexpr (SEEDED) {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const u32x4 d = draws4<true>(nullptr, bits_base, base + j * kWave + lane);
+            r[j] = make_uint4(d[0], d[1], d[2], d[3]);
+        }
+    } else if (full) {
         dma_slab_issue<kIdx, true>(reinterpret_cast<const char*>(idx + base), lds, lane);
         dma_wait_sync();
 #pragma unroll
@@ -102,10 +123,11 @@ inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
 // the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
 // and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
 // staging to fit the block's LDS (checked on the host).
-template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock>
+template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock, bool SEEDED = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n) {
+    uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
+    uint64_t bits_base = 0) {
     constexpr int kTile = kWave * P;
     constexpr int kStage = kTile * 36;
     extern __shared__ __attribute__((aligned(16))) char dyn[];
@@ -126,7 +148,7 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int64_t p = tile * kTile + j * kWave + lane;
-            r[j] = p < n ? ld16<true>(reinterpret_cast<const char*>(idx + p)) : u32x4{0, 0, 0, 0};
+            r[j] = p < n ? draws4<SEEDED>(idx, bits_base, p) : u32x4{0, 0, 0, 0};
         }
     };
     // index rows of the next PF tiles stay in flight while this tile is solved
@@ -213,7 +235,7 @@ inline int launch_sample_wide(const float2* ps, const float2* pt, uint32_t npool
     do {                                                                                       \
         auto k = sample_solve_lds_kernel<A, N, P, 1, WPB>;                                     \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;           \
-        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n);                         \
+        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n, 0);                      \
     } while (0)
     if (algo == 0) { if (norm) HG_SW(kACA, true); else HG_SW(kACA, false); }
     else { if (norm) HG_SW(kSKS, true); else HG_SW(kSKS, false); }
@@ -414,6 +436,41 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 #undef HG_SL2
     }
 #undef HG_SL
+    return (int)hipGetLastError();
+}
+
+// The seeded sampler's launcher: the shipped tiles of launch_sample_solve (LDS pool, P = 2,
+// while the pool fits 64 KiB of LDS; else the global-gather form) with the draws made in
+// the kernel from bits_base = seed * kBitsMul + offset.
+inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
+                                uint64_t bits_base, float* H, int64_t n, int algo, bool norm,
+                                hipStream_t s) {
+    constexpr int P = 2;
+    const size_t lds = sample_lds_bytes<P>(npool);
+    if (lds > kSampleLdsMax) {
+        const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
+        if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+        const unsigned g = (unsigned)blocks;
+#define HG_SG(A, N) \
+    sample_solve_kernel<A, N, P, true><<<g, kBlock, 0, s>>>(ps, pt, npool, nullptr, H, n, bits_base)
+        if (algo == 0) { if (norm) HG_SG(kACA, true); else HG_SG(kACA, false); }
+        else { if (norm) HG_SG(kSKS, true); else HG_SG(kSKS, false); }
+#undef HG_SG
+        return (int)hipGetLastError();
+    }
+    const int64_t tiles = (n + (int64_t)kWave * P - 1) / ((int64_t)kWave * P);
+    const int64_t want = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
+    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
+    per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
+    const int64_t cap = per_cu * cu_count();
+    const unsigned g = (unsigned)(want < cap ? want : cap);
+    const uint64_t magic = fastmod_magic(npool);
+#define HG_SD(A, N)                                                                          \
+    sample_solve_lds_kernel<A, N, P, 1, kWavesPerBlock, true><<<g, kBlock, lds, s>>>(         \
+        ps, pt, npool, magic, nullptr, H, n, bits_base)
+    if (algo == 0) { if (norm) HG_SD(kACA, true); else HG_SD(kACA, false); }
+    else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }
+#undef HG_SD
     return (int)hipGetLastError();
 }
 

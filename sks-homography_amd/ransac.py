@@ -73,6 +73,25 @@ def sample_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, idx: torch.Tens
     return out
 
 
+def sample_solve_seeded(pool_src: torch.Tensor, pool_tar: torch.Tensor, n: int, seed: int,
+                        offset: int = 0, algo: str = "aca", normalize: bool = True) -> torch.Tensor:
+    """``n`` hypotheses drawn AND solved in one launch: bit for bit
+    ``sample_solve(pool_src, pool_tar, fill_bits(4 * n, seed, offset).view(n, 4))``, with the
+    draws made in the kernel instead of read from an index array.  (n,9)."""
+    dev = _require_device(pool_src, pool_tar)
+    if algo not in ("aca", "sks"):
+        raise ValueError(f"algo must be 'aca' or 'sks', got {algo!r}")
+    if n < 0:
+        raise ValueError(f"n must be >= 0, got {n}")
+    ps, pt = _pool(pool_src), _pool(pool_tar)
+    out = torch.empty((n, 9), dtype=torch.float32, device=dev)
+    with _guard(dev):
+        _lib.call("hg_sample_solve_seeded_f32", ps.data_ptr(), pt.data_ptr(), ps.shape[0],
+                  seed, offset, out.data_ptr(), n, 0 if algo == "aca" else 1,
+                  1 if normalize else 0, _stream(dev))
+    return out
+
+
 def score(H: torch.Tensor, pool_src: torch.Tensor, pool_tar: torch.Tensor,
           thresh: float) -> torch.Tensor:
     """Inlier count of every hypothesis H (n,9) over the pool: points whose
@@ -97,11 +116,10 @@ class RansacResult(NamedTuple):
 
 def ransac(pool_src: torch.Tensor, pool_tar: torch.Tensor, hypotheses: int, thresh: float,
            seed: int = 11, algo: str = "aca") -> RansacResult:
-    """Draws ``hypotheses`` random 4-point samples, solves them all, scores them all
-    and returns the best (ties: lowest index)."""
-    dev = _require_device(pool_src, pool_tar)
-    idx = fill_bits(hypotheses * 4, seed, 0, dev).view(hypotheses, 4)
-    H = sample_solve(pool_src, pool_tar, idx, algo=algo, normalize=True)
+    """Draws ``hypotheses`` random 4-point samples and solves them (one fused launch),
+    scores them all and returns the best (ties: lowest index)."""
+    _require_device(pool_src, pool_tar)
+    H = sample_solve_seeded(pool_src, pool_tar, hypotheses, seed, 0, algo=algo, normalize=True)
     counts = score(H, pool_src, pool_tar, thresh)
     best = int((counts == counts.max()).nonzero()[0].item())
     return RansacResult(H[best].clone(), int(counts[best].item()), best, counts)

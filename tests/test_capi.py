@@ -96,6 +96,13 @@ def test_other_entry_validation(pkg):
     assert lib.hg_sample_solve_f32(None, None, 5, None, None, 4, 9, 0, None) == 1  # algo
     assert lib.hg_sample_solve_f32(None, None, 5, 8, 16, 4, 0, 0, None) == 1      # unaligned idx
     assert lib.hg_fill_bits_u32(None, -1, 0, 0, None) == 1
+    assert lib.hg_sample_solve_seeded_f32(None, None, 0, 1, 0, None, 4, 0, 0, None) == 1  # npool 0
+    assert lib.hg_sample_solve_seeded_f32(None, None, 5, 1, 0, None, 4, 2, 0, None) == 1  # algo
+    assert lib.hg_sample_solve_seeded_f32(None, None, 5, 1, 0, None, 4, 0, 4, None) == 1  # flags
+    assert lib.hg_sample_solve_seeded_f32(None, None, 5, 1, 0, None, -1, 0, 0, None) == 1  # n < 0
+    assert lib.hg_sample_solve_seeded_f32(None, None, 5, 1, 0, None, 0, 0, 0, None) == 0  # empty
+    assert lib.hg_sample_solve_seeded_f32(None, None, 5, 1, 0, None, 4, 0, 0, None) == 1  # NULL
+    assert lib.hg_sample_solve_seeded_f32(8, 8, 5, 1, 0, 8, 4, 0, 0, None) == 1  # H unaligned
     assert lib.hg_fill_bits_u32(None, 0, 0, 0, None) == 0
     assert lib.hg_ransac_score_f32(None, -1, None, None, 0, 1.0, None, None) == 1
     assert lib.hg_ransac_score_f32(None, 0, None, None, 0, 1.0, None, None) == 0

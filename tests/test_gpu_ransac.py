@@ -114,3 +114,34 @@ def test_score_special_values_vs_oracle(oracle, pkg, dev):
         got = pkg.ransac_score(torch.from_numpy(H).to(dev), torch.from_numpy(ps).to(dev),
                                torch.from_numpy(pt).to(dev), thresh).cpu().numpy().view(np.uint32)
         np.testing.assert_array_equal(got, oracle.ransac_score(H, ps, pt, thresh))
+
+
+@pytest.mark.parametrize("npool", [1, 3, 2540, 20_000])
+def test_sample_solve_seeded_vs_oracle(orc, oracle, pkg, dev, npool):
+    """The seeded fused sampler (draws made in the kernel) equals fill_bits + the indexed
+    sampler bit for bit, and both equal the oracle: LDS-pool and global-gather forms
+    (npool 20 000 exceeds the LDS pool), ragged batches, offsets past 2^32, both solvers,
+    normalised or not."""
+    g = np.random.default_rng(npool + 1)
+    ps = (g.random((npool, 2)) * 1000).astype(np.float32)
+    pt = (g.random((npool, 2)) * 1000).astype(np.float32)
+    dps, dpt = torch.from_numpy(ps).to(dev), torch.from_numpy(pt).to(dev)
+    for n, seed, off in ((1, 3, 0), (129, 11, 977), (70_001, 12345, (1 << 33) + 5)):
+        bits = pkg.fill_bits(n * 4, seed, off, dev).view(n, 4)
+        s, t = oracle.sample_problems(ps, pt, oracle.fill_bits(n * 4, seed, off).reshape(n, 4))
+        for algo in ("aca", "sks"):
+            for norm in (True, False):
+                H = pkg.sample_solve_seeded(dps, dpt, n, seed, off, algo=algo, normalize=norm)
+                ref = pkg.sample_solve(dps, dpt, bits, algo=algo, normalize=norm)
+                assert torch.equal(H.view(torch.int32), ref.view(torch.int32)), (n, algo, norm)
+                ok = orc.same_bits(H.cpu().numpy(), oracle.solve(algo, s, t, normalize=norm))
+                assert ok.all(), f"npool {npool} n {n} {algo} norm={norm}: {(~ok).sum()} differ"
+
+
+def test_sample_solve_seeded_zero_and_errors(pkg, dev):
+    ps = torch.rand(10, 2, device=dev)
+    assert pkg.sample_solve_seeded(ps, ps, 0, 1).shape == (0, 9)
+    with pytest.raises(ValueError):
+        pkg.sample_solve_seeded(ps, ps, 5, 1, algo="ge")
+    with pytest.raises(ValueError):
+        pkg.sample_solve_seeded(ps, ps, -1, 1)
