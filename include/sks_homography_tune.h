@@ -38,7 +38,8 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
 int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
                  float b, void* stream);
 
-/* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2). */
+/* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2), 3 P = 2 with
+ * two-tile prefetch, 4-6 wider blocks, 7 P = 2 with the 64-bit remainder. */
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
 
@@ -51,6 +52,11 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
  * 1 (16,8), 2 (8,4), 3 (4,2), 4 (2,1), 5 (16,9) with 4 chunks per lane, 6 (32,16). */
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
                     int64_t pitch_bytes, void* stream);
+
+/* Seeded fused sampler: 0 shipped (32-bit round-up remainder), 1 64-bit remainder. */
+int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
+                          uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
+                          int algo, int flags, void* stream);
 
 /* binary64 AoS sweep: 0 P1 nt LDS-DMA (shipped), 1 P2 nt LDS-DMA, 2 P1 nt register-staged,
  * 3 P1 LDS-DMA default policy. */

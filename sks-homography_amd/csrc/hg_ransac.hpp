@@ -107,14 +107,44 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     }
 }
 
-// r mod d for every 32-bit r and d >= 1 by one 64-bit multiply and a high multiply
-// (Lemire, Kaser & Kurz, "Faster remainder by direct computation", 2019), with
-// M = floor((2^64 - 1) / d) + 1 computed once on the host.  Equals r % d exactly.
-__device__ __forceinline__ uint32_t fastmod_u32(uint32_t r, uint64_t M, uint32_t d) {
+// r mod d for every 32-bit r and d >= 1 with one high and one low 32-bit multiply:
+// division by an invariant integer in the round-up form with a 33-bit multiplier
+// (Granlund & Montgomery, PLDI 1994; Robison, ARITH 2005): for d = 2^l + x (0 < x < 2^l),
+// M = floor(2^(33+l) / d) + 1 exceeds 2^32, so with m = M - 2^32 and hi = umulhi(r, m),
+// floor(r M / 2^(33+l)) = (((r - hi) >> 1) + hi) >> l exactly for every r < 2^32
+// (M d - 2^(33+l) <= d < 2^(l+1)).  Powers of two use m = 0 and shift l - 1; d = 1
+// and d = 2 share m = 0, shift 0, and the min() clamps d = 1's remainder to 0 (a no-op
+// for every other d).  Host side packs (shift << 32) | m.
+__device__ __forceinline__ uint32_t fastmod_u32(uint32_t r, uint64_t packed, uint32_t d) {
+    const uint32_t m = (uint32_t)packed, sh = (uint32_t)(packed >> 32);
+    const uint32_t hi = __umulhi(r, m);
+    const uint32_t q = (((r - hi) >> 1) + hi) >> sh;
+    const uint32_t rem = r - q * d;
+    return rem < d - 1 ? rem : d - 1;
+}
+
+inline uint64_t fastmod_magic(uint32_t d) {
+    if (d <= 2) return 0;
+    const uint32_t l = 31u - (uint32_t)__builtin_clz(d);
+    if ((d & (d - 1)) == 0) return (uint64_t)(l - 1) << 32;
+    const unsigned __int128 M = (((unsigned __int128)1) << (33 + l)) / d + 1;
+    return ((uint64_t)l << 32) | (uint64_t)(uint32_t)(M - ((unsigned __int128)1 << 32));
+}
+
+// The alternative measured against it (tools/kbench_sample.py): Lemire, Kaser & Kurz,
+// "Faster remainder by direct computation" (2019) -- M = floor((2^64 - 1) / d) + 1,
+// r mod d = umulhi64(M r mod 2^64, d): five multiplies, a shorter dependency chain.
+__device__ __forceinline__ uint32_t fastmod64_u32(uint32_t r, uint64_t M, uint32_t d) {
     return (uint32_t)__umul64hi(M * (uint64_t)r, (uint64_t)d);
 }
 
-inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
+inline uint64_t fastmod64_magic(uint32_t d) { return ~0ull / d + 1; }
+
+template <bool MOD64>
+__device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uint32_t d) {
+    if constexpr (MOD64) return fastmod64_u32(r, magic, d);
+    else return fastmod_u32(r, magic, d);
+}
 
 // The same sampler with the pool staged in LDS once per block: {x, y, u, v} 16-B
 // records, so a hypothesis gathers with 4 ds_read_b128 instead of 8 scattered global
@@ -123,7 +153,8 @@ inline uint64_t fastmod_magic(uint32_t d) { return ~0ull / d + 1; }
 // the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
 // and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
 // staging to fit the block's LDS (checked on the host).
-template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock, bool SEEDED = false>
+template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock, bool SEEDED = false,
+          bool MOD64 = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -162,10 +193,10 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
         float h[P][9];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const uint32_t id[4] = {fastmod_u32(cur[j].x, magic, npool),
-                                    fastmod_u32(cur[j].y, magic, npool),
-                                    fastmod_u32(cur[j].z, magic, npool),
-                                    fastmod_u32(cur[j].w, magic, npool)};
+            const uint32_t id[4] = {reduce_index<MOD64>(cur[j].x, magic, npool),
+                                    reduce_index<MOD64>(cur[j].y, magic, npool),
+                                    reduce_index<MOD64>(cur[j].z, magic, npool),
+                                    reduce_index<MOD64>(cur[j].w, magic, npool)};
             float s[8], tt[8];
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
@@ -230,7 +261,7 @@ inline int launch_sample_wide(const float2* ps, const float2* pt, uint32_t npool
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cus;
     const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = ~0ull / npool + 1;
+    const uint64_t magic = fastmod_magic(npool);
 #define HG_SW(A, N)                                                                            \
     do {                                                                                       \
         auto k = sample_solve_lds_kernel<A, N, P, 1, WPB>;                                     \
@@ -392,13 +423,15 @@ inline int cu_count() {
 }
 
 // variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
-// P = 1 / 2; 3 = LDS-pool P = 2 with the index rows two tiles ahead (falls back to 0
-// when the pool does not fit).
+// P = 1 / 2; 3 = LDS-pool P = 2 with the index rows two tiles ahead; 4 = LDS-pool P = 2
+// with the 64-bit remainder (fastmod64_u32).  The LDS forms fall back to 0 when the pool
+// does not fit.
 inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
                         const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
     constexpr int kShippedP = 2;
     const bool pf2 = variant == 3;
-    int use_p = variant == -1 ? kShippedP : (pf2 ? 2 : variant);
+    const bool mod64 = variant == 4;
+    int use_p = variant == -1 ? kShippedP : (pf2 || mod64 ? 2 : variant);
     const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
     if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
     if (use_p == 0) {
@@ -419,12 +452,19 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = fastmod_magic(npool);
+    const uint64_t magic = mod64 ? fastmod64_magic(npool) : fastmod_magic(npool);
 #define HG_SL(PP, A, N) \
     sample_solve_lds_kernel<A, N, PP><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
     if (use_p == 1) {
         if (algo == 0) { if (norm) HG_SL(1, kACA, true); else HG_SL(1, kACA, false); }
         else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
+    } else if (mod64) {
+#define HG_SL64(A, N)                                                                        \
+    sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, false, true><<<g, kBlock, lds, s>>>( \
+        ps, pt, npool, magic, ix, H, n, 0)
+        if (algo == 0) { if (norm) HG_SL64(kACA, true); else HG_SL64(kACA, false); }
+        else { if (norm) HG_SL64(kSKS, true); else HG_SL64(kSKS, false); }
+#undef HG_SL64
     } else if (!pf2) {
         if (algo == 0) { if (norm) HG_SL(2, kACA, true); else HG_SL(2, kACA, false); }
         else { if (norm) HG_SL(2, kSKS, true); else HG_SL(2, kSKS, false); }
@@ -442,6 +482,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // The seeded sampler's launcher: the shipped tiles of launch_sample_solve (LDS pool, P = 2,
 // while the pool fits 64 KiB of LDS; else the global-gather form) with the draws made in
 // the kernel from bits_base = seed * kBitsMul + offset.
+template <bool MOD64 = false>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t bits_base, float* H, int64_t n, int algo, bool norm,
                                 hipStream_t s) {
@@ -464,9 +505,9 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = fastmod_magic(npool);
+    const uint64_t magic = MOD64 ? fastmod64_magic(npool) : fastmod_magic(npool);
 #define HG_SD(A, N)                                                                          \
-    sample_solve_lds_kernel<A, N, P, 1, kWavesPerBlock, true><<<g, kBlock, lds, s>>>(         \
+    sample_solve_lds_kernel<A, N, P, 1, kWavesPerBlock, true, MOD64><<<g, kBlock, lds, s>>>(  \
         ps, pt, npool, magic, nullptr, H, n, bits_base)
     if (algo == 0) { if (norm) HG_SD(kACA, true); else HG_SD(kACA, false); }
     else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }

@@ -459,7 +459,7 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
 // same argument checks as hg_sample_solve_f32.
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
-    if (n <= 0 || npool == 0 || variant < 0 || variant > 6 || (algo != 0 && algo != 1))
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 7 || (algo != 0 && algo != 1))
         return (int)hipErrorInvalidValue;
     if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
         (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
@@ -474,6 +474,7 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
         case 4: return hg::launch_sample_wide<1, 8>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
         case 5: return hg::launch_sample_wide<1, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
         case 6: return hg::launch_sample_wide<2, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
+        case 7: return hg::launch_sample_solve(4, ps, pt, npool, ix, H, n, algo, norm, st);
         default: break;
     }
     return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
@@ -481,6 +482,25 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
                                    reinterpret_cast<const uint4*>(idx), H, n, algo,
                                    (flags & HG_FLAG_NORMALIZE) != 0,
                                    reinterpret_cast<hipStream_t>(stream));
+}
+
+// Seeded sampler variants (tools/kbench_sample.py): 0 = shipped (32-bit round-up
+// remainder), 1 = the 64-bit remainder.
+int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
+                          uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
+                          int algo, int flags, void* stream) {
+    if (n <= 0 || npool == 0 || !pool_src || !pool_tar || !H || (algo != 0 && algo != 1))
+        return (int)hipErrorInvalidValue;
+    const auto* ps = reinterpret_cast<const float2*>(pool_src);
+    const auto* pt = reinterpret_cast<const float2*>(pool_tar);
+    const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
+    const uint64_t base = seed * hg::kBitsMul + offset;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    switch (variant) {
+        case 0: return hg::launch_sample_seeded<false>(ps, pt, npool, base, H, n, algo, norm, st);
+        case 1: return hg::launch_sample_seeded<true>(ps, pt, npool, base, H, n, algo, norm, st);
+        default: return (int)hipErrorInvalidValue;
+    }
 }
 
 // Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),

@@ -1,0 +1,47 @@
+"""The sampler's index reduction r mod npool (hg_ransac.hpp fastmod_u32 / fastmod_magic:
+one umulhi + one mullo, round-up division by an invariant integer) restated with Python
+integers at 32-bit width and checked against % for divisors across the whole uint32
+range -- every d up to 4096, powers of two and their neighbours, random large d -- and
+the numerators where such schemes break (0, d-1, d, multiples of d, 2^32-1, ...).  The
+GPU tests (test_gpu_ransac.py) check the device code itself against the oracle's %."""
+import numpy as np
+
+M32 = (1 << 32) - 1
+
+
+def magic(d):
+    if d <= 2:
+        return 0, 0
+    l = d.bit_length() - 1
+    if d & (d - 1) == 0:
+        return 0, l - 1
+    M = (1 << (33 + l)) // d + 1
+    assert (1 << 32) < M < (1 << 33)
+    return M - (1 << 32), l
+
+
+def fastmod(r, m, sh, d):
+    hi = (r * m) >> 32
+    q = ((((r - hi) & M32) >> 1) + hi) >> sh
+    rem = (r - q * d) & M32
+    return min(rem, d - 1)
+
+
+def _numerators(d, rng):
+    base = {0, 1, 2, d - 1, d, d + 1, 2 * d - 1, 2 * d, M32, M32 - 1, M32 - d, (1 << 31),
+            (1 << 31) - 1, (M32 // d) * d, (M32 // d) * d - 1}
+    base |= set(int(x) for x in rng.integers(0, 1 << 32, 64, dtype=np.uint64))
+    return [r for r in base if 0 <= r <= M32]
+
+
+def test_fastmod_matches_modulo_everywhere():
+    rng = np.random.default_rng(3)
+    ds = set(range(1, 4097))
+    for k in range(1, 32):
+        ds |= {(1 << k) - 1, 1 << k, (1 << k) + 1}
+    ds |= {M32, M32 - 1, 2540, 20_000, 65_537}
+    ds |= set(int(x) for x in rng.integers(1, 1 << 32, 400, dtype=np.uint64))
+    for d in sorted(ds):
+        m, sh = magic(d)
+        for r in _numerators(d, rng):
+            assert fastmod(r, m, sh, d) == r % d, (d, r)

@@ -68,11 +68,11 @@ def _tune_sample(pkg):
     return f
 
 
-@pytest.mark.parametrize("npool", [1, 2, 3, 7, 2540, 3900, 20_000])
+@pytest.mark.parametrize("npool", [1, 2, 3, 4, 7, 8, 1024, 1025, 2540, 3900, 20_000])
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_sample_solve_variants_vs_oracle(orc, oracle, pkg, dev, npool, variant):
     """Every sampler form (global gather; pool staged in LDS, P = 1/2) against the oracle:
-    pools from 1 point (fastmod's magic wraps to 0) to beyond the LDS limit (the LDS
+    pools from 1 point (the remainder clamp) and powers of two to beyond the LDS limit (the LDS
     forms fall back), ragged batches over the persistent grid, indices spanning all of
     uint32 (modulo reduction as get_rand_list, .cu:56-59)."""
     g = np.random.default_rng(npool)

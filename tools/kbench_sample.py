@@ -1,6 +1,7 @@
 """Fused RANSAC sampler + solver (hg_tune_sample variants: 0 global gather, 1 / 2 pool in
-LDS with P = 1 / 2) across batch sizes over the reference's orig_pts_wall.txt pool
-(tests/golden).  Device time per launch from event-bracketed back-to-back launches,
+LDS with P = 1 / 2, 3 prefetch 2, 4-6 wider blocks, 7 the 64-bit remainder) across batch sizes over the reference's orig_pts_wall.txt pool
+(tests/golden), and the seeded form (draws made in the kernel, 36 B of H per hypothesis;
+hg_tune_sample_seeded) with either remainder.  Device time per launch from event-bracketed back-to-back launches,
 interleaved rounds, median; algorithmic GB/s at 16 B of indices + 36 B of H per
 hypothesis (the pool is cache-resident).  Outputs compared bit for bit with variant 0."""
 import ctypes
@@ -18,7 +19,8 @@ import __graft_entry__ as ge  # noqa: E402
 
 NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2", 3: "LDS pool P2 prefetch 2",
          4: "LDS pool P1, 8 waves/block", 5: "LDS pool P1, 16 waves/block",
-         6: "LDS pool P2, 16 waves/block"}
+         6: "LDS pool P2, 16 waves/block", 7: "LDS pool P2, 64-bit remainder"}
+SEEDED = {0: "seeded P2 (shipped)", 1: "seeded P2, 64-bit remainder"}
 
 
 def main():
@@ -27,6 +29,11 @@ def main():
     f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_void_p,
                   ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     f.restype = ctypes.c_int
+    fs = pkg._lib.tune().hg_tune_sample_seeded
+    fs.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                   ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                   ctypes.c_void_p]
+    fs.restype = ctypes.c_int
     dev = torch.device("cuda:0")
     g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
     ps = torch.from_numpy(g["pool_src"]).to(dev)
@@ -35,23 +42,28 @@ def main():
     out = {}
     for n in (1 << 20, 1 << 22, 1 << 24):
         idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
-        outs = {v: torch.empty((n, 9), device=dev) for v in NAMES}
+        keys = list(NAMES) + [("s", v) for v in SEEDED]
+        outs = {v: torch.empty((n, 9), device=dev) for v in keys}
         st = torch.cuda.current_stream(dev).cuda_stream
 
         def run(v):
-            assert f(v, ps.data_ptr(), pt.data_ptr(), npool, idx.data_ptr(), outs[v].data_ptr(), n,
-                     0, 1, st) == 0
+            if isinstance(v, tuple):
+                assert fs(v[1], ps.data_ptr(), pt.data_ptr(), npool, 11, 0, outs[v].data_ptr(), n,
+                          0, 1, st) == 0
+            else:
+                assert f(v, ps.data_ptr(), pt.data_ptr(), npool, idx.data_ptr(), outs[v].data_ptr(),
+                         n, 0, 1, st) == 0
 
-        for v in NAMES:
+        for v in keys:
             for _ in range(3):
                 run(v)
         torch.cuda.synchronize()
         exact = {v: bool(torch.equal(outs[v].view(torch.int32), outs[0].view(torch.int32)))
-                 for v in NAMES}
-        times = {v: [] for v in NAMES}
+                 for v in keys}
+        times = {v: [] for v in keys}
         reps = 20
         for _ in range(7):
-            for v in NAMES:
+            for v in keys:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(reps):
@@ -60,10 +72,12 @@ def main():
                 torch.cuda.synchronize()
                 times[v].append(e0.elapsed_time(e1) / reps * 1e3)
         res = {}
-        for v, name in NAMES.items():
+        for v in keys:
+            name = SEEDED[v[1]] if isinstance(v, tuple) else NAMES[v]
             us = statistics.median(times[v])
+            nb = 36 if isinstance(v, tuple) else 52
             res[name] = {"us": round(us, 2), "G_hyp_per_s": round(n / us / 1e3, 2),
-                         "algorithmic_gbps": round(n * 52 / us / 1e3, 1), "bit_exact": exact[v]}
+                         "algorithmic_gbps": round(n * nb / us / 1e3, 1), "bit_exact": exact[v]}
             print(n, name, res[name], flush=True)
         out[str(n)] = res
         del idx, outs
