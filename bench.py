@@ -19,6 +19,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 import numpy as np
@@ -43,6 +44,8 @@ def parse():
     ap.add_argument("--no-extras", action="store_true", help="ACA headline only")
     ap.add_argument("--no-gather", action="store_true",
                     help="N>1: skip the timed split (scatter) / gather through rank 0")
+    ap.add_argument("--gather-deadline", type=float, default=180.0,
+                    help="N>1: seconds the split / gather may take before the job ends without it")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
@@ -680,8 +683,24 @@ def main():
 
     if d.world > 1 and not args.no_gather:
         run("aca")()
+        # The split / gather is reported beside the measurement, never part of it: should its
+        # point-to-point traffic stall, every rank's watchdog ends the job after the deadline
+        # and rank 0 still prints the measured line (with the stall recorded).
+        done = threading.Event()
+
+        def watchdog(limit=args.gather_deadline):
+            if done.wait(limit):
+                return
+            if d.rank == 0:
+                line["split_gather"] = {"error": f"no completion within {limit} s"}
+                print(json.dumps(line), flush=True)
+            sys.stderr.flush()
+            os._exit(0)
+
+        threading.Thread(target=watchdog, daemon=True).start()
         line["split_gather"] = split_gather_section(d, pkg, src, tar, H, n, n_total,
                                                     wall / args.steps * 1e3)
+        done.set()
 
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         line["cpu_baseline"] = cpu_baseline(min(n, 10_000_000))

@@ -76,6 +76,12 @@ for step in $STEPS; do
             run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
                 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 4 --steps 10 \
                 --warmup 2 --no-extras --dist-backend gloo ;;
+        dist2_deadline)
+            # the split / gather watchdog: a deadline too short to meet ends every rank and
+            # rank 0 still prints the measured line, with the stall recorded
+            run dist2_deadline 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 2 --steps 20 \
+                --warmup 2 --no-extras --dist-backend gloo --gather-deadline 0.001 ;;
         torchrun1)
             run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 50 \
