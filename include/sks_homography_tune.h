@@ -48,6 +48,10 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream);
 
+/* Cache-policy probe over `bytes` (< 2 GiB): 0-5 buffer stores with aux 0 / sc0 / nt / sc0|nt /
+ * sc1 / sc1|nt, 6-11 buffer loads with the same bits (one sink dword per lane into dst). */
+int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void* stream);
+
 /* Row-stream probe: RI input / RO output rows of row_bytes at pitch_bytes; variant 0 (16,9),
  * 1 (16,8), 2 (8,4), 3 (4,2), 4 (2,1), 5 (16,9) with 4 chunks per lane, 6 (32,16). */
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,

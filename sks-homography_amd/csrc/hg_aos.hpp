@@ -25,6 +25,7 @@ enum : int {
     kPersist = 16,   // persistent grid: blocks loop over tiles
     kLdsDma = 32,    // with kLdsLoad: global_load_lds_dwordx4 (LDS-DMA, no VGPR staging)
     kXcdMap = 64,    // one-shot grid: each XCD's blocks take one contiguous range of tiles
+    kStSc1 = 128,    // staged H stores as buffer stores with sc1 (| nt with kNtStore); tune only
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -173,7 +174,7 @@ __device__ __forceinline__ void store_rows_staged(char* __restrict__ out, const 
     wave_lds_sync();
 }
 
-template <typename T, int P, bool NT>
+template <typename T, int P, bool NT, bool SC1 = false>
 __device__ __forceinline__ void store_rows9_staged(char* __restrict__ out, const T (&h)[P][9],
                                                    char* lds, int lane) {
     T* st = reinterpret_cast<T*>(lds);
@@ -187,8 +188,15 @@ __device__ __forceinline__ void store_rows9_staged(char* __restrict__ out, const
 #pragma unroll
     for (int c = 0; c < kIters; ++c) {
         const int chunk = c * kWave + lane;
-        if (kChunks % kWave == 0 || chunk < kChunks)
-            st16<NT>(out + 16 * chunk, *reinterpret_cast<const u32x4*>(lds + 16 * chunk));
+        if (kChunks % kWave == 0 || chunk < kChunks) {
+            const u32x4 v = *reinterpret_cast<const u32x4*>(lds + 16 * chunk);
+            if constexpr (SC1) {
+                const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(out, 0, kChunks * 16, 0x00020000);
+                __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, 16 * chunk, 0, NT ? 18 : 16);
+            } else {
+                st16<NT>(out + 16 * chunk, v);
+            }
+        }
     }
     wave_lds_sync();  // the caller may rewrite the staging bytes next
 }
@@ -249,7 +257,8 @@ __device__ __forceinline__ void aos_wave_tile(const T* __restrict__ src, const T
     if constexpr (!(FL & kDirectSt)) {
       if (full) {
         staged = true;
-        store_rows9_staged<T, P, NTS>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        store_rows9_staged<T, P, NTS, (FL & kStSc1) != 0>(reinterpret_cast<char*>(H + base * 9), h,
+                                                          lds, lane);
       }
     }
     if (!staged) {

@@ -72,6 +72,8 @@ const Variant kVariants[] = {
     {"P1 nt lds-dma xcd-contig", launch_variant<1, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
     {"P4 nt lds-dma xcd-contig", launch_variant<4, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kXcdMap>},
     {"P2 lds-dma plain (cached)", launch_variant<2, kLdsLoad | kLdsDma>},
+    {"P2 nt lds-dma, sc1|nt buffer stores", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kStSc1>},
+    {"P2 nt lds-dma, sc1 buffer stores", launch_variant<2, kNtLoad | kLdsLoad | kLdsDma | kStSc1>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.
@@ -226,6 +228,38 @@ __global__ __launch_bounds__(kBlock) void row_streams(const u32x4* __restrict__ 
     }
 }
 
+// Cache-policy probe (tools/hbm_policy.py): 16-B buffer stores / loads with explicit aux
+// bits (gfx950: 1 = sc0, 2 = nt, 16 = sc1) over a 1 GB stream, U chunks per lane.
+template <int AUX, int U>
+__global__ __launch_bounds__(kBlock) void write_policy(char* __restrict__ dst, int64_t n16) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(dst, 0, 0x7fffffff, 0x00020000);
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    const u32x4 v = {1u, 2u, 3u, 4u};
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) __builtin_amdgcn_raw_buffer_store_b128(v, rsrc, (int)(i * 16), 0, AUX);
+    }
+}
+
+template <int AUX, int U>
+__global__ __launch_bounds__(kBlock) void read_policy(const char* __restrict__ src,
+                                                      uint32_t* __restrict__ sink, int64_t n16) {
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(src), 0, 0x7fffffff,
+                                                        0x00020000);
+    const int64_t base = (int64_t)blockIdx.x * kBlock * U + threadIdx.x;
+    uint32_t acc = 0;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const int64_t i = base + (int64_t)u * kBlock;
+        if (i < n16) {
+            const u32x4 v = __builtin_amdgcn_raw_buffer_load_b128(rsrc, (int)(i * 16), 0, AUX);
+            acc ^= v[0] ^ v[1] ^ v[2] ^ v[3];
+        }
+    }
+    sink[(int64_t)blockIdx.x * kBlock + threadIdx.x] = acc;
+}
+
 __global__ void empty_kernel() {}
 __global__ void store_one_kernel(uint32_t* p) {
     if (threadIdx.x == 0) p[0] = 1u;
@@ -304,6 +338,34 @@ int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, f
         return (int)hipErrorInvalidValue;
     return kVariants[variant].launch(algo, src, tar, H, n, per_cu > 0 ? per_cu : 8,
                                      reinterpret_cast<hipStream_t>(stream));
+}
+
+// Cache-policy probe: variant 0-5 = stores with aux 0 / 1 / 2 / 3 / 16 / 18,
+// 6-11 = loads with the same aux values (sink: one dword per lane into dst).  bytes < 2 GiB.
+int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void* stream) {
+    if (bytes <= 0 || (bytes & 15) || bytes >= 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const int64_t n16 = bytes / 16;
+    const unsigned g = (unsigned)((n16 + 4 * kBlock - 1) / (4 * kBlock));
+    char* d = reinterpret_cast<char*>(dst);
+    const char* s = reinterpret_cast<const char*>(src);
+    uint32_t* sink = reinterpret_cast<uint32_t*>(dst);
+    switch (variant) {
+        case 0: write_policy<0, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 1: write_policy<1, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 2: write_policy<2, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 3: write_policy<3, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 4: write_policy<16, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 5: write_policy<18, 4><<<g, kBlock, 0, st>>>(d, n16); break;
+        case 6: read_policy<0, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        case 7: read_policy<1, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        case 8: read_policy<2, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        case 9: read_policy<3, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        case 10: read_policy<16, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        case 11: read_policy<18, 4><<<g, kBlock, 0, st>>>(s, sink, n16); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
 }
 
 // Row-stream probe: variant -> (RI, RO, U); see row_streams.  in / out hold RI / RO rows
