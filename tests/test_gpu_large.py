@@ -1,0 +1,83 @@
+"""Maximum sizes: batches past 2^31 problems (the reference kernels index with `int id` /
+`int offset`, GPU_Runtime Test.cu:82, and stop at 2^31) run through the
+int64 paths and agree with the oracle on slices at the start, across the 2^31 boundary and
+at the end.  MI355X's 288 GB hold a 2^31-problem f32 AoS batch (200 GB) outright; the test
+skips when the device has less free memory."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+N_BIG = (1 << 31) + 4099   # ragged: not a multiple of any tile
+
+
+def _free_bytes(dev):
+    free, _ = torch.cuda.mem_get_info(dev)
+    return free
+
+
+def _slices(n):
+    b = 1 << 31
+    return [(0, 1000), (b - 700, b + 700), (n - 1000, n)]
+
+
+def test_aos_f32_beyond_2_31_vs_oracle(orc, oracle, pkg, dev):
+    need = N_BIG * (32 + 32 + 36) + (2 << 30)
+    if _free_bytes(dev) < need:
+        pytest.skip(f"needs {need / 1e9:.0f} GB of free device memory")
+    src = pkg.fill_uniform(N_BIG * 8, 23, 0, device=dev).view(N_BIG, 8)
+    tar = pkg.fill_uniform(N_BIG * 8, 23, N_BIG * 8, device=dev).view(N_BIG, 8)
+    try:
+        for algo in ("aca", "sks"):
+            H = pkg.solve(algo, src, tar, normalize=True)
+            for a, b in _slices(N_BIG):
+                s = oracle.fill_uniform((b - a) * 8, 23, a * 8).reshape(-1, 8)
+                t = oracle.fill_uniform((b - a) * 8, 23, N_BIG * 8 + a * 8).reshape(-1, 8)
+                ok = orc.same_bits(H[a:b].cpu().numpy(), oracle.solve(algo, s, t))
+                assert ok.all(), f"{algo} rows [{a},{b}): {(~ok).sum()} differ"
+            del H
+    finally:
+        del src, tar
+        torch.cuda.empty_cache()
+
+
+def test_seeded_sampler_beyond_2_31_vs_oracle(orc, oracle, pkg, dev):
+    need = N_BIG * 36 + (2 << 30)
+    if _free_bytes(dev) < need:
+        pytest.skip(f"needs {need / 1e9:.0f} GB of free device memory")
+    rng = np.random.default_rng(31)
+    ps = (rng.random((2540, 2)) * 1000).astype(np.float32)
+    pt = (rng.random((2540, 2)) * 1000).astype(np.float32)
+    dps, dpt = torch.from_numpy(ps).to(dev), torch.from_numpy(pt).to(dev)
+    try:
+        H = pkg.sample_solve_seeded(dps, dpt, N_BIG, 77, 5)
+        for a, b in _slices(N_BIG):
+            bits = oracle.fill_bits((b - a) * 4, 77, 5 + 4 * a).reshape(-1, 4)
+            s, t = oracle.sample_problems(ps, pt, bits)
+            ok = orc.same_bits(H[a:b].cpu().numpy(), oracle.solve("aca", s, t))
+            assert ok.all(), f"rows [{a},{b}): {(~ok).sum()} differ"
+        del H
+    finally:
+        torch.cuda.empty_cache()
+
+
+def test_soa_f32_beyond_2_31_vs_oracle(orc, oracle, pkg, dev):
+    need = N_BIG * (32 + 32 + 36) + (2 << 30)
+    if _free_bytes(dev) < need:
+        pytest.skip(f"needs {need / 1e9:.0f} GB of free device memory")
+    # SoA rows: component k of problem p at k * n + p (the narrow kernel, int64 row offsets)
+    src = pkg.fill_uniform(N_BIG * 8, 29, 0, device=dev).view(8, N_BIG)
+    tar = pkg.fill_uniform(N_BIG * 8, 29, N_BIG * 8, device=dev).view(8, N_BIG)
+    try:
+        H = pkg.solve("aca", src, tar, normalize=False, layout="soa")
+        for a, b in _slices(N_BIG):
+            s = np.stack([oracle.fill_uniform(b - a, 29, k * N_BIG + a) for k in range(8)], 1)
+            t = np.stack([oracle.fill_uniform(b - a, 29, N_BIG * 8 + k * N_BIG + a)
+                          for k in range(8)], 1)
+            ok = orc.same_bits(H[:, a:b].T.cpu().numpy(), oracle.solve("aca", s, t, normalize=False))
+            assert ok.all(), f"SoA rows [{a},{b}): {(~ok).sum()} differ"
+        del H
+    finally:
+        del src, tar
+        torch.cuda.empty_cache()
