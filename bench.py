@@ -401,18 +401,21 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     big = 16 * hyps  # the sampler's HBM-rate figure (16 B idx + 36 B H per hypothesis)
     idx_b = pkg.fill_bits(big * 4, SEED, 0, d.dev).view(big, 4)
     f_big = lambda: pkg.sample_solve(ps, pt, idx_b)  # noqa: E731
-    for _ in range(3):
+    # the box's clocks wander under these VALU-heavy launches for the first ~100 of them
+    # (135 -> 190 -> 131 us per seeded launch in one rocprofv3 trace): warm, then take the
+    # median of 20 ten-launch groups instead of one short mean
+    for _ in range(30):
         f_big()
-    _, ms_big = timed_region(d, f_big, 10)
+    ms_big = launch_stats(d, f_big, groups=20)["median_us"] * 1e-3
     # the two-launch form a caller of the reference pipeline runs (draws, then gather+solve)
     # against the seeded fused sampler (draws made in the kernel: 36 B per hypothesis)
     f_two = lambda: pkg.sample_solve(ps, pt, pkg.fill_bits(big * 4, SEED, 0, d.dev).view(big, 4))  # noqa: E731
     f_seed = lambda: pkg.sample_solve_seeded(ps, pt, big, SEED, 0)  # noqa: E731
-    for _ in range(3):
+    for _ in range(30):
         f_two()
         f_seed()
-    _, ms_two = timed_region(d, f_two, 10)
-    _, ms_seed = timed_region(d, f_seed, 10)
+    ms_two = launch_stats(d, f_two, groups=20)["median_us"] * 1e-3
+    ms_seed = launch_stats(d, f_seed, groups=20)["median_us"] * 1e-3
     seeded_same = bool(torch.equal(pkg.sample_solve_seeded(ps, pt, hyps, SEED, 0).view(torch.int32),
                                    H.view(torch.int32)))
     del idx_b

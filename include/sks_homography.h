@@ -127,9 +127,10 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
 int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
                         float hi, void* stream);
 
-/* Counter-based 32-bit draws: out[i] = high 32 bits of
- * splitmix64(seed * 0xA0761D6478BD642F + offset + i).  The RANSAC sampler's index
- * source (the reference draws with cuRAND MRG32K3A, GPU_Runtime Test.cu:1443-1446). */
+/* Counter-based 32-bit draws: out[i] = word(offset + i), where word w is the high (w even)
+ * or low (w odd) 32 bits of splitmix64(seed * 0xA0761D6478BD642F + w / 2) -- one 64-bit
+ * finaliser per two draws.  The RANSAC sampler's index source (the reference draws with
+ * cuRAND MRG32K3A, GPU_Runtime Test.cu:1443-1446).  out: 4-B aligned. */
 int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset,
                      void* stream);
 

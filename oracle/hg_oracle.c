@@ -368,9 +368,15 @@ int oracle_tensor_aca_rect_backward_f32(const float* src, const float* tar, cons
 /* Restates hg_fill_bits_u32 and hg_ransac_score_f32 (csrc/hg_ransac.hip), the
  * SURVEY 8(f).2 extension; the reference has no scorer, so these pin our own
  * definition (the division-free squared reprojection test, fixed FMA placement). */
+/* Word w of stream S = seed * K is half of mix64(S + w/2): the high 32 bits for even w,
+ * the low 32 for odd w (csrc/hg_ransac.hpp word_half / fill_bits_kernel). */
 int oracle_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offset) {
-    const uint64_t base = seed * 0xA0761D6478BD642Full + offset;
-    for (int64_t i = 0; i < count; ++i) out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
+    const uint64_t S = seed * 0xA0761D6478BD642Full;
+    for (int64_t i = 0; i < count; ++i) {
+        const uint64_t w = offset + (uint64_t)i;
+        const uint64_t z = mix64(S + (w >> 1));
+        out[i] = (w & 1) ? (uint32_t)z : (uint32_t)(z >> 32);
+    }
     return 0;
 }
 

@@ -55,7 +55,7 @@ int hg_sample_solve_seeded_f32(const float* pool_src, const float* pool_tar, uin
         return (int)hipErrorInvalidValue;
     return hg::launch_sample_seeded(reinterpret_cast<const float2*>(pool_src),
                                     reinterpret_cast<const float2*>(pool_tar), npool,
-                                    seed * hg::kBitsMul + offset, H, n, algo,
+                                    seed, offset, H, n, algo,
                                     (flags & HG_FLAG_NORMALIZE) != 0,
                                     reinterpret_cast<hipStream_t>(stream));
 }

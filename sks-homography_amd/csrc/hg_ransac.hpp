@@ -17,22 +17,59 @@ namespace hg {
 
 constexpr uint64_t kBitsMul = 0xA0761D6478BD642Full;
 
+// Word w of stream S = seed * kBitsMul is one half of the splitmix64 finaliser of counter
+// S + w/2: the high 32 bits for even w, the low 32 for odd w -- one 64-bit hash per two
+// draws (each finaliser costs six quarter-rate 32-bit multiplies; taking both halves
+// halved the seeded sampler's hashing, tools/kbench_sample.py).  Restated in
+// oracle/hg_oracle.c.
+__device__ __forceinline__ uint32_t word_half(uint64_t z, bool lo) {
+    return lo ? (uint32_t)z : (uint32_t)(z >> 32);
+}
+
+// out[i] = word(offset + i).  Thread t owns the hash of counter S + (offset >> 1) + t, i.e.
+// words 2j, 2j + 1 of the stream; the pair lands in out[2t - (offset & 1)] and the next.
 static __global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __restrict__ out,
                                                            int64_t count, uint64_t seed,
                                                            uint64_t offset) {
-    const uint64_t base = seed * kBitsMul + offset;
+    const uint64_t base = seed * kBitsMul + (offset >> 1);
+    const int64_t odd = (int64_t)(offset & 1);
+    const int64_t pairs = (count + odd + 1) >> 1;
     const int64_t stride = (int64_t)gridDim.x * kBlock;
-    for (int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x; i < count; i += stride)
-        out[i] = (uint32_t)(mix64(base + (uint64_t)i) >> 32);
+    const bool vec = odd == 0 && (reinterpret_cast<uintptr_t>(out) & 7u) == 0;
+    for (int64_t t = (int64_t)blockIdx.x * kBlock + threadIdx.x; t < pairs; t += stride) {
+        const uint64_t z = mix64(base + (uint64_t)t);
+        const int64_t i = 2 * t - odd;  // out index of word 2j (may be -1 when odd)
+        if (vec && i + 1 < count) {
+            *reinterpret_cast<uint2*>(out + i) = make_uint2(word_half(z, false), word_half(z, true));
+        } else {
+            if (i >= 0 && i < count) out[i] = word_half(z, false);
+            if (i + 1 < count) out[i + 1] = word_half(z, true);
+        }
+    }
 }
 
-// The 4 draws of hypothesis p: row p of the (n,4) index array, or -- SEEDED -- the same
-// four words generated in place, out[4p .. 4p+3] of fill_bits_kernel with
-// base = seed * kBitsMul + offset (so a seeded launch equals fill_bits + an indexed one,
-// bit for bit, without the 16 B per hypothesis of index traffic).
-template <bool SEEDED>
-__device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, int64_t p) {
-    if constexpr (SEEDED) {
+// Where a hypothesis' four draws come from.
+constexpr int kDrawsIndexed = 0;  // row p of the (n,4) index array
+constexpr int kDrawsPaired = 1;   // seeded: fill_bits' stream generated in place (shipped)
+constexpr int kDrawsSingle = 2;   // seeded, tune only: one hash per draw (the earlier stream)
+
+// The 4 draws of hypothesis p: row p of the (n,4) index array, or -- seeded -- the same
+// four words generated in place: words offset + 4p ... + 3 of the stream, i.e. out[4p ..
+// 4p+3] of fill_bits_kernel (so a seeded launch equals fill_bits + an indexed one, bit for
+// bit, without the 16 B per hypothesis of index traffic).  bits_base = S + (offset >> 1);
+// an odd offset shifts the four words across three hashes (a wave-uniform branch).
+template <int DRAWS>
+__device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, bool odd, int64_t p) {
+    if constexpr (DRAWS == kDrawsPaired) {
+        const uint64_t b = bits_base + 2 * (uint64_t)p;
+        const uint64_t z0 = mix64(b), z1 = mix64(b + 1);
+        if (!odd)
+            return u32x4{word_half(z0, false), word_half(z0, true), word_half(z1, false),
+                         word_half(z1, true)};
+        const uint64_t z2 = mix64(b + 2);
+        return u32x4{word_half(z0, true), word_half(z1, false), word_half(z1, true),
+                     word_half(z2, false)};
+    } else if constexpr (DRAWS == kDrawsSingle) {
         const uint64_t b = bits_base + 4 * (uint64_t)p;
         return u32x4{(uint32_t)(mix64(b) >> 32), (uint32_t)(mix64(b + 1) >> 32),
                      (uint32_t)(mix64(b + 2) >> 32), (uint32_t)(mix64(b + 3) >> 32)};
@@ -46,10 +83,11 @@ __device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, in
 // (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
 // LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
 // does (.cu:56-59, modulo bias and duplicates included).
-template <int ALGO, bool NORM, int P, bool SEEDED = false>
+template <int ALGO, bool NORM, int P, int DRAWS = kDrawsIndexed>
 __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
-    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n, uint64_t bits_base = 0) {
+    const uint4* __restrict__ idx, float* __restrict__ H, int64_t n, uint64_t bits_base = 0,
+    uint32_t bits_odd = 0) {
     constexpr int kTile = kWave * P;
     constexpr int kIdx = kTile * 16;
     constexpr int kLds = kIdx > kTile * 36 ? kIdx : kTile * 36;
@@ -61,10 +99,10 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     char* lds = smem[wave];
     const bool full = base + kTile <= n;
     uint4 r[P];
-    if constexpr (SEEDED) {
+    if constexpr (DRAWS != kDrawsIndexed) {
 #pragma unroll
         for (int j = 0; j < P; ++j) {
-            const u32x4 d = draws4<true>(nullptr, bits_base, base + j * kWave + lane);
+            const u32x4 d = draws4<DRAWS>(nullptr, bits_base, bits_odd != 0, base + j * kWave + lane);
             r[j] = make_uint4(d[0], d[1], d[2], d[3]);
         }
     } else if (full) {
@@ -153,12 +191,12 @@ __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uin
 // the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
 // and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
 // staging to fit the block's LDS (checked on the host).
-template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock, bool SEEDED = false,
-          bool MOD64 = false>
+template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
+          int DRAWS = kDrawsIndexed, bool MOD64 = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
-    uint64_t bits_base = 0) {
+    uint64_t bits_base = 0, uint32_t bits_odd = 0) {
     constexpr int kTile = kWave * P;
     constexpr int kStage = kTile * 36;
     extern __shared__ __attribute__((aligned(16))) char dyn[];
@@ -179,7 +217,7 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int64_t p = tile * kTile + j * kWave + lane;
-            r[j] = p < n ? draws4<SEEDED>(idx, bits_base, p) : u32x4{0, 0, 0, 0};
+            r[j] = p < n ? draws4<DRAWS>(idx, bits_base, bits_odd != 0, p) : u32x4{0, 0, 0, 0};
         }
     };
     // index rows of the next PF tiles stay in flight while this tile is solved
@@ -266,7 +304,7 @@ inline int launch_sample_wide(const float2* ps, const float2* pt, uint32_t npool
     do {                                                                                       \
         auto k = sample_solve_lds_kernel<A, N, P, 1, WPB>;                                     \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;           \
-        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n, 0);                      \
+        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n, 0, 0);                   \
     } while (0)
     if (algo == 0) { if (norm) HG_SW(kACA, true); else HG_SW(kACA, false); }
     else { if (norm) HG_SW(kSKS, true); else HG_SW(kSKS, false); }
@@ -460,7 +498,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
         else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
     } else if (mod64) {
 #define HG_SL64(A, N)                                                                        \
-    sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, false, true><<<g, kBlock, lds, s>>>( \
+    sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, true><<<g, kBlock, lds, s>>>( \
         ps, pt, npool, magic, ix, H, n, 0)
         if (algo == 0) { if (norm) HG_SL64(kACA, true); else HG_SL64(kACA, false); }
         else { if (norm) HG_SL64(kSKS, true); else HG_SL64(kSKS, false); }
@@ -479,36 +517,46 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
     return (int)hipGetLastError();
 }
 
-// The seeded sampler's launcher: the shipped tiles of launch_sample_solve (LDS pool, P = 2,
-// while the pool fits 64 KiB of LDS; else the global-gather form) with the draws made in
-// the kernel from bits_base = seed * kBitsMul + offset.
-template <bool MOD64 = false>
+// The seeded sampler's launcher.  Shipped shape: the LDS-pool kernel with P = 2 and 8 waves
+// per block (the pool copy shared by twice the waves; LDS opt-in past 64 KiB) while the
+// pool plus staging fit the CU's 160 KiB, else the global-gather form.  The draws are made
+// in the kernel from word `offset` of stream seed * kBitsMul (draws4).  P, WPB, DRAWS and
+// MOD64 are open for the variant sweep (hg_tune_sample_seeded).
+template <int P = 2, int WPB = 8, int DRAWS = kDrawsPaired, bool MOD64 = false>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
-                                uint64_t bits_base, float* H, int64_t n, int algo, bool norm,
-                                hipStream_t s) {
-    constexpr int P = 2;
-    const size_t lds = sample_lds_bytes<P>(npool);
-    if (lds > kSampleLdsMax) {
-        const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
+                                uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
+                                bool norm, hipStream_t s) {
+    const uint64_t bits_base = DRAWS == kDrawsSingle ? seed * kBitsMul + offset
+                                                     : seed * kBitsMul + (offset >> 1);
+    const uint32_t odd = DRAWS == kDrawsSingle ? 0u : (uint32_t)(offset & 1);
+    const size_t lds = sample_lds_bytes<P, WPB>(npool);
+    if (lds > kSampleLdsOptIn) {
+        constexpr int PG = 2;
+        const int64_t blocks = (n + (int64_t)kBlock * PG - 1) / ((int64_t)kBlock * PG);
         if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         const unsigned g = (unsigned)blocks;
-#define HG_SG(A, N) \
-    sample_solve_kernel<A, N, P, true><<<g, kBlock, 0, s>>>(ps, pt, npool, nullptr, H, n, bits_base)
+#define HG_SG(A, N)                                                                       \
+    sample_solve_kernel<A, N, PG, DRAWS><<<g, kBlock, 0, s>>>(ps, pt, npool, nullptr, H, n, \
+                                                              bits_base, odd)
         if (algo == 0) { if (norm) HG_SG(kACA, true); else HG_SG(kACA, false); }
         else { if (norm) HG_SG(kSKS, true); else HG_SG(kSKS, false); }
 #undef HG_SG
         return (int)hipGetLastError();
     }
+    // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
     const int64_t tiles = (n + (int64_t)kWave * P - 1) / ((int64_t)kWave * P);
-    const int64_t want = (tiles + kWavesPerBlock - 1) / kWavesPerBlock;
-    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
+    const int64_t want = (tiles + WPB - 1) / WPB;
+    int64_t per_cu = (int64_t)kSampleLdsOptIn / (int64_t)lds;
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
     const uint64_t magic = MOD64 ? fastmod64_magic(npool) : fastmod_magic(npool);
-#define HG_SD(A, N)                                                                          \
-    sample_solve_lds_kernel<A, N, P, 1, kWavesPerBlock, true, MOD64><<<g, kBlock, lds, s>>>(  \
-        ps, pt, npool, magic, nullptr, H, n, bits_base)
+#define HG_SD(A, N)                                                                         \
+    do {                                                                                    \
+        auto k = sample_solve_lds_kernel<A, N, P, 1, WPB, DRAWS, MOD64>;                    \
+        if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
+        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, nullptr, H, n, bits_base, odd); \
+    } while (0)
     if (algo == 0) { if (norm) HG_SD(kACA, true); else HG_SD(kACA, false); }
     else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }
 #undef HG_SD

@@ -546,8 +546,10 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
                                    reinterpret_cast<hipStream_t>(stream));
 }
 
-// Seeded sampler variants (tools/kbench_sample.py): 0 = shipped (32-bit round-up
-// remainder), 1 = the 64-bit remainder.
+// Seeded sampler variants (tools/kbench_sample.py), (P, waves per block): 0 = shipped (2, 8);
+// 1 = (2, 4); 2 = (1, 16); 3 = (2, 16); 4 = shipped shape with the 64-bit remainder;
+// 5 / 6 = one hash per draw (the earlier stream, not fill_bits': compared by time only) at
+// (2, 4) / (2, 8).
 int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
                           uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
                           int algo, int flags, void* stream) {
@@ -556,11 +558,16 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
     const auto* ps = reinterpret_cast<const float2*>(pool_src);
     const auto* pt = reinterpret_cast<const float2*>(pool_tar);
     const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
-    const uint64_t base = seed * hg::kBitsMul + offset;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    using namespace hg;
     switch (variant) {
-        case 0: return hg::launch_sample_seeded<false>(ps, pt, npool, base, H, n, algo, norm, st);
-        case 1: return hg::launch_sample_seeded<true>(ps, pt, npool, base, H, n, algo, norm, st);
+        case 0: return launch_sample_seeded<2, 8>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 1: return launch_sample_seeded<2, 4>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 2: return launch_sample_seeded<1, 16>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 3: return launch_sample_seeded<2, 16>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 4: return launch_sample_seeded<2, 8, kDrawsPaired, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 5: return launch_sample_seeded<2, 4, kDrawsSingle>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 6: return launch_sample_seeded<2, 8, kDrawsSingle>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -17,9 +17,23 @@ def _pool(dev):
 
 
 def test_fill_bits_matches_host(oracle, pkg, dev):
-    for off in (0, 977, (1 << 34) + 3):
-        got = pkg.fill_bits(50_001, 7, off, dev).cpu().numpy().view(np.uint32)
-        np.testing.assert_array_equal(got, oracle.fill_bits(50_001, 7, off))
+    for off in (0, 2, 977, (1 << 34) + 3):
+        for count in (1, 2, 3, 50_001, 50_002):
+            got = pkg.fill_bits(count, 7, off, dev).cpu().numpy().view(np.uint32)
+            np.testing.assert_array_equal(got, oracle.fill_bits(count, 7, off), err_msg=f"{off} {count}")
+
+
+def test_fill_bits_unaligned_output(oracle, pkg, dev):
+    """An output 4-B but not 8-B aligned takes the per-word store path (the paired uint2
+    store needs 8 B): same words, nothing written outside [0, count)."""
+    buf = torch.full((1 + 4099 + 1,), -1, dtype=torch.int32, device=dev)
+    for off in (0, 1):
+        buf.fill_(-1)
+        pkg._lib.call("hg_fill_bits_u32", buf.data_ptr() + 4, 4099, 9, off,
+                      torch.cuda.current_stream(dev).cuda_stream)
+        got = buf.cpu().numpy().view(np.uint32)
+        assert got[0] == 0xFFFFFFFF and got[-1] == 0xFFFFFFFF
+        np.testing.assert_array_equal(got[1:-1], oracle.fill_bits(4099, 9, off))
 
 
 @pytest.mark.parametrize("n", [1, 127, 128, 129, 1000, 65_537])

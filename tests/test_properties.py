@@ -70,3 +70,34 @@ def test_gpu_bit_exact_on_arbitrary_floats(orc, oracle, pkg, dev, batch):
         H64 = pkg.solve(algo, ds.double(), dt.double()).cpu().numpy()
         assert orc.same_bits(H64, oracle.solve(algo, src.astype(np.float64),
                                                tar.astype(np.float64))).all()
+
+
+def _splitmix64(z: int) -> int:
+    """splitmix64's finaliser (Steele, Lea & Flood, OOPSLA 2014), in Python integers."""
+    m = (1 << 64) - 1
+    z = (z + 0x9E3779B97F4A7C15) & m
+    z = ((z ^ (z >> 30)) * 0xBF58476D1CE4E5B9) & m
+    z = ((z ^ (z >> 27)) * 0x94D049BB133111EB) & m
+    return z ^ (z >> 31)
+
+
+@pytest.mark.parametrize("seed,offset,count", [(11, 0, 9), (7, 1, 8), (0, 5, 7), (2**63 + 3, 2**40 + 1, 5)])
+def test_oracle_fill_bits_stream(oracle, seed, offset, count):
+    """The RANSAC draw stream (hg_fill_bits_u32): word w = high half (w even) or low half
+    (w odd) of splitmix64(seed * K + w // 2), K = 0xA0761D6478BD642F, restated here in
+    Python integers against the oracle's C, odd offsets included."""
+    m = (1 << 64) - 1
+    S = (seed * 0xA0761D6478BD642F) & m
+    want = []
+    for i in range(count):
+        w = offset + i
+        z = _splitmix64((S + (w >> 1)) & m)
+        want.append(z & 0xFFFFFFFF if w & 1 else z >> 32)
+    np.testing.assert_array_equal(oracle.fill_bits(count, seed, offset), np.array(want, np.uint32))
+
+
+def test_oracle_fill_bits_slices(oracle):
+    """Counter based: any window of the stream equals the same slice of a longer draw."""
+    whole = oracle.fill_bits(4099, 5, 0)
+    for off in (1, 2, 3, 1000, 1001):
+        np.testing.assert_array_equal(oracle.fill_bits(37, 5, off), whole[off:off + 37])
