@@ -5,7 +5,11 @@
 
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdint>
+#include <mutex>
+#include <utility>
+#include <vector>
 
 #include "hg_aos.hpp"
 #include "hg_solvers.hpp"
@@ -277,13 +281,26 @@ constexpr size_t sample_lds_bytes(uint32_t npool) {
 constexpr size_t kSampleLdsMax = 64 * 1024;      // per-block dynamic LDS without opt-in
 constexpr size_t kSampleLdsOptIn = 160 * 1024;   // gfx950: a workgroup may take the whole LDS
 
-// Allows a kernel more than 64 KiB of dynamic LDS (once per instantiation).
+// Allows `kernel` more than 64 KiB of dynamic LDS on the current device.  Remembered per
+// (device, kernel): the kernels of one signature share a function type, so a static per
+// template instantiation would opt in only the first of them.
+inline bool lds_opt_in(const void* kernel) {
+    static std::mutex mu;
+    static std::vector<std::pair<int, const void*>> done;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return false;
+    std::lock_guard<std::mutex> lock(mu);
+    for (const auto& e : done)
+        if (e.first == dev && e.second == kernel) return true;
+    if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            (int)kSampleLdsOptIn) != hipSuccess)
+        return false;
+    done.emplace_back(dev, kernel);
+    return true;
+}
 template <typename K>
 inline bool lds_opt_in(K kernel) {
-    static const bool ok = hipFuncSetAttribute(reinterpret_cast<const void*>(kernel),
-                                               hipFuncAttributeMaxDynamicSharedMemorySize,
-                                               (int)kSampleLdsOptIn) == hipSuccess;
-    return ok;
+    return lds_opt_in(reinterpret_cast<const void*>(kernel));
 }
 
 // Variant sweep helper: the LDS-pool sampler with WPB waves per block (tools/kbench_sample.py).
@@ -449,15 +466,19 @@ __global__ __launch_bounds__(kBlock) void ransac_score_sgpr_kernel(
     if (p0 + 1 < n) counts[p0 + 1] = (uint32_t)cnt.y;
 }
 
+// Compute units of the current device (queried once per device).
 inline int cu_count() {
-    static int cus = [] {
-        int dev = 0, v = 0;
-        if (hipGetDevice(&dev) != hipSuccess ||
-            hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-            return 256;
-        return v > 0 ? v : 256;
-    }();
-    return cus;
+    constexpr int kMaxDevices = 64;
+    static std::atomic<int> cache[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return 256;
+    int v = cache[dev].load(std::memory_order_relaxed);
+    if (v == 0) {
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || v <= 0)
+            v = 256;
+        cache[dev].store(v, std::memory_order_relaxed);
+    }
+    return v;
 }
 
 // variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
