@@ -393,9 +393,12 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     f_score = lambda: pkg.ransac_score(H, ps, pt, thresh)  # noqa: E731
     for _ in range(3):
         f_solve()
-        f_score()
     _, ms_solve = timed_region(d, f_solve, 20)
-    _, ms_score = timed_region(d, f_score, 5)
+    # the scorer is VALU-bound (~0.8 ms a launch): warm ~25 ms, then the median of 10
+    # three-launch groups (clock wander, as for the 16M samplers below)
+    for _ in range(30):
+        f_score()
+    ms_score = launch_stats(d, f_score, groups=10, per_group=3)["median_us"] * 1e-3
     counts = pkg.ransac_score(H, ps, pt, thresh)
     pairs = hyps * ps.shape[0]
     big = 16 * hyps  # the sampler's HBM-rate figure (16 B idx + 36 B H per hypothesis)

@@ -108,6 +108,15 @@ def _dev_scalar(x, dev: torch.device) -> torch.Tensor:
     return torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)[:1]
 
 
+def _gpu_device(device) -> torch.device:
+    """A `device=` argument resolved to a GPU device (kernels must never see host memory)."""
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise ValueError("sks_homography_amd kernels run on the GPU only; got device "
+                         f"{dev} (no CPU fallback by design)")
+    return dev
+
+
 def _gpu_only(t: torch.Tensor) -> None:
     if not t.is_cuda:
         raise ValueError("sks_homography_amd kernels run on the GPU only; got a "
@@ -179,9 +188,16 @@ def tensor_aca_rect_autograd(src: torch.Tensor, tar: torch.Tensor, scale: Scalar
 def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: float = 1024.0,
                  device: Union[str, torch.device] = "cuda", out=None) -> torch.Tensor:
     """Counter-based U[lo,hi) float32 stream generated on the device."""
-    dev = torch.device(device)
+    if count < 0:
+        raise ValueError(f"count must be >= 0, got {count}")
     if out is None:
+        dev = _gpu_device(device)
         out = torch.empty(count, dtype=torch.float32, device=dev)
+    else:
+        dev = _require_device(out)
+        if out.dtype != torch.float32 or not out.is_contiguous() or out.numel() < count:
+            raise ValueError(f"out must be a contiguous float32 tensor of >= {count} elements, "
+                             f"got {out.dtype} {tuple(out.shape)}")
     with _guard(dev):
         _lib.call("hg_fill_uniform_f32", out.data_ptr(), count, seed, offset, lo, hi, _stream(dev))
     return out
@@ -190,6 +206,8 @@ def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: fl
 def stream_copy(src: torch.Tensor, dst: torch.Tensor) -> None:
     dev = _require_device(src, dst)
     nbytes = src.numel() * src.element_size()
+    if not (src.is_contiguous() and dst.is_contiguous()) or dst.numel() * dst.element_size() < nbytes:
+        raise ValueError("stream_copy needs contiguous tensors and dst at least as large as src")
     with _guard(dev):
         _lib.call("hg_stream_copy", src.data_ptr(), dst.data_ptr(), nbytes, _stream(dev))
 

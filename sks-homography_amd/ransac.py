@@ -13,7 +13,7 @@ from typing import NamedTuple
 import torch
 
 from . import _lib
-from .ops import _guard, _require_device, _stream
+from .ops import _gpu_device, _guard, _require_device, _stream
 
 
 def read_points(filename: str):
@@ -41,7 +41,9 @@ def read_points(filename: str):
 def fill_bits(count: int, seed: int, offset: int = 0, device="cuda") -> torch.Tensor:
     """Counter-based uint32 draws (held in an int32 tensor), bit-identical to the
     host regeneration."""
-    dev = torch.device(device)
+    if count < 0:
+        raise ValueError(f"count must be >= 0, got {count}")
+    dev = _gpu_device(device)
     out = torch.empty(count, dtype=torch.int32, device=dev)
     with _guard(dev):
         _lib.call("hg_fill_bits_u32", out.data_ptr(), count, seed, offset, _stream(dev))

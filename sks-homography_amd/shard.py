@@ -35,6 +35,10 @@ def gather_blocks(block: torch.Tensor, n_total: int, world: int, rank: int, dst:
     """
     import torch.distributed as dist
 
+    lo, hi = shard_range(n_total, world, rank)
+    if block.shape[0] != hi - lo:
+        # checked before any send/recv: a wrong-sized block would leave a peer waiting
+        raise ValueError(f"rank {rank} holds {block.shape[0]} rows, its block is [{lo},{hi})")
     if world == 1:
         return block
     if rank == dst:
@@ -50,7 +54,6 @@ def gather_blocks(block: torch.Tensor, n_total: int, world: int, rank: int, dst:
         for w in dist.batch_isend_irecv(ops) if ops else []:
             w.wait()
         return full
-    lo, hi = shard_range(n_total, world, rank)
     if hi > lo:
         for w in dist.batch_isend_irecv([dist.P2POp(dist.isend, block.contiguous(), dst, group)]):
             w.wait()
@@ -65,6 +68,8 @@ def scatter_blocks(full: Optional[torch.Tensor], n_total: int, world: int, rank:
     import torch.distributed as dist
 
     lo, hi = shard_range(n_total, world, rank)
+    if rank == src and (full is None or full.shape[0] != n_total):
+        raise ValueError(f"rank {src} must hold the whole ({n_total}, ...) batch")
     if world == 1:
         return full
     if rank == src:

@@ -137,6 +137,20 @@ def test_product_rejects_cpu_tensors(pkg):
         pkg.aca(x, x)
     with pytest.raises(ValueError, match="GPU only"):
         pkg.tensor_aca_rect(torch.zeros(2, 3, 4), torch.zeros(2, 3, 4), 1.0, 1.0)
+    # the generators take a device, not a tensor: a host device (or host `out`) must be
+    # refused before any kernel could be handed host memory
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.fill_bits(16, 1, 0, device="cpu")
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.fill_uniform(16, 1, device="cpu")
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.fill_uniform(16, 1, out=torch.empty(16))
+    with pytest.raises(ValueError, match="count"):
+        pkg.fill_bits(-1, 1, 0)
+    with pytest.raises(ValueError, match="count"):
+        pkg.fill_uniform(-1, 1)
+    with pytest.raises(ValueError, match="GPU only"):
+        pkg.stream_copy(torch.zeros(4), torch.zeros(4))
 
 
 def test_missing_library_fails_loudly(pkg, monkeypatch):

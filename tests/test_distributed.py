@@ -28,6 +28,19 @@ def test_shard_range_rejects_bad(pkg):
             pkg.shard_range(*args)
 
 
+def test_gather_scatter_reject_wrong_blocks(pkg):
+    """Shape errors are raised before any send/recv (no peer is left waiting)."""
+    import torch
+    from importlib import import_module
+    shard = import_module("sks_homography_amd.shard")
+    with pytest.raises(ValueError, match="rows"):
+        shard.gather_blocks(torch.zeros(4, 9), 10, 2, 1)   # rank 1's block is 5 rows
+    with pytest.raises(ValueError, match="whole"):
+        shard.scatter_blocks(torch.zeros(9, 8), 10, 2, 0, torch.zeros(1, 8))
+    with pytest.raises(ValueError, match="whole"):
+        shard.scatter_blocks(None, 10, 2, 0, torch.zeros(1, 8))
+
+
 def _free_port():
     with socket.socket() as s:
         s.bind(("127.0.0.1", 0))

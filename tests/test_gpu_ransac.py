@@ -159,3 +159,17 @@ def test_sample_solve_seeded_zero_and_errors(pkg, dev):
         pkg.sample_solve_seeded(ps, ps, 5, 1, algo="ge")
     with pytest.raises(ValueError):
         pkg.sample_solve_seeded(ps, ps, -1, 1)
+
+
+def test_generators_validate_out(pkg, dev):
+    """fill_uniform's `out` must hold `count` contiguous float32 elements on the GPU."""
+    with pytest.raises(ValueError, match="out must be"):
+        pkg.fill_uniform(100, 1, out=torch.empty(99, device=dev))
+    with pytest.raises(ValueError, match="out must be"):
+        pkg.fill_uniform(10, 1, out=torch.empty(10, dtype=torch.float64, device=dev))
+    with pytest.raises(ValueError, match="out must be"):
+        pkg.fill_uniform(10, 1, out=torch.empty(20, device=dev)[::2])
+    o = torch.empty(12, device=dev)
+    assert pkg.fill_uniform(10, 1, out=o) is o
+    with pytest.raises(ValueError, match="stream_copy"):
+        pkg.stream_copy(torch.zeros(8, device=dev), torch.zeros(4, device=dev))
