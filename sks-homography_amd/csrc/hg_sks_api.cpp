@@ -21,27 +21,41 @@ bool is_device_pointer(const void* p) {
 // serialise on the legacy default stream) and 9 values of host memory mapped into the
 // device address space, which the kernel writes directly.  The points go in the kernel
 // arguments (hg_solve_one_*), so a call is one launch + one stream synchronisation.
+// One slot per device the thread has used; released when the thread exits.
 template <typename T>
 struct Scratch {
-    T* host = nullptr;
-    T* mapped = nullptr;
-    hipStream_t stream = nullptr;
-    int device = -1;
+    static constexpr int kMaxDevices = 64;
+    struct Slot {
+        T* host = nullptr;
+        T* mapped = nullptr;
+        hipStream_t stream = nullptr;
+    };
+    Slot slot[kMaxDevices];
+    Slot* cur = nullptr;
+
     int ensure() {
-        int cur = 0;
-        hipError_t e = hipGetDevice(&cur);
+        int dev = 0;
+        hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return (int)e;
-        if (host && device == cur) return 0;
-        if ((e = hipStreamCreateWithFlags(&stream, hipStreamNonBlocking)) != hipSuccess)
+        if (dev < 0 || dev >= kMaxDevices) return (int)hipErrorInvalidDevice;
+        Slot& sl = slot[dev];
+        cur = &sl;
+        if (sl.mapped) return 0;
+        if (!sl.stream && (e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking)) != hipSuccess)
             return (int)e;
-        if ((e = hipHostMalloc(reinterpret_cast<void**>(&host), 16 * sizeof(T),
-                               hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+        if (!sl.host && (e = hipHostMalloc(reinterpret_cast<void**>(&sl.host), 16 * sizeof(T),
+                                           hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
             return (int)e;
-        if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&mapped), host, 0)) !=
+        if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.mapped), sl.host, 0)) !=
             hipSuccess)
             return (int)e;
-        device = cur;
         return 0;
+    }
+    ~Scratch() {
+        for (Slot& sl : slot) {
+            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            if (sl.host) (void)hipHostFree(sl.host);
+        }
     }
 };
 
@@ -77,15 +91,15 @@ int solve_one(T* src, T* tar, T* result) {
         hipError_t e = hipMemcpy(in, src, 8 * sizeof(T), hipMemcpyDefault);
         if (e == hipSuccess) e = hipMemcpy(in + 8, tar, 8 * sizeof(T), hipMemcpyDefault);
         if (e != hipSuccess) return (int)e;
-        rc = ONE(ALGO, in, in + 8, s.mapped, HG_FLAG_NORMALIZE, s.stream);
+        rc = ONE(ALGO, in, in + 8, s.cur->mapped, HG_FLAG_NORMALIZE, s.cur->stream);
     } else {
-        rc = ONE(ALGO, src, tar, s.mapped, HG_FLAG_NORMALIZE, s.stream);
+        rc = ONE(ALGO, src, tar, s.cur->mapped, HG_FLAG_NORMALIZE, s.cur->stream);
     }
     if (rc) return rc;
-    hipError_t e = hipStreamSynchronize(s.stream);
+    hipError_t e = hipStreamSynchronize(s.cur->stream);
     if (e != hipSuccess) return (int)e;
-    if (dr) return (int)hipMemcpy(result, s.host, 9 * sizeof(T), hipMemcpyHostToDevice);
-    std::memcpy(result, s.host, 9 * sizeof(T));
+    if (dr) return (int)hipMemcpy(result, s.cur->host, 9 * sizeof(T), hipMemcpyHostToDevice);
+    std::memcpy(result, s.cur->host, 9 * sizeof(T));
     return 0;
 }
 
