@@ -339,9 +339,12 @@ def reference_layout(d: Dist, pkg):
 def host_boundary_section(d: Dist, pkg, n: int):
     """What the host-buffer side of the boundary costs (reported, never `value`):
     (1) the reference's single-problem C++ call sks::runKernel_ACA on host pointers
-    (one H2D + launch + D2H each, synchronous like ACA_SKS.cpp:24); (2) a host-resident
-    n-problem batch: pinned H2D of src/tar + the kernel + D2H of H, i.e. the
-    PCIe-inclusive rate of a caller whose data lives in host memory."""
+    (the points ride in the launch, H comes back through mapped memory; synchronous like
+    ACA_SKS.cpp:24); (2) a host-resident n-problem batch, the PCIe-inclusive rate of a
+    caller whose data lives in host memory: `staged` = pinned H2D of src/tar + the kernel
+    + D2H of H on one stream; `zero_copy_*` = hg_solve_host_f32, the kernel reading and
+    writing the host buffers over PCIe itself, from pinned and from pageable memory (the
+    latter registered for the call); `h2d_bound` = the 64 B/problem H2D copy alone."""
     import ctypes
     lib = pkg.lib()
     f = lib._ZN3sks13runKernel_ACAEPfS0_S0_
@@ -356,27 +359,45 @@ def host_boundary_section(d: Dist, pkg, n: int):
     for _ in range(reps):
         f(s8, t8, h9)
     single_us = (time.perf_counter() - t0) / reps * 1e6
+    ds = pkg.fill_uniform(n * 8, SEED, 0, device=d.dev).view(n, 8)
+    dt = pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(n, 8)
     hs = torch.empty((n, 8), dtype=torch.float32).pin_memory()
     ht = torch.empty((n, 8), dtype=torch.float32).pin_memory()
     hH = torch.empty((n, 9), dtype=torch.float32).pin_memory()
-    hs.copy_(pkg.fill_uniform(n * 8, SEED, 0, device=d.dev).view(n, 8).cpu())
-    ht.copy_(pkg.fill_uniform(n * 8, SEED, n * 8, device=d.dev).view(n, 8).cpu())
-    ds = torch.empty((n, 8), device=d.dev)
-    dt = torch.empty((n, 8), device=d.dev)
+    hs.copy_(ds.cpu())
+    ht.copy_(dt.cpu())
     dH = torch.empty((n, 9), device=d.dev)
+    want = pkg.solve("aca", ds, dt, out=dH).cpu()
 
-    def step():
+    def staged():
         ds.copy_(hs, non_blocking=True)
         dt.copy_(ht, non_blocking=True)
         pkg.solve("aca", ds, dt, out=dH)
         hH.copy_(dH, non_blocking=True)
 
-    step()
-    wall, _ = timed_region(d, step, 5)
-    return {"single_problem_host_ptr_us": round(single_us, 2),
-            "pcie_inclusive_batch": n, "pcie_inclusive_ms": round(wall / 5 * 1e3, 3),
-            "pcie_inclusive_M_homographies_per_s": round(n * 5 / wall / 1e6, 1),
-            "pcie_bytes_per_problem": 100}
+    def h2d():
+        ds.copy_(hs, non_blocking=True)
+        dt.copy_(ht, non_blocking=True)
+
+    qs, qt = hs.clone(), ht.clone()  # pageable copies
+    qH = torch.empty((n, 9), dtype=torch.float32)
+    out = {"single_problem_host_ptr_us": round(single_us, 2), "batch": n,
+           "pcie_bytes_per_problem": 100}
+    for name, fn, res in (("staged", staged, hH),
+                          ("zero_copy_pinned", lambda: pkg.solve_host("aca", hs, ht, out=hH), hH),
+                          ("zero_copy_pageable", lambda: pkg.solve_host("aca", qs, qt, out=qH), qH),
+                          ("h2d_bound", h2d, None)):
+        fn()
+        torch.cuda.synchronize(d.dev)
+        wall, _ = timed_region(d, fn, 5)
+        ms = wall / 5 * 1e3
+        rec = {"ms": round(ms, 3), "M_homographies_per_s": round(n / ms / 1e3, 1)}
+        if res is not None:
+            rec["bit_exact"] = bool(torch.equal(res.view(torch.int32), want.view(torch.int32)))
+        out[name] = rec
+    out["zero_copy_speedup_vs_staged"] = round(out["staged"]["ms"] / out["zero_copy_pinned"]["ms"], 2)
+    del hs, ht, hH, qs, qt, qH, ds, dt, dH
+    return out
 
 
 def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):

@@ -2,7 +2,8 @@
 // the MI355X library.  It makes the calls the reference's CPU harness makes
 // ("C++ Codes/Runtime Test/CPU_Runtime Test/main.cpp:87-114": sks::runKernel_ACA /
 // _ACA_double / _SKS / _SKS_double on 8-float point lists) and then the batch form a
-// throughput caller should use (device buffers, one launch per batch).
+// throughput caller should use (device buffers, one launch per batch; or host vectors,
+// read and written by the kernel over PCIe).
 //
 // Build (see tests/test_gpu_cpp_api.py):
 //   g++ -std=c++17 -Iinclude -I/opt/rocm/include -D__HIP_PLATFORM_AMD__ examples/dropin_main.cpp
@@ -64,6 +65,16 @@ int main() {
             std::fprintf(stderr, "batch row %lld differs from the single call\n", (long long)i);
             return 6;
         }
+    // the same batch straight from std::vector (pageable host memory, the reference's own
+    // data placement): the kernel reads and writes it over PCIe (hg_solve_host_f32)
+    std::vector<float> hH2(n * 9, -1.0f);
+    if (check(sks::runKernel_ACA_batch(hs.data(), ht.data(), hH2.data(), n),
+              "runKernel_ACA_batch(host vectors)"))
+        return 11;
+    if (std::memcmp(hH2.data(), hH.data(), n * 36) != 0) {
+        std::fprintf(stderr, "host-vector batch differs from the device batch\n");
+        return 12;
+    }
     // device pointers through the single-problem signature too
     if (check(sks::runKernel_SKS(ds, dt, dH), "runKernel_SKS(device ptrs)")) return 7;
     float row[9];

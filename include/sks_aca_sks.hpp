@@ -11,8 +11,11 @@
 // Returns 0 on success (the reference always returns 0, ACA_SKS.cpp:101), or the
 // hipError_t of a failed copy/launch.
 //
-// The *_batch overloads are the bulk entry points a caller should use: device
-// pointers, AoS (n,8)/(n,8)/(n,9), asynchronous on `stream` (hipStream_t or NULL).
+// The *_batch overloads are the bulk entry points a caller should use: AoS
+// (n,8)/(n,8)/(n,9), normalised.  Device-visible buffers (device, managed or pinned host
+// memory) are solved asynchronously on `stream` (hipStream_t or NULL); if any buffer is
+// pageable host memory the call goes through hg_solve_host_* (registered for the call,
+// read and written over PCIe by the kernel, synchronous).
 #pragma once
 #include <cstdint>
 

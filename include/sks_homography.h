@@ -2,7 +2,7 @@
  * sks_homography.h -- C ABI of the MI355X (gfx950) batched 4-point homography
  * solver.  Library: sks-homography_amd/lib/libsks_homography_amd.so
  *
- * Every entry point:
+ * Every entry point except hg_solve_host_* (host-resident batches, synchronous, below):
  *   - takes DEVICE pointers the caller owns (the library allocates nothing),
  *   - enqueues its work on `stream` (a hipStream_t; NULL = the legacy default
  *     stream) and returns without synchronising,
@@ -170,6 +170,33 @@ int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int
                      void* stream);
 int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, int flags,
                      void* stream);
+
+/* Solver ids of hg_solve_host_*. */
+#define HG_ALGO_ACA 0
+#define HG_ALGO_SKS 1
+#define HG_ALGO_GE 2
+#define HG_ALGO_GPT 3 /* binary64 only */
+
+/* A batch whose src/tar/H live in HOST memory -- the reference C++ API's data placement
+ * (ACA_SKS.hpp:17-20 take host arrays; CPU_Runtime Test/main.cpp:87-114), batched.  The
+ * kernel of hg_<algo>_f32/_f64 reads src/tar from host memory over PCIe and writes H back
+ * there directly (zero-copy: both link directions busy at once, no device buffer): pinned
+ * memory (hipHostMalloc / hipHostRegister with a device mapping) is used as it is;
+ * pageable memory is registered (hipHostRegisterMapped, whole pages, overlapping buffers
+ * merged) for the call and unregistered before it returns -- such calls are serialised
+ * process-wide, and fail (hipErrorHostMemoryAlreadyRegistered ...) if the caller holds a
+ * registration over part of those pages.  Device or managed pointers are accepted too.
+ * SYNCHRONOUS, unlike every other entry point: H is complete on return.  stream NULL =
+ * hipStreamPerThread when any buffer is host memory, else the legacy default stream.
+ * Same layouts, flags, validation and bits as hg_<algo>_*; algo is an HG_ALGO_* id
+ * (HG_ALGO_GPT binary64 only).  hipErrorInvalidValue also when a buffer's first and
+ * last bytes lie in different kinds of memory (e.g. a pinned block and pageable memory
+ * after it).  Buffers must be the caller's own, whole: the call cannot see every
+ * overrun. */
+int hg_solve_host_f32(int algo, const float* src, const float* tar, float* H, int64_t n,
+                      int layout, int flags, void* stream);
+int hg_solve_host_f64(int algo, const double* src, const double* tar, double* H, int64_t n,
+                      int layout, int flags, void* stream);
 
 /* Deterministic sums of the rows of x (rows, cols), row-major, into out[rows]: a fixed
  * two-level order (chunks of 4096 in order, folded by halving strides), so the bits do

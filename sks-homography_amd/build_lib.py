@@ -23,7 +23,7 @@ TORCH_LIB = os.path.join(LIB_DIR, "libsks_homography_torch.so")
 TUNE_LIB = os.path.join(LIB_DIR, "libsks_homography_tune.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
-SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_sks_api.cpp"]
+SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_sks_api.cpp", "hg_host.cpp"]
 # kernel-variant sweeps and timing loops (tools/, tests): a separate library so the product
 # library carries only the shipped kernels
 TUNE_SOURCES = ["hg_tune.hip"]

@@ -103,6 +103,35 @@ int solve_one(T* src, T* tar, T* result) {
     return 0;
 }
 
+// Batches: device-visible buffers (device, managed or pinned host memory) are solved
+// asynchronously on `stream`; a batch with any pageable host buffer goes through
+// hg_solve_host_* (registered for the call, zero-copy, synchronous).
+bool is_pageable(const void* p) {
+    hipPointerAttribute_t attr;
+    if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return true;
+    }
+    return attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged &&
+           attr.type != hipMemoryTypeHost;
+}
+
+template <typename T>
+using HostFn = int (*)(int, const T*, const T*, T*, int64_t, int, int, void*);
+
+template <typename T>
+int solve_batch(BatchFn<T> dev, int algo, const T* src, const T* tar, T* result, int64_t n,
+                void* stream) {
+    if (n > 0 && src && tar && result &&
+        (is_pageable(src) || is_pageable(tar) || is_pageable(result))) {
+        HostFn<T> host;
+        if constexpr (sizeof(T) == 4) host = hg_solve_host_f32;
+        else host = hg_solve_host_f64;
+        return host(algo, src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+    }
+    return dev(src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+}
+
 }  // namespace
 
 namespace sks {
@@ -122,19 +151,19 @@ int runKernel_SKS_double(double* src, double* tar, double* result) {
 
 int runKernel_ACA_batch(const float* src, const float* tar, float* result, int64_t n,
                         void* stream) {
-    return hg_aca_f32(src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+    return solve_batch<float>(hg_aca_f32, HG_ALGO_ACA, src, tar, result, n, stream);
 }
 int runKernel_ACA_double_batch(const double* src, const double* tar, double* result,
                                int64_t n, void* stream) {
-    return hg_aca_f64(src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+    return solve_batch<double>(hg_aca_f64, HG_ALGO_ACA, src, tar, result, n, stream);
 }
 int runKernel_SKS_batch(const float* src, const float* tar, float* result, int64_t n,
                         void* stream) {
-    return hg_sks_f32(src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+    return solve_batch<float>(hg_sks_f32, HG_ALGO_SKS, src, tar, result, n, stream);
 }
 int runKernel_SKS_double_batch(const double* src, const double* tar, double* result,
                                int64_t n, void* stream) {
-    return hg_sks_f64(src, tar, result, n, HG_LAYOUT_AOS, HG_FLAG_NORMALIZE, stream);
+    return solve_batch<double>(hg_sks_f64, HG_ALGO_SKS, src, tar, result, n, stream);
 }
 
 }  // namespace sks

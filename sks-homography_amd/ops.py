@@ -88,6 +88,53 @@ def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = Tru
     return _OPS.solve.out(src, tar, algo_id, normalize, lay, out=out)
 
 
+def solve_host(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = True,
+               layout: str = "aos", out: Optional[torch.Tensor] = None,
+               device: Union[int, str, torch.device, None] = None) -> torch.Tensor:
+    """``solve`` for a batch that lives in HOST memory (CPU tensors, pinned or not): the
+    GPU kernel reads src/tar over PCIe and writes H into the host tensor directly
+    (hg_solve_host_*, zero-copy; pageable tensors are registered for the call).  Returns
+    when H is complete.  ``device`` picks the GPU (default: the current one).  The
+    computation is the same HIP kernel with the same bits -- there is no CPU solver."""
+    algo_id = _ALGO_ID.get(algo)
+    if algo_id is None:
+        raise ValueError(f"algo must be 'aca', 'sks', 'ge' or 'gpt', got {algo!r}")
+    lay = _LAYOUT_ID.get(layout)
+    if lay is None:
+        raise ValueError(f"layout must be 'aos' or 'soa', got {layout!r}")
+    for t in (src, tar) + ((out,) if out is not None else ()):
+        if t.device.type != "cpu":
+            raise ValueError(f"solve_host takes host tensors, got a {t.device} tensor (use solve)")
+        if not t.is_contiguous():
+            raise ValueError("solve_host needs contiguous tensors (the kernel reads raw memory)")
+    if src.dtype not in _DTYPES or tar.dtype is not src.dtype:
+        raise TypeError(f"src/tar must both be float32 or float64, got {src.dtype}/{tar.dtype}")
+    if algo_id == 3 and src.dtype is not torch.float64:
+        raise TypeError("the GPT-LU baseline (cal_Homo_GPT) is float64 only")
+    if lay == 0:
+        n = src.shape[0] if src.dim() else -1
+        ok = (src.dim() == 2 and src.shape[1] == 8) or (src.dim() == 3 and tuple(src.shape[1:]) == (4, 2))
+        want_out = (n, 9)
+    else:
+        n = src.shape[1] if src.dim() == 2 else -1
+        ok = src.dim() == 2 and src.shape[0] == 8
+        want_out = (9, n)
+    if not ok or tar.shape != src.shape:
+        raise ValueError(f"{layout} src/tar must be {'(n,8) or (n,4,2)' if lay == 0 else '(8,n)'} "
+                         f"and equal, got {tuple(src.shape)} / {tuple(tar.shape)}")
+    if out is None:
+        out = torch.empty(want_out, dtype=src.dtype)
+    elif tuple(out.shape) != want_out or out.dtype is not src.dtype:
+        raise ValueError(f"out must be {want_out} {src.dtype}, got {tuple(out.shape)} {out.dtype}")
+    dev = _gpu_device("cuda" if device is None else
+                      (torch.device("cuda", device) if isinstance(device, int) else device))
+    fn = "hg_solve_host_f32" if src.dtype is torch.float32 else "hg_solve_host_f64"
+    with _guard(dev):
+        _lib.call(fn, algo_id, src.data_ptr(), tar.data_ptr(), out.data_ptr(), n, lay,
+                  _lib.HG_FLAG_NORMALIZE if normalize else 0, None)
+    return out
+
+
 def aca(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torch.Tensor:
     return solve("aca", src, tar, normalize, layout, out)
 

@@ -126,7 +126,36 @@ def test_other_entry_validation(pkg):
     assert lib.hg_fill_bits_u32(None, 0, 0, 0, None) == 0
     assert lib.hg_stream_copy(None, None, 17, None) == 1                          # not x16
     assert lib.hg_stream_copy(None, None, 0, None) == 0
+    # host-resident batches: every check before the first HIP call
+    for f in (lib.hg_solve_host_f32, lib.hg_solve_host_f64):
+        assert f(0, None, None, None, -1, 0, 1, None) == 1                      # n < 0
+        assert f(0, None, None, None, 0, 0, 1, None) == 0                       # empty
+        assert f(0, None, None, None, 5, 0, 1, None) == 1                       # NULL
+        assert f(-1, None, None, None, 0, 0, 1, None) == 1                      # algo
+        assert f(0, None, None, None, 0, 2, 1, None) == 1                       # layout
+        assert f(0, None, None, None, 0, 0, 2, None) == 1                       # flags
+    assert lib.hg_solve_host_f32(3, None, None, None, 0, 0, 1, None) == 1       # GPT: f64 only
+    assert lib.hg_solve_host_f64(3, None, None, None, 0, 0, 1, None) == 0
+    assert lib.hg_solve_host_f64(4, None, None, None, 0, 0, 1, None) == 1
     assert pkg.version().startswith("sks-homography-amd")
+
+
+def test_solve_host_argument_checks(pkg):
+    """ops.solve_host validates shapes, dtypes and contiguity before the C call."""
+    import torch
+    x = torch.zeros(4, 8)
+    with pytest.raises(ValueError, match="contiguous"):
+        pkg.solve_host("aca", torch.zeros(8, 4).t(), x)
+    with pytest.raises(ValueError, match="equal"):
+        pkg.solve_host("aca", x, torch.zeros(5, 8))
+    with pytest.raises(ValueError, match="out must be"):
+        pkg.solve_host("aca", x, x, out=torch.zeros(4, 8))
+    with pytest.raises(TypeError, match="float64 only"):
+        pkg.solve_host("gpt", x, x)
+    with pytest.raises(ValueError, match="algo"):
+        pkg.solve_host("dlt", x, x)
+    with pytest.raises(ValueError, match=r"\(8,n\)"):
+        pkg.solve_host("aca", x, x, layout="soa")
 
 
 def test_product_rejects_cpu_tensors(pkg):

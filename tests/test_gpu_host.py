@@ -1,0 +1,149 @@
+"""Host-resident batches (hg_solve_host_f32/_f64, ops.solve_host): the kernel reads src/tar
+from host memory and writes H there.  Pinned and pageable buffers, every solver, both
+layouts, buffers cut from one allocation (sharing pages), misaligned views, threads at
+once -- each bit-identical to the device-resident solve, which tests/test_gpu_parity.py
+pins to the oracle; a small batch is also checked against the oracle directly."""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+SEED = 5
+
+
+def _inputs(pkg, dev, n, dtype, layout, off=0):
+    s = pkg.fill_uniform(n * 8, SEED, off, device=dev)
+    t = pkg.fill_uniform(n * 8, SEED, off + n * 8, device=dev)
+    shape = (n, 8) if layout == "aos" else (8, n)
+    return s.view(shape).to(dtype), t.view(shape).to(dtype)
+
+
+def _bits(x):
+    return x.view(torch.int32 if x.dtype is torch.float32 else torch.int64)
+
+
+def _hip():
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipPointerGetAttributes.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    return hip
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+@pytest.mark.parametrize("pinned", [False, True])
+def test_host_batch_matches_device(pkg, dev, dtype, layout, pinned):
+    n = 70001  # ragged: not a multiple of any tile
+    algos = ["aca", "sks", "ge"] + (["gpt"] if dtype is torch.float64 else [])
+    ds, dt = _inputs(pkg, dev, n, dtype, layout)
+    hs, ht = ds.cpu(), dt.cpu()
+    if pinned:
+        hs, ht = hs.pin_memory(), ht.pin_memory()
+    for algo in algos:
+        for norm in (True, False):
+            want = pkg.solve(algo, ds, dt, normalize=norm, layout=layout).cpu()
+            out = torch.full(want.shape, float("nan"), dtype=dtype)
+            if pinned:
+                out = out.pin_memory()
+            got = pkg.solve_host(algo, hs, ht, normalize=norm, layout=layout, out=out)
+            assert got is out
+            assert torch.equal(_bits(got), _bits(want)), (algo, norm)
+
+
+def test_host_batch_vs_oracle(pkg, dev, oracle):
+    n = 4099
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=123)
+    hs, ht = ds.cpu(), dt.cpu()
+    for algo in ("aca", "sks"):
+        got = pkg.solve_host(algo, hs, ht, normalize=True)
+        want = oracle.solve(algo, hs.numpy(), ht.numpy(), normalize=True)
+        assert np.array_equal(got.numpy().view(np.uint32), want.view(np.uint32)), algo
+
+
+def test_host_buffers_sharing_pages_and_misaligned(pkg, dev):
+    """src, tar and H carved out of ONE pageable allocation (neighbours share pages, so
+    the registrations must merge), H at a 4-B offset (not 16-B aligned: the generic
+    kernel), and the registration gone afterwards."""
+    n = 30011
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=77)
+    want = pkg.solve("aca", ds, dt, normalize=True).cpu()
+    buf = torch.zeros(n * 8 * 2 + 1 + n * 9, dtype=torch.float32)
+    s = buf[:n * 8].view(n, 8)
+    t = buf[n * 8:n * 16].view(n, 8)
+    h = buf[n * 16 + 1:].view(n, 9)  # 4 B past a 16-B boundary
+    s.copy_(ds.cpu())
+    t.copy_(dt.cpu())
+    pkg.solve_host("aca", s, t, out=h)
+    assert torch.equal(_bits(h), _bits(want))
+    assert torch.equal(_bits(s), _bits(ds.cpu()))  # inputs untouched
+    # unregistered again: a second registration of the same pages succeeds
+    hip = _hip()
+    attrs = ctypes.create_string_buffer(256)
+    rc = hip.hipPointerGetAttributes(attrs, ctypes.c_void_p(buf.data_ptr()))
+    hip.hipGetLastError()
+    assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the call"
+    pkg.solve_host("aca", s, t, out=h)
+    assert torch.equal(_bits(h), _bits(want))
+
+
+def test_host_entry_accepts_device_and_mixed(pkg, dev):
+    n = 5000
+    ds, dt = _inputs(pkg, dev, n, torch.float64, "aos", off=9)
+    want = pkg.solve("sks", ds, dt, normalize=True)
+    lib = pkg.lib()
+    dH = torch.empty_like(want)
+    assert lib.hg_solve_host_f64(1, ds.data_ptr(), dt.data_ptr(), dH.data_ptr(), n, 0, 1, None) == 0
+    assert torch.equal(_bits(dH), _bits(want))
+    hH = torch.empty((n, 9), dtype=torch.float64)  # host H, device inputs
+    assert lib.hg_solve_host_f64(1, ds.data_ptr(), dt.data_ptr(), hH.data_ptr(), n, 0, 1, None) == 0
+    assert torch.equal(_bits(hH), _bits(want.cpu()))
+
+
+def test_host_threads_at_once(pkg, dev):
+    """Eight threads, each its own pageable batch (registrations serialised), plus one
+    pinned caller that never takes the registration lock."""
+    n = 20000
+    jobs = []
+    for k in range(8):
+        ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=k * 1_000_000)
+        jobs.append((ds.cpu(), dt.cpu(), pkg.solve("aca", ds, dt).cpu()))
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=99_000_000)
+    jobs.append((ds.cpu().pin_memory(), dt.cpu().pin_memory(), pkg.solve("aca", ds, dt).cpu()))
+    bad = []
+
+    def work(k):
+        s, t, want = jobs[k]
+        for _ in range(5):
+            got = pkg.solve_host("aca", s, t)
+            if not torch.equal(_bits(got), _bits(want)):
+                bad.append(k)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad
+
+
+def test_host_full_size(pkg, dev):
+    """BASELINE configs[1] size, 10 M problems, from pageable memory."""
+    n = 10_000_000
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos")
+    want = pkg.solve("aca", ds, dt).cpu()
+    got = pkg.solve_host("aca", ds.cpu(), dt.cpu())
+    assert torch.equal(_bits(got), _bits(want))
+
+
+def test_host_entry_errors(pkg, dev):
+    lib = pkg.lib()
+    s = torch.zeros((4, 8))
+    h = torch.zeros((4, 9))
+    assert lib.hg_solve_host_f32(3, s.data_ptr(), s.data_ptr(), h.data_ptr(), 4, 0, 1, None) == 1
+    assert lib.hg_solve_host_f32(0, s.data_ptr(), s.data_ptr(), h.data_ptr(), 4, 3, 1, None) == 1
+    assert lib.hg_solve_host_f32(0, s.data_ptr(), s.data_ptr(), h.data_ptr(), 0, 0, 1, None) == 0
+    with pytest.raises(ValueError):
+        pkg.solve_host("aca", s.cuda(), s.cuda())
