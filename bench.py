@@ -46,6 +46,8 @@ def parse():
                     help="N>1: skip the timed split (scatter) / gather through rank 0")
     ap.add_argument("--gather-deadline", type=float, default=180.0,
                     help="N>1: seconds the split / gather may take before the job ends without it")
+    ap.add_argument("--no-host-shard", action="store_true",
+                    help="skip the shared-memory host-resident batch (per-rank zero-copy)")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
@@ -400,6 +402,50 @@ def host_boundary_section(d: Dist, pkg, n: int):
     return out
 
 
+def host_sharded_section(d: Dist, pkg, src, tar, H, n: int, n_total: int):
+    """The whole n_total-problem batch in HOST memory (one /dev/shm file every rank maps,
+    shard.SharedHostBatch); every rank's GPU reads its block and writes its H rows over its
+    own PCIe link (hg_solve_host_f32, zero-copy): the end-to-end rate of a host-resident
+    batch, with N links working at once and no xGMI traffic.  Each rank fills its block
+    with its own device inputs and checks the H rows it wrote against its device solve."""
+    from importlib import import_module
+    shard = import_module("sks_homography_amd.shard")
+    need = n_total * 100
+    try:
+        st = os.statvfs("/dev/shm")
+        room = st.f_bavail * st.f_frsize
+    except OSError:
+        room = 0
+    if d.max(0.0 if room >= 1.25 * need else 1.0) != 0.0:  # every rank takes the same branch
+        return {"skipped": f"/dev/shm too small for {need} B"}
+    name = f"sks_hg_bench_{os.environ.get('MASTER_PORT', '0')}_{n_total}"
+    try:
+        batch = shard.SharedHostBatch(name, n_total, d.rank, d.barrier)
+    except OSError as e:
+        return {"error": str(e)}
+    try:
+        lo, hi = batch.block(d.world)
+        batch.src[lo:hi].copy_(src)
+        batch.tar[lo:hi].copy_(tar)
+        batch.solve_block(d.world, device=d.dev)  # warm: registration path, clocks
+        ts = []
+        for _ in range(3):
+            d.barrier()
+            t0 = time.perf_counter()
+            batch.solve_block(d.world, device=d.dev)
+            d.barrier()
+            ts.append(d.max(time.perf_counter() - t0))
+        ms = sorted(ts)[1] * 1e3
+        ok = torch.equal(batch.H[lo:hi].view(torch.int32), H.cpu().view(torch.int32))
+        verified = d.max(0.0 if ok else 1.0) == 0.0
+    finally:
+        batch.close()
+    return {"batch": n_total, "ms": round(ms, 3),
+            "M_homographies_per_s": round(n_total / ms / 1e3, 1),
+            "pcie_gbps_per_gpu": round(n * 100 / ms / 1e6, 1), "verified": bool(verified),
+            "note": "shared-memory host batch, per-rank zero-copy over its own PCIe link"}
+
+
 def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     """1M random 4-point hypotheses over the reference's own
     correspondence file (orig_pts_wall.txt, 2540 pairs, committed in tests/golden):
@@ -707,6 +753,10 @@ def main():
                                "G_homographies_per_s": round(n / (ms64 * 1e-3) / 1e9, 2),
                                "achieved_gbps": round(n * 200 / (ms64 * 1e-3) / 1e9, 1)}
         del s64, t64, H64
+        if not args.no_host_shard:
+            run("aca")()  # H = this rank's device result again (the f64 step used other buffers)
+            torch.cuda.synchronize(d.dev)
+            line["host_sharded"] = host_sharded_section(d, pkg, src, tar, H, n, n_total)
 
     if d.world > 1 and not args.no_gather:
         run("aca")()

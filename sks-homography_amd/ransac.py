@@ -121,6 +121,8 @@ def ransac(pool_src: torch.Tensor, pool_tar: torch.Tensor, hypotheses: int, thre
     """Draws ``hypotheses`` random 4-point samples and solves them (one fused launch),
     scores them all and returns the best (ties: lowest index)."""
     _require_device(pool_src, pool_tar)
+    if hypotheses < 1:
+        raise ValueError(f"ransac needs at least one hypothesis, got {hypotheses}")
     H = sample_solve_seeded(pool_src, pool_tar, hypotheses, seed, 0, algo=algo, normalize=True)
     counts = score(H, pool_src, pool_tar, thresh)
     best = int((counts == counts.max()).nonzero()[0].item())

@@ -8,10 +8,17 @@ collectives are the optional split / gather a caller with host- or rank-0-reside
 needs: scatter_blocks hands each rank its block of one rank's batch, gather_blocks
 collects every H block on one rank, both as paired send/recv over RCCL
 (torch.distributed "nccl" == RCCL on ROCm) -- reported separately by bench.py.
+
+A batch that lives in HOST memory needs neither: SharedHostBatch puts src/tar/H in one
+shared-memory file every rank maps, and each rank's GPU reads its block and writes its H
+rows over its own PCIe link (ops.solve_host, zero-copy) -- N links in parallel, no xGMI
+traffic, no rank-0 bottleneck.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+import mmap
+import os
+from typing import Callable, List, Optional, Tuple
 
 import torch
 
@@ -86,3 +93,79 @@ def scatter_blocks(full: Optional[torch.Tensor], n_total: int, world: int, rank:
         for w in dist.batch_isend_irecv([dist.P2POp(dist.irecv, block, src, group)]):
             w.wait()
     return block
+
+
+class SharedHostBatch:
+    """An (n, 8) src, (n, 8) tar and (n, 9) H float32 batch in one shared-memory file
+    (``/dev/shm/<name>``) that every rank of the node maps.  Rank ``owner`` creates it
+    (``posix_fallocate`` reserves the pages up front, so a full /dev/shm fails here with
+    OSError instead of a SIGBUS later), the others attach after ``barrier()``.  Each rank
+    then solves its block with ``solve_block`` (the GPU reads and writes the shared pages
+    directly).  ``close()`` unmaps; the owner also unlinks."""
+
+    def __init__(self, name: str, n: int, rank: int, barrier: Callable[[], None],
+                 owner: int = 0, directory: str = "/dev/shm"):
+        if n < 0:
+            raise ValueError(f"n must be >= 0, got {n}")
+        self.n, self.rank, self.owner = n, rank, owner
+        self.path = os.path.join(directory, name)
+        nbytes = max(n * (8 + 8 + 9) * 4, 4096)
+        self._mm = None
+        err = None
+        if rank == owner:
+            try:
+                fd = os.open(self.path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
+                try:
+                    os.posix_fallocate(fd, 0, nbytes)
+                    self._mm = mmap.mmap(fd, nbytes)
+                finally:
+                    os.close(fd)
+            except OSError as e:  # reported after the barrier, so no peer waits forever
+                err = e
+                try:
+                    os.unlink(self.path)
+                except OSError:
+                    pass
+        barrier()
+        if rank == owner and err is not None:
+            raise err
+        if rank != owner:
+            fd = os.open(self.path, os.O_RDWR)
+            try:
+                if os.fstat(fd).st_size < nbytes:
+                    raise OSError(f"{self.path} holds fewer than {nbytes} bytes")
+                self._mm = mmap.mmap(fd, nbytes)
+            finally:
+                os.close(fd)
+        flat = torch.frombuffer(self._mm, dtype=torch.float32, count=nbytes // 4)
+        self.src = flat[:n * 8].view(n, 8)
+        self.tar = flat[n * 8:n * 16].view(n, 8)
+        self.H = flat[n * 16:n * 25].view(n, 9)
+
+    def block(self, world: int, rank: Optional[int] = None) -> Tuple[int, int]:
+        return shard_range(self.n, world, self.rank if rank is None else rank)
+
+    def solve_block(self, world: int, algo: str = "aca", normalize: bool = True,
+                    device=None) -> Tuple[int, int]:
+        """Solves this rank's block in place (H rows of the shared file); returns it."""
+        from .ops import solve_host
+
+        lo, hi = self.block(world)
+        if hi > lo:
+            solve_host(algo, self.src[lo:hi], self.tar[lo:hi], normalize=normalize,
+                       out=self.H[lo:hi], device=device)
+        return lo, hi
+
+    def close(self) -> None:
+        self.src = self.tar = self.H = None
+        if self._mm is not None:
+            try:
+                self._mm.close()
+            except BufferError:  # a caller still holds a view: leave the mapping to GC
+                pass
+            self._mm = None
+        if self.rank == self.owner:
+            try:
+                os.unlink(self.path)
+            except OSError:
+                pass

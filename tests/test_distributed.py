@@ -90,3 +90,61 @@ def test_scatter_gather_blocks_gloo(world, n_total):
         assert p.exitcode == 0
     assert all(ok for ok, _ in res)
     assert all(m == float(world) for _, m in res)
+
+
+def _shm_worker(rank, world, port, n_total, name, q):
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ge.load_package()
+    from sks_homography_amd.shard import SharedHostBatch
+    b = SharedHostBatch(name, n_total, rank, dist.barrier)
+    lo, hi = b.block(world)
+    # each rank writes its own block (as the GPU writes its H rows), rank 0 reads them all
+    b.src[lo:hi] = torch.arange(lo, hi, dtype=torch.float32).unsqueeze(1)
+    b.H[lo:hi] = float(rank)
+    dist.barrier()
+    ok = True
+    if rank == 0:
+        want = torch.arange(n_total, dtype=torch.float32).unsqueeze(1).expand(n_total, 8)
+        owner = torch.cat([torch.full((pb - pa, 9), float(r)) for r in range(world)
+                           for pa, pb in [b.block(world, r)]])
+        ok = bool(torch.equal(b.src, want)) and bool(torch.equal(b.H, owner))
+    dist.barrier()
+    b.close()
+    dist.barrier()
+    q.put((rank, ok, os.path.exists(os.path.join("/dev/shm", name))))
+    dist.destroy_process_group()
+
+
+def test_shared_host_batch_gloo():
+    """bench.py's host-resident batch: rank 0 creates the /dev/shm file, the others map
+    it, every rank's writes land in the one file, and it is gone after close()."""
+    world, n_total = 3, 1001
+    name = f"sks_hg_test_{os.getpid()}"
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_shm_worker, args=(r, world, port, n_total, name, q))
+             for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    assert all(ok for _, ok, _ in res)
+    assert not os.path.exists(os.path.join("/dev/shm", name))
+
+
+def test_shared_host_batch_full_shm_fails_cleanly(tmp_path):
+    """No room for the file: OSError at creation (posix_fallocate), not a SIGBUS later."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from sks_homography_amd.shard import SharedHostBatch
+    with pytest.raises(OSError):
+        SharedHostBatch("x", 1 << 40, 0, lambda: None, directory=str(tmp_path / "missing"))

@@ -78,6 +78,12 @@ for step in $STEPS; do
             run dist4 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 4 \
                 --master-addr 127.0.0.1 --master-port 29521 bench.py --gpus 4 --steps 10 \
                 --warmup 2 --no-extras --dist-backend gloo ;;
+        dist2_full)
+            # the driver's N>1 command as it runs it (every extra section on), 2 ranks sharing
+            # the one GPU over gloo: all sections keep the ranks in step to the one JSON line
+            run dist2_full 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29525 bench.py --gpus 2 --steps 20 \
+                --warmup 2 --dist-backend gloo ;;
         dist2_deadline)
             # the split / gather watchdog: a deadline too short to meet ends every rank and
             # rank 0 still prints the measured line, with the stall recorded
