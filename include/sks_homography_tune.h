@@ -44,7 +44,11 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
 
 /* cal_ACA's launch loop in native code: `loops` back-to-back C-ABI launches, timed with
- * HIP events on `stream`; returns us per launch or -(hipError_t).  elem 4 / 8 bytes. */
+ * HIP events on `stream`; returns us per launch or -(hipError_t).  elem 4 / 8 bytes.
+ * algo 0 ACA, 1 SKS; launch-floor probes: 2 empty kernel, 3 + hipGetLastError, 4 / 5 / 7
+ * raw SoA f64 ACA kernels, 6 one-dword store, 8-11 one-dword store with sc0 sc1 / sc1 /
+ * sc0 sc1 nt / nt, 12 one load per lane and no store, 13 pointer arguments never read, 14
+ * arguments read and no other memory access. */
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream);
 

@@ -264,6 +264,30 @@ __global__ void empty_kernel() {}
 __global__ void store_one_kernel(uint32_t* p) {
     if (threadIdx.x == 0) p[0] = 1u;
 }
+// The same one-dword store under each cache policy (launch-floor probe: is the ~1.2 us a
+// written kernel costs over an empty one the end-of-kernel L2 writeback of dirty lines?)
+template <int POL>
+__global__ void store_one_policy_kernel(uint32_t* p) {
+    if (threadIdx.x != 0) return;
+    const uint32_t v = 1u;
+    if constexpr (POL == 0)
+        asm volatile("global_store_dword %0, %1, off sc0 sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 1)
+        asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else if constexpr (POL == 2)
+        asm volatile("global_store_dword %0, %1, off sc0 sc1 nt" ::"v"(p), "v"(v) : "memory");
+    else
+        __builtin_nontemporal_store(v, p);
+}
+__global__ void args_unused_kernel(const uint32_t*, uint32_t*) {}
+// reads its kernel arguments (s_load from the kernarg segment) but touches no other memory
+__global__ void args_read_kernel(uint64_t a, uint64_t b) {
+    if (a == b + 12345u) __builtin_amdgcn_s_sleep(1);
+}
+__global__ void load_one_kernel(const uint32_t* p, uint32_t* never) {
+    const uint32_t v = p[threadIdx.x];
+    if (v == 0xdeadbeefu && threadIdx.x == 65) never[0] = v;  // never taken: no store
+}
 // one lane per problem, plain loads/stores (the latency probe's generic form)
 template <int ALGO, bool NORM, typename T, bool SOA>
 __global__ __launch_bounds__(kBlock) void solve_generic_t(const T* __restrict__ src,
@@ -446,11 +470,33 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
 // 1 SKS; elem 4 (float) or 8 (double).
 double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar, void* H,
                            int64_t n, int layout, int flags, int loops, void* stream) {
-    if (algo < 0 || algo > 7 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
+    if (algo < 0 || algo > 14 || (elem != 4 && elem != 8) || loops <= 0) return -1.0;
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     auto launch = [&]() -> int {
         if (algo == 2) {  // the floor: an empty kernel, raw launch, no checks
             empty_kernel<<<1, kWave, 0, st>>>();
+            return 0;
+        }
+        if (algo >= 8 && algo <= 11) {  // one-dword store: sc0 sc1 / sc1 / sc0 sc1 nt / nt
+            auto* h = static_cast<uint32_t*>(H);
+            if (algo == 8) store_one_policy_kernel<0><<<1, kWave, 0, st>>>(h);
+            if (algo == 9) store_one_policy_kernel<1><<<1, kWave, 0, st>>>(h);
+            if (algo == 10) store_one_policy_kernel<2><<<1, kWave, 0, st>>>(h);
+            if (algo == 11) store_one_policy_kernel<3><<<1, kWave, 0, st>>>(h);
+            return 0;
+        }
+        if (algo == 13) {  // pointer arguments, never read
+            args_unused_kernel<<<1, kWave, 0, st>>>(static_cast<const uint32_t*>(src),
+                                                    static_cast<uint32_t*>(H));
+            return 0;
+        }
+        if (algo == 14) {  // arguments read, no other memory access
+            args_read_kernel<<<1, kWave, 0, st>>>((uint64_t)(uintptr_t)src, (uint64_t)n);
+            return 0;
+        }
+        if (algo == 12) {  // one load per lane, no store
+            load_one_kernel<<<1, kWave, 0, st>>>(static_cast<const uint32_t*>(src),
+                                                 static_cast<uint32_t*>(H));
             return 0;
         }
         if (algo == 3) {  // the floor plus the error query every C-ABI call makes

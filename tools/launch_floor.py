@@ -29,6 +29,12 @@ for rep in range(2):
     row["aca1000_raw_nt"] = round(loop(5, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000, 1, 0,
                                        20000, st), 2)
     row["store_one"] = round(loop(6, 8, 0, 0, h.data_ptr(), 0, 1, 0, 20000, st), 2)
+    for algo, name in ((8, "store_one_sc0sc1"), (9, "store_one_sc1"), (10, "store_one_sc0sc1nt"),
+                       (11, "store_one_nt")):
+        row[name] = round(loop(algo, 8, 0, 0, h.data_ptr(), 0, 1, 0, 20000, st), 2)
+    row["load_one"] = round(loop(12, 8, a.data_ptr(), 0, h.data_ptr(), 0, 1, 0, 20000, st), 2)
+    row["args_unused"] = round(loop(13, 8, a.data_ptr(), 0, h.data_ptr(), 0, 1, 0, 20000, st), 2)
+    row["args_read"] = round(loop(14, 8, a.data_ptr(), 0, h.data_ptr(), 7, 1, 0, 20000, st), 2)
     row["aca1000_generic_raw"] = round(loop(7, 8, a.data_ptr(), a.data_ptr(), h.data_ptr(), 1000,
                                             1, 0, 20000, st), 2)
     for n in (1, 2, 3, 4, 10, 1000):
@@ -43,4 +49,5 @@ for rep in range(2):
         h = torch.empty(n, 9, device=dev)
         row[f"aos_f32_aca{n}"] = round(loop(0, 4, a.data_ptr(), a.data_ptr(), h.data_ptr(), n, 0, 1,
                                             20000, st), 2)
+    row["HIP_FORCE_DEV_KERNARG"] = os.environ.get("HIP_FORCE_DEV_KERNARG")
     print(row, flush=True)
