@@ -419,10 +419,15 @@ def host_sharded_section(d: Dist, pkg, src, tar, H, n: int, n_total: int):
     if d.max(0.0 if room >= 1.25 * need else 1.0) != 0.0:  # every rank takes the same branch
         return {"skipped": f"/dev/shm too small for {need} B"}
     name = f"sks_hg_bench_{os.environ.get('MASTER_PORT', '0')}_{n_total}"
+    batch, err = None, None
     try:
         batch = shard.SharedHostBatch(name, n_total, d.rank, d.barrier)
     except OSError as e:
-        return {"error": str(e)}
+        err = str(e)
+    if d.max(0.0 if batch is not None else 1.0) != 0.0:  # all ranks leave together
+        if batch is not None:
+            batch.close()
+        return {"error": err or "another rank could not map the shared batch"}
     try:
         lo, hi = batch.block(d.world)
         batch.src[lo:hi].copy_(src)
