@@ -84,6 +84,12 @@ for step in $STEPS; do
             run dist2_full 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29525 bench.py --gpus 2 --steps 20 \
                 --warmup 2 --dist-backend gloo ;;
+        dist2_fail)
+            # the extras guard: rank 1 fails as the extras start; rank 0 must still print the
+            # headline line (with extras_error) -- directly or through the extras watchdog
+            run dist2_fail 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+                --master-addr 127.0.0.1 --master-port 29527 bench.py --gpus 2 --steps 20 \
+                --warmup 2 --dist-backend gloo --inject-extras-failure 1 --extras-deadline 60 ;;
         dist2_deadline)
             # the split / gather watchdog: a deadline too short to meet ends every rank and
             # rank 0 still prints the measured line, with the stall recorded
