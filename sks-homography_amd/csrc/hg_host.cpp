@@ -24,6 +24,7 @@ struct View {
     const void* host = nullptr;  // the caller's pointer
     size_t bytes = 0;
     void* dev = nullptr;         // device address once known
+    bool in_host = true;         // host memory (pinned or pageable), read over PCIe
 };
 
 // Device address of [p, p + bytes) if the whole range is device-visible, nullptr if it is
@@ -56,6 +57,7 @@ int classify(View& v) {
         v.dev = da;
     } else {
         v.dev = const_cast<void*>(v.host);  // device or managed memory: use as is
+        v.in_host = false;
     }
     return 0;
 }
@@ -106,30 +108,36 @@ std::mutex& registration_mutex() {
     return mu;
 }
 
+// The solvers with the host-memory cache policy (hg_kernels.hip, library-internal).
+extern "C" int hg_internal_solve_host_f32(int, const float*, const float*, float*, int64_t, int,
+                                          int, void*);
+extern "C" int hg_internal_solve_host_f64(int, const double*, const double*, double*, int64_t,
+                                          int, int, void*);
+
 template <typename T>
 int launch(int algo, const T* s, const T* t, T* h, int64_t n, int layout, int flags,
-           void* stream);
-
-template <>
-int launch<float>(int algo, const float* s, const float* t, float* h, int64_t n, int layout,
-                  int flags, void* stream) {
-    switch (algo) {
-        case HG_ALGO_ACA: return hg_aca_f32(s, t, h, n, layout, flags, stream);
-        case HG_ALGO_SKS: return hg_sks_f32(s, t, h, n, layout, flags, stream);
-        case HG_ALGO_GE: return hg_ge_f32(s, t, h, n, layout, flags, stream);
-        default: return kInvalid;
+           void* stream, bool host) {
+    if (host) {  // any buffer in host memory: the host-memory cache policy
+        if constexpr (sizeof(T) == 4)
+            return hg_internal_solve_host_f32(algo, s, t, h, n, layout, flags, stream);
+        else
+            return hg_internal_solve_host_f64(algo, s, t, h, n, layout, flags, stream);
     }
-}
-
-template <>
-int launch<double>(int algo, const double* s, const double* t, double* h, int64_t n,
-                   int layout, int flags, void* stream) {
-    switch (algo) {
-        case HG_ALGO_ACA: return hg_aca_f64(s, t, h, n, layout, flags, stream);
-        case HG_ALGO_SKS: return hg_sks_f64(s, t, h, n, layout, flags, stream);
-        case HG_ALGO_GE: return hg_ge_f64(s, t, h, n, layout, flags, stream);
-        case HG_ALGO_GPT: return hg_gpt_f64(s, t, h, n, layout, flags, stream);
-        default: return kInvalid;
+    if constexpr (sizeof(T) == 4) {  // all in device memory: the ordinary entry points
+        switch (algo) {
+            case HG_ALGO_ACA: return hg_aca_f32(s, t, h, n, layout, flags, stream);
+            case HG_ALGO_SKS: return hg_sks_f32(s, t, h, n, layout, flags, stream);
+            case HG_ALGO_GE: return hg_ge_f32(s, t, h, n, layout, flags, stream);
+            default: return kInvalid;
+        }
+    } else {
+        switch (algo) {
+            case HG_ALGO_ACA: return hg_aca_f64(s, t, h, n, layout, flags, stream);
+            case HG_ALGO_SKS: return hg_sks_f64(s, t, h, n, layout, flags, stream);
+            case HG_ALGO_GE: return hg_ge_f64(s, t, h, n, layout, flags, stream);
+            case HG_ALGO_GPT: return hg_gpt_f64(s, t, h, n, layout, flags, stream);
+            default: return kInvalid;
+        }
     }
 }
 
@@ -152,11 +160,7 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
         if (rc) return rc;
         if (!x.dev) pageable.push_back(&x);
     }
-    const bool all_device = pageable.empty() && [&] {
-        for (View& x : v)
-            if (x.dev != x.host) return false;
-        return true;
-    }();
+    const bool all_device = !v[0].in_host && !v[1].in_host && !v[2].in_host;
     // Device-resident data may come from work queued on the legacy default stream, so
     // with no stream given it is solved there (a private stream would race it); host
     // data has no such producer and goes on the calling thread's own default stream.
@@ -164,7 +168,7 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
     if (!s && !all_device) s = hipStreamPerThread;
     auto run = [&]() -> int {
         int rc = launch<T>(algo, static_cast<const T*>(v[0].dev), static_cast<const T*>(v[1].dev),
-                           static_cast<T*>(v[2].dev), n, layout, flags, s);
+                           static_cast<T*>(v[2].dev), n, layout, flags, s, !all_device);
         const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
         return rc ? rc : (int)e;
     };

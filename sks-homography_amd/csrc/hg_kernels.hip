@@ -183,9 +183,14 @@ inline unsigned generic_grid(int64_t n) {
 
 inline int launch_status() { return (int)hipGetLastError(); }
 
+// host = the buffers are host memory read and written over PCIe (hg_solve_host_*): the
+// non-temporal hints are about HBM / MALL residency and buy nothing there, so host batches
+// take the default policy -- which also keeps their 12 ms launches apart from the
+// headline's in kernel traces.
 template <int ALGO, bool NORM, typename T>
-int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipStream_t s) {
-    const bool cached = n <= kMallResidentBytes / (25 * (int64_t)sizeof(T));  // 25 values/problem
+int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipStream_t s,
+                  bool host = false) {
+    const bool cached = host || n <= kMallResidentBytes / (25 * (int64_t)sizeof(T));  // 25 values/problem
     if (layout == HG_LAYOUT_SOA) {
         constexpr int V = 16 / sizeof(T);
         if (sizeof(T) == 8 && cached && n >= kSoaWideMinN && n % V == 0 && aligned16(src) &&
@@ -221,15 +226,16 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
 }
 
 template <int ALGO, typename T>
-int dispatch(const T* src, const T* tar, T* H, int64_t n, int layout, int flags, void* stream) {
+int dispatch(const T* src, const T* tar, T* H, int64_t n, int layout, int flags, void* stream,
+             bool host = false) {
     if (n < 0) return kErrInvalid;
     if (layout != HG_LAYOUT_AOS && layout != HG_LAYOUT_SOA) return kErrInvalid;
     if (flags & ~HG_FLAG_NORMALIZE) return kErrInvalid;
     if (n == 0) return 0;
     if (!src || !tar || !H) return kErrInvalid;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    if (flags & HG_FLAG_NORMALIZE) return launch_solver<ALGO, true>(src, tar, H, n, layout, s);
-    return launch_solver<ALGO, false>(src, tar, H, n, layout, s);
+    if (flags & HG_FLAG_NORMALIZE) return launch_solver<ALGO, true>(src, tar, H, n, layout, s, host);
+    return launch_solver<ALGO, false>(src, tar, H, n, layout, s, host);
 }
 
 // The square specialisation (ACA_rect.m:28) is taken only where the ratio is known on
@@ -326,6 +332,29 @@ int hg_ge_f64(const double* src, const double* tar, double* H, int64_t n, int la
 int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
                int flags, void* stream) {
     return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream);
+}
+
+// Library-internal (not in the public header): the solvers for buffers in host memory,
+// reached from hg_solve_host_* (hg_host.cpp) with device-visible addresses.
+int hg_internal_solve_host_f32(int algo, const float* src, const float* tar, float* H,
+                               int64_t n, int layout, int flags, void* stream) {
+    switch (algo) {
+        case HG_ALGO_ACA: return hg::dispatch<hg::kACA>(src, tar, H, n, layout, flags, stream, true);
+        case HG_ALGO_SKS: return hg::dispatch<hg::kSKS>(src, tar, H, n, layout, flags, stream, true);
+        case HG_ALGO_GE: return hg::dispatch<hg::kGE>(src, tar, H, n, layout, flags, stream, true);
+        default: return hg::kErrInvalid;
+    }
+}
+
+int hg_internal_solve_host_f64(int algo, const double* src, const double* tar, double* H,
+                               int64_t n, int layout, int flags, void* stream) {
+    switch (algo) {
+        case HG_ALGO_ACA: return hg::dispatch<hg::kACA>(src, tar, H, n, layout, flags, stream, true);
+        case HG_ALGO_SKS: return hg::dispatch<hg::kSKS>(src, tar, H, n, layout, flags, stream, true);
+        case HG_ALGO_GE: return hg::dispatch<hg::kGE>(src, tar, H, n, layout, flags, stream, true);
+        case HG_ALGO_GPT: return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream, true);
+        default: return hg::kErrInvalid;
+    }
 }
 
 int hg_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
