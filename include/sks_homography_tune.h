@@ -61,9 +61,11 @@ int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void*
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
                     int64_t pitch_bytes, void* stream);
 
-/* Seeded fused sampler, (P, waves per block): 0 shipped (2, 8), 1 (2, 4), 2 (1, 16), 3 (2, 16),
- * 4 shipped shape with the 64-bit remainder, 5 / 6 one hash per draw (a different stream) at
- * (2, 4) / (2, 8). */
+/* Seeded fused sampler, (P, waves per block[, draws in place]): 0 shipped (1, 16, in place),
+ * 1 (2, 4), 2 (1, 16), 3 (2, 16), 4 (2, 8) with the 64-bit remainder, 5 / 6 one hash per draw
+ * (a different stream) at (2, 4) / (2, 8), 7 (2, 8, in place), 8 (2, 4, in place), 9 (2, 8)
+ * -- the previous shipped form.  "In place": each tile's draws made where they are used
+ * rather than one tile ahead. */
 int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
                           uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
                           int algo, int flags, void* stream);

@@ -221,17 +221,21 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int64_t p = tile * kTile + j * kWave + lane;
-            r[j] = p < n ? draws4<DRAWS>(idx, bits_base, bits_odd != 0, p) : u32x4{0, 0, 0, 0};
+            // generated draws need no bound: past n they feed rows that are never stored
+            r[j] = (DRAWS != kDrawsIndexed || p < n) ? draws4<DRAWS>(idx, bits_base, bits_odd != 0, p)
+                                                     : u32x4{0, 0, 0, 0};
         }
     };
-    // index rows of the next PF tiles stay in flight while this tile is solved
-    static_assert(PF == 1 || PF == 2, "prefetch depth 1 or 2");
+    // index rows of the next PF tiles stay in flight while this tile is solved; PF = 0
+    // makes each tile's draws where they are used (nothing to hide when they are computed)
+    static_assert(PF >= 0 && PF <= 2, "prefetch depth 0, 1 or 2");
     u32x4 cur[P], ahead[P]{};
-    if (t < tiles) load(t, cur);
+    if (PF > 0 && t < tiles) load(t, cur);
     if (PF == 2 && t + stride < tiles) load(t + stride, ahead);
     for (; t < tiles; t += stride) {
         u32x4 nxt[P]{};
-        if (t + PF * stride < tiles) load(t + PF * stride, nxt);
+        if constexpr (PF == 0) load(t, cur);
+        else if (t + PF * stride < tiles) load(t + PF * stride, nxt);
         float h[P][9];
 #pragma unroll
         for (int j = 0; j < P; ++j) {
@@ -266,7 +270,7 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
             if constexpr (PF == 2) {
                 cur[j] = ahead[j];
                 ahead[j] = nxt[j];
-            } else {
+            } else if constexpr (PF == 1) {
                 cur[j] = nxt[j];
             }
         }
@@ -538,12 +542,14 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
     return (int)hipGetLastError();
 }
 
-// The seeded sampler's launcher.  Shipped shape: the LDS-pool kernel with P = 2 and 8 waves
-// per block (the pool copy shared by twice the waves; LDS opt-in past 64 KiB) while the
-// pool plus staging fit the CU's 160 KiB, else the global-gather form.  The draws are made
-// in the kernel from word `offset` of stream seed * kBitsMul (draws4).  P, WPB, DRAWS and
-// MOD64 are open for the variant sweep (hg_tune_sample_seeded).
-template <int P = 2, int WPB = 8, int DRAWS = kDrawsPaired, bool MOD64 = false>
+// The seeded sampler's launcher.  Shipped shape: the LDS-pool kernel with P = 1 and 16 waves
+// per block (the pool copy shared by 16 waves; LDS opt-in past 64 KiB; 2 blocks = 32 waves
+// per CU), each tile's draws made where they are used (PF = 0: nothing to hide when the
+// draws are computed), while the pool plus staging fit the CU's 160 KiB, else the
+// global-gather form.  The draws are made in the kernel from word `offset` of stream
+// seed * kBitsMul (draws4).  P, WPB, DRAWS, MOD64 and PF are open for the variant sweep
+// (hg_tune_sample_seeded).
+template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
                                 bool norm, hipStream_t s) {
@@ -574,7 +580,7 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     const uint64_t magic = MOD64 ? fastmod64_magic(npool) : fastmod_magic(npool);
 #define HG_SD(A, N)                                                                         \
     do {                                                                                    \
-        auto k = sample_solve_lds_kernel<A, N, P, 1, WPB, DRAWS, MOD64>;                    \
+        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64>;                   \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
         k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, nullptr, H, n, bits_base, odd); \
     } while (0)

@@ -607,13 +607,16 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     using namespace hg;
     switch (variant) {
-        case 0: return launch_sample_seeded<2, 8>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 1: return launch_sample_seeded<2, 4>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 2: return launch_sample_seeded<1, 16>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 3: return launch_sample_seeded<2, 16>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 4: return launch_sample_seeded<2, 8, kDrawsPaired, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 5: return launch_sample_seeded<2, 4, kDrawsSingle>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 6: return launch_sample_seeded<2, 8, kDrawsSingle>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 0: return launch_sample_seeded<>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 1: return launch_sample_seeded<2, 4, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 2: return launch_sample_seeded<1, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 3: return launch_sample_seeded<2, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 4: return launch_sample_seeded<2, 8, kDrawsPaired, true, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 5: return launch_sample_seeded<2, 4, kDrawsSingle, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 6: return launch_sample_seeded<2, 8, kDrawsSingle, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 7: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 8: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 9: return launch_sample_seeded<2, 8, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

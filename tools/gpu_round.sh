@@ -66,6 +66,7 @@ for step in $STEPS; do
         op_overhead) run op_overhead 300 python tools/op_overhead.py ;;
         kbench_rect) run kbench_rect 300 python tools/kbench_rect.py ;;
         kbench_sample) run kbench_sample 300 python tools/kbench_sample.py ;;
+        kbench_seeded) KB_SEEDED_ONLY=1 run kbench_seeded 300 python tools/kbench_sample.py ;;
         kbench_soa_small) run kbench_soa_small 300 python tools/kbench_soa_small.py ;;
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
         kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;

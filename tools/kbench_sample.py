@@ -21,10 +21,14 @@ import __graft_entry__ as ge  # noqa: E402
 NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2", 3: "LDS pool P2 prefetch 2",
          4: "LDS pool P1, 8 waves/block", 5: "LDS pool P1, 16 waves/block",
          6: "LDS pool P2, 16 waves/block", 7: "LDS pool P2, 64-bit remainder"}
-SEEDED = {0: "seeded P2, 8 waves/block (shipped)", 1: "seeded P2, 4 waves/block",
+SEEDED = {0: "seeded P1, 16 waves/block, draws in place (shipped)", 1: "seeded P2, 4 waves/block",
           2: "seeded P1, 16 waves/block", 3: "seeded P2, 16 waves/block",
           4: "seeded P2, 8 waves/block, 64-bit remainder",
-          5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw"}
+          5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw",
+          7: "seeded P2, 8 waves/block, draws in place", 8: "seeded P2, 4 waves/block, draws in place",
+          9: "seeded P2, 8 waves/block (previous shipped)"}
+# KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
+SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
 OTHER_STREAM = (5, 6)  # one hash per draw: a different stream, not comparable bit for bit
 
 
@@ -45,9 +49,9 @@ def main():
     pt = torch.from_numpy(g["pool_tar"]).to(dev)
     npool = ps.shape[0]
     out = {}
-    for n in (1 << 20, 1 << 22, 1 << 24):
+    for n in ((1 << 22, 1 << 24) if SEEDED_ONLY else (1 << 20, 1 << 22, 1 << 24)):
         idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
-        keys = list(NAMES) + [("s", v) for v in SEEDED]
+        keys = ([0] if SEEDED_ONLY else list(NAMES)) + [("s", v) for v in SEEDED]
         outs = {v: torch.empty((n, 9), device=dev) for v in keys}
         st = torch.cuda.current_stream(dev).cuda_stream
 
