@@ -5,9 +5,10 @@
 // output semantics (normalised H, H[8] == 1, bit-identical values).  The pointers
 // may be host memory -- the reference's one-call-per-homography use in
 // CPU_Runtime Test/main.cpp:87-114: the 16 values ride in the kernel launch
-// (hg_solve_one_*) and H comes back through per-thread mapped host memory on a
-// per-thread stream -- or device memory (solved in place, on the legacy default
-// stream).  The call is synchronous, as the reference's is, and thread-safe.
+// and H comes back through per-thread mapped host memory on a per-thread stream, the
+// thread spinning on a completion word the kernel writes after H (~9 us per call) -- or
+// device memory (solved in place, on the legacy default stream).  The call is
+// synchronous, as the reference's is, and thread-safe.
 // Returns 0 on success (the reference always returns 0, ACA_SKS.cpp:101), or the
 // hipError_t of a failed copy/launch.
 //

@@ -85,6 +85,21 @@ __global__ __launch_bounds__(kWave) void solve_one_kernel(Quad<T> q, T* __restri
     for (int k = 0; k < 9; ++k) H[k] = h[k];
 }
 
+// The same, then a completion word: H first, a system-scope fence, then *done = seq, so a
+// host thread that sees seq in mapped memory also sees all of H (the sks:: host-pointer
+// calls spin on it instead of waiting for the stream: hg_sks_api.cpp).
+template <int ALGO, bool NORM, typename T>
+__global__ __launch_bounds__(kWave) void solve_one_signal_kernel(Quad<T> q, T* __restrict__ H,
+                                                                 uint32_t* done, uint32_t seq) {
+    if (threadIdx.x != 0) return;
+    T h[9];
+    solve<ALGO, NORM>(q.src, q.tar, h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H[k] = h[k];
+    __threadfence_system();
+    __hip_atomic_store(done, seq, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // Deterministic row sums, in place (hg_sum_rows_f32).  Pass 1: block (c, r) sums chunk c
 // = x[r][c*kSumChunk, (c+1)*kSumChunk) -- thread t adds elements c*kSumChunk + t + 256 i,
 // i = 0, 1, ... in order (out-of-range elements count as +0), then the 256 sums fold by
@@ -272,7 +287,8 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
 }
 
 template <typename T>
-int launch_one(int algo, const T* src, const T* tar, T* H, int flags, void* stream) {
+int launch_one(int algo, const T* src, const T* tar, T* H, int flags, void* stream,
+               uint32_t* done = nullptr, uint32_t seq = 0) {
     if (!src || !tar || !H || (flags & ~HG_FLAG_NORMALIZE)) return kErrInvalid;
     if (algo != kACA && algo != kSKS) return kErrInvalid;
     Quad<T> q;
@@ -282,13 +298,17 @@ int launch_one(int algo, const T* src, const T* tar, T* H, int flags, void* stre
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool norm = flags & HG_FLAG_NORMALIZE;
+#define HG_ONE(A, N)                                                                  \
+    do {                                                                              \
+        if (done) solve_one_signal_kernel<A, N, T><<<1, kWave, 0, s>>>(q, H, done, seq); \
+        else solve_one_kernel<A, N, T><<<1, kWave, 0, s>>>(q, H);                     \
+    } while (0)
     if (algo == kACA) {
-        if (norm) solve_one_kernel<kACA, true, T><<<1, kWave, 0, s>>>(q, H);
-        else solve_one_kernel<kACA, false, T><<<1, kWave, 0, s>>>(q, H);
+        if (norm) HG_ONE(kACA, true); else HG_ONE(kACA, false);
     } else {
-        if (norm) solve_one_kernel<kSKS, true, T><<<1, kWave, 0, s>>>(q, H);
-        else solve_one_kernel<kSKS, false, T><<<1, kWave, 0, s>>>(q, H);
+        if (norm) HG_ONE(kSKS, true); else HG_ONE(kSKS, false);
     }
+#undef HG_ONE
     return launch_status();
 }
 
@@ -332,6 +352,18 @@ int hg_ge_f64(const double* src, const double* tar, double* H, int64_t n, int la
 int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
                int flags, void* stream) {
     return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream);
+}
+
+// Library-internal: the single-problem launch with a completion word (hg_sks_api.cpp).
+int hg_internal_solve_one_signal_f32(int algo, const float* src, const float* tar, float* H,
+                                     int flags, uint32_t* done, uint32_t seq, void* stream) {
+    if (!done) return hg::kErrInvalid;
+    return hg::launch_one(algo, src, tar, H, flags, stream, done, seq);
+}
+int hg_internal_solve_one_signal_f64(int algo, const double* src, const double* tar, double* H,
+                                     int flags, uint32_t* done, uint32_t seq, void* stream) {
+    if (!done) return hg::kErrInvalid;
+    return hg::launch_one(algo, src, tar, H, flags, stream, done, seq);
 }
 
 // Library-internal (not in the public header): the solvers for buffers in host memory,

@@ -2,9 +2,16 @@
 // of the C ABI.  Every call goes to the GPU; there is no CPU solver in the product.
 #include <hip/hip_runtime_api.h>
 
+#include <chrono>
 #include <cstring>
 
 #include "sks_aca_sks.hpp"
+
+// Library-internal (hg_kernels.hip): one problem, then *done = seq after H (system scope).
+extern "C" int hg_internal_solve_one_signal_f32(int, const float*, const float*, float*, int,
+                                                uint32_t*, uint32_t, void*);
+extern "C" int hg_internal_solve_one_signal_f64(int, const double*, const double*, double*, int,
+                                                uint32_t*, uint32_t, void*);
 
 namespace {
 
@@ -18,17 +25,23 @@ bool is_device_pointer(const void* p) {
 }
 
 // Per-thread state for host-pointer calls: a non-blocking stream (threads never
-// serialise on the legacy default stream) and 9 values of host memory mapped into the
-// device address space, which the kernel writes directly.  The points go in the kernel
-// arguments (hg_solve_one_*), so a call is one launch + one stream synchronisation.
-// One slot per device the thread has used; released when the thread exits.
+// serialise on the legacy default stream) and host memory mapped into the device address
+// space -- 16 values for H plus a completion word -- which the kernel writes directly.
+// The points go in the kernel arguments, so a call is one launch, and the thread then
+// spins on the completion word (the kernel stores it after H, system scope) instead of
+// waiting on the stream: ~half the latency of a stream synchronisation.  One slot per
+// device the thread has used; released when the thread exits.
 template <typename T>
 struct Scratch {
     static constexpr int kMaxDevices = 64;
+    static constexpr size_t kDoneOffset = 16 * sizeof(T);  // the completion word, after H
     struct Slot {
         T* host = nullptr;
         T* mapped = nullptr;
         hipStream_t stream = nullptr;
+        uint32_t seq = 0;
+        volatile uint32_t* done_host() { return reinterpret_cast<volatile uint32_t*>(reinterpret_cast<char*>(host) + kDoneOffset); }
+        uint32_t* done_dev() { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(mapped) + kDoneOffset); }
     };
     Slot slot[kMaxDevices];
     Slot* cur = nullptr;
@@ -43,9 +56,12 @@ struct Scratch {
         if (sl.mapped) return 0;
         if (!sl.stream && (e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking)) != hipSuccess)
             return (int)e;
-        if (!sl.host && (e = hipHostMalloc(reinterpret_cast<void**>(&sl.host), 16 * sizeof(T),
-                                           hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
-            return (int)e;
+        if (!sl.host) {
+            if ((e = hipHostMalloc(reinterpret_cast<void**>(&sl.host), kDoneOffset + 64,
+                                   hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
+                return (int)e;
+            *sl.done_host() = 0;
+        }
         if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.mapped), sl.host, 0)) !=
             hipSuccess)
             return (int)e;
@@ -68,7 +84,24 @@ Scratch<T>& scratch() {
 template <typename T>
 using BatchFn = int (*)(const T*, const T*, T*, int64_t, int, int, void*);
 template <typename T>
-using OneFn = int (*)(int, const T*, const T*, T*, int, void*);
+using OneFn = int (*)(int, const T*, const T*, T*, int, uint32_t*, uint32_t, void*);
+
+// Waits until the kernel has published H (*done == seq): a spin with pause, bounded; past
+// the bound (a fault, a stalled device) the stream's own status decides.
+template <typename T>
+int wait_done(typename Scratch<T>::Slot& sl, uint32_t seq) {
+    auto seen = [&] { return __atomic_load_n(sl.done_host(), __ATOMIC_ACQUIRE) == seq; };
+    const auto t0 = std::chrono::steady_clock::now();
+    for (uint32_t i = 0; !seen(); ++i) {
+        __builtin_ia32_pause();
+        if ((i & 1023) == 1023 && std::chrono::steady_clock::now() - t0 > std::chrono::milliseconds(200)) {
+            const hipError_t e = hipStreamSynchronize(sl.stream);
+            if (e != hipSuccess) return (int)e;
+            return seen() ? 0 : (int)hipErrorUnknown;
+        }
+    }
+    return 0;
+}
 
 template <typename T, BatchFn<T> F, OneFn<T> ONE, int ALGO>
 int solve_one(T* src, T* tar, T* result) {
@@ -85,19 +118,20 @@ int solve_one(T* src, T* tar, T* result) {
     Scratch<T>& s = scratch<T>();
     int rc = s.ensure();
     if (rc) return rc;
+    auto& sl = *s.cur;
+    const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;  // never 0, the word's initial value
     if (ds || dt) {
         // mixed: stage device-resident inputs to the host first (rare)
         T in[16];
         hipError_t e = hipMemcpy(in, src, 8 * sizeof(T), hipMemcpyDefault);
         if (e == hipSuccess) e = hipMemcpy(in + 8, tar, 8 * sizeof(T), hipMemcpyDefault);
         if (e != hipSuccess) return (int)e;
-        rc = ONE(ALGO, in, in + 8, s.cur->mapped, HG_FLAG_NORMALIZE, s.cur->stream);
+        rc = ONE(ALGO, in, in + 8, sl.mapped, HG_FLAG_NORMALIZE, sl.done_dev(), seq, sl.stream);
     } else {
-        rc = ONE(ALGO, src, tar, s.cur->mapped, HG_FLAG_NORMALIZE, s.cur->stream);
+        rc = ONE(ALGO, src, tar, sl.mapped, HG_FLAG_NORMALIZE, sl.done_dev(), seq, sl.stream);
     }
     if (rc) return rc;
-    hipError_t e = hipStreamSynchronize(s.cur->stream);
-    if (e != hipSuccess) return (int)e;
+    if ((rc = wait_done<T>(sl, seq))) return rc;
     if (dr) return (int)hipMemcpy(result, s.cur->host, 9 * sizeof(T), hipMemcpyHostToDevice);
     std::memcpy(result, s.cur->host, 9 * sizeof(T));
     return 0;
@@ -137,16 +171,16 @@ int solve_batch(BatchFn<T> dev, int algo, const T* src, const T* tar, T* result,
 namespace sks {
 
 int runKernel_ACA(float* src, float* tar, float* result) {
-    return solve_one<float, hg_aca_f32, hg_solve_one_f32, 0>(src, tar, result);
+    return solve_one<float, hg_aca_f32, hg_internal_solve_one_signal_f32, 0>(src, tar, result);
 }
 int runKernel_ACA_double(double* src, double* tar, double* result) {
-    return solve_one<double, hg_aca_f64, hg_solve_one_f64, 0>(src, tar, result);
+    return solve_one<double, hg_aca_f64, hg_internal_solve_one_signal_f64, 0>(src, tar, result);
 }
 int runKernel_SKS(float* src, float* tar, float* result) {
-    return solve_one<float, hg_sks_f32, hg_solve_one_f32, 1>(src, tar, result);
+    return solve_one<float, hg_sks_f32, hg_internal_solve_one_signal_f32, 1>(src, tar, result);
 }
 int runKernel_SKS_double(double* src, double* tar, double* result) {
-    return solve_one<double, hg_sks_f64, hg_solve_one_f64, 1>(src, tar, result);
+    return solve_one<double, hg_sks_f64, hg_internal_solve_one_signal_f64, 1>(src, tar, result);
 }
 
 int runKernel_ACA_batch(const float* src, const float* tar, float* result, int64_t n,
