@@ -75,6 +75,7 @@ for step in $STEPS; do
         soa_streams) run soa_streams 300 python tools/soa_streams.py ;;
         hbm_policy) run hbm_policy 300 python tools/hbm_policy.py ;;
         host_probe) run host_probe 300 python tools/host_probe.py ;;
+        numa_probe) run numa_probe 300 python tools/numa_probe.py ;;
         dist2)
             # rehearse the N>1 control path (barriers, max-over-ranks, one JSON line) with
             # 2 ranks sharing the one GPU over gloo; the real N>1 run uses RCCL
