@@ -4,6 +4,7 @@ layouts, buffers cut from one allocation (sharing pages), misaligned views, thre
 once -- each bit-identical to the device-resident solve, which tests/test_gpu_parity.py
 pins to the oracle; a small batch is also checked against the oracle directly."""
 import ctypes
+import os
 import threading
 
 import numpy as np
@@ -147,3 +148,43 @@ def test_host_entry_errors(pkg, dev):
     assert lib.hg_solve_host_f32(0, s.data_ptr(), s.data_ptr(), h.data_ptr(), 0, 0, 1, None) == 0
     with pytest.raises(ValueError):
         pkg.solve_host("aca", s.cuda(), s.cuda())
+
+
+def test_ctypes_numpy_binding_as_documented(pkg, dev):
+    """INTEGRATION.md section 4's plain-ctypes binding on numpy arrays (pageable memory)."""
+    lib = pkg.lib()
+    n = 12345
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=321)
+    want = pkg.solve("aca", ds, dt).cpu().numpy()
+    src = np.ascontiguousarray(ds.cpu().numpy(), np.float32)
+    tar = np.ascontiguousarray(dt.cpu().numpy(), np.float32)
+    H = np.empty((len(src), 9), np.float32)
+    rc = lib.hg_solve_host_f32(0, src.ctypes.data, tar.ctypes.data, H.ctypes.data, len(src), 0, 1, None)
+    assert rc == 0
+    assert np.array_equal(H.view(np.uint32), want.view(np.uint32))
+
+
+def test_shared_host_batch_solve_block(pkg, dev):
+    """shard.SharedHostBatch in one process (world 1 and a 3-way split solved block by
+    block): the GPU reads and writes the /dev/shm pages, bits equal the device solve."""
+    from sks_homography_amd.shard import SharedHostBatch
+    n = 50001
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=777)
+    want = pkg.solve("aca", ds, dt).cpu()
+    b = SharedHostBatch(f"sks_hg_gpu_test_{os.getpid()}", n, 0, lambda: None)
+    try:
+        b.src.copy_(ds.cpu())
+        b.tar.copy_(dt.cpu())
+        assert b.solve_block(1) == (0, n)
+        assert torch.equal(b.H.view(torch.int32), want.view(torch.int32))
+        b.H.zero_()
+        for r in range(3):  # what three ranks would each do for their own rows
+            b.rank = r
+            lo, hi = b.solve_block(3)
+            assert (lo, hi) == pkg.shard_range(n, 3, r)
+        b.rank = 0
+        assert torch.equal(b.H.view(torch.int32), want.view(torch.int32))
+    finally:
+        b.rank = 0
+        b.close()
+    assert not os.path.exists(f"/dev/shm/sks_hg_gpu_test_{os.getpid()}")
