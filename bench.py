@@ -237,6 +237,17 @@ def cpu_baseline(n_sample: int):
         reps = max(1, int(0.5 / max(t1, 1e-6)))
         sweep[str(t_count)] = round(n_sample * reps / engine.time_batch(
             "aca", src, tar, H, t_count, reps) / 1e6, 1)
+    native = None
+    if kind == "reference" and os.path.exists(orc.REF_NATIVE_SO) and orc.cpu_has_avx512():
+        # the reference built for speed (not bit-exact): a stronger CPU yardstick beside the
+        # bit-exact one; the GPU is never compared with anything but both
+        fast = orc.RefOracle(orc.REF_NATIVE_SO)
+        native = {"flags": "g++ -O3 -march=x86-64-v4 -ffp-contract=fast -flto (not bit-exact)"}
+        for algo in ("aca", "sks"):
+            t1 = fast.time_batch(algo, src, tar, H, threads, 1)
+            reps = max(1, int(1.0 / max(t1, 1e-6)))
+            native[algo + "_value"] = round(
+                n_sample * reps / fast.time_batch(algo, src, tar, H, threads, reps) / 1e6, 1)
     single = {}
     if kind == "reference":
         # the reference's own CPU methodology (main.cpp:87-92): one set, 10 M calls
@@ -249,6 +260,7 @@ def cpu_baseline(n_sample: int):
                    f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, {threads} std::threads"),
         "single_core_same_points_us_per_H": single or None,
         "aca_thread_sweep_M_per_s": sweep,
+        "native_march": native,
         "host": host_info(),
     }
 
@@ -838,6 +850,9 @@ def main():
             # the speed-up is quoted against the multi-threaded host baseline
             line["cpu_baseline"]["gpu_speedup"] = round(
                 line["value"] / line["cpu_baseline"]["value"], 1)
+            nat = line["cpu_baseline"].get("native_march")
+            if nat:
+                nat["gpu_speedup"] = round(line["value"] / nat["aca_value"], 1)
         except Exception as e:  # noqa: BLE001
             line["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
     all_done.set()

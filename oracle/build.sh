@@ -38,6 +38,20 @@ if [[ -f "$REF_SRC" ]]; then
         "$HERE/_ref/ref_batch.o" -lpthread
     rm -f "$HERE/_ref/"*.o
     echo "built oracle/_ref/libsks_ref.so from $REF_SRC"
+    # The same sources built for speed, for bench.py's CPU baseline only (never a checker):
+    # -O3, AVX-512 (x86-64-v4, which the GPU boxes' EPYC 9575F has; bench checks the CPU
+    # flags before loading it), FMA contraction on, LTO so the batch loop can inline the
+    # solver.  Not bit-exact (about a third of the outputs keep every bit).
+    NFLAGS=(-O3 -fPIC -march=x86-64-v4 -ffp-contract=fast -flto)
+    sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_SRC" |
+        g++ -std=c++17 "${NFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/aca_sks_native.o"
+    sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_GE" |
+        g++ -std=c++17 "${NFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/ge_native.o"
+    g++ -std=c++17 "${NFLAGS[@]}" -c "$HERE/ref_batch.cpp" -o "$HERE/_ref/ref_batch_native.o"
+    g++ "${NFLAGS[@]}" -shared -o "$HERE/_ref/libsks_ref_native.so" "$HERE/_ref/aca_sks_native.o" \
+        "$HERE/_ref/ge_native.o" "$HERE/_ref/ref_batch_native.o" -lpthread
+    rm -f "$HERE/_ref/"*.o
+    echo "built oracle/_ref/libsks_ref_native.so (speed build, not bit-exact)"
 else
     echo "reference source absent; oracle/_ref not rebuilt"
 fi

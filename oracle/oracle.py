@@ -18,6 +18,19 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 ORACLE_SO = os.path.join(HERE, "_build", "libhg_oracle.so")
 REF_SO = os.path.join(HERE, "_ref", "libsks_ref.so")
+# the same reference sources built for speed (-O3, AVX-512, FMA contraction, LTO): a CPU
+# baseline for bench.py only, never a checker -- its outputs are not bit-exact
+REF_NATIVE_SO = os.path.join(HERE, "_ref", "libsks_ref_native.so")
+
+
+def cpu_has_avx512() -> bool:
+    """The x86-64-v4 feature set REF_NATIVE_SO was built for (loading it elsewhere would
+    fault on the first AVX-512 instruction)."""
+    try:
+        flags = open("/proc/cpuinfo").read()
+    except OSError:
+        return False
+    return all(f" {f}" in flags for f in ("avx512f", "avx512bw", "avx512cd", "avx512dq", "avx512vl"))
 
 _f32p = ctypes.POINTER(ctypes.c_float)
 _f64p = ctypes.POINTER(ctypes.c_double)
