@@ -329,6 +329,56 @@ def table8_sweep(d: Dist, pkg):
     return out
 
 
+def grouped_section(d: Dist, pkg, k: int = 64, m: int = 1000):
+    """A caller with many of Table 8's N = 1000 batches (f64 SoA, unnormalised, cal_Homo_ACA's
+    contract): hg_solve_grouped_f64 (32 batches per launch) called as a native caller would,
+    with its pointer arrays built once, against one launch per batch (`table8_sweep`'s native
+    C++ loop at n = 1000 is the per-launch figure; `one_launch_each` here goes through
+    ops.solve from Python) and against ops.solve_grouped, whose per-tensor checks cost more
+    host time than the launches.  Device time per batch from HIP events."""
+    import ctypes
+    srcs, tars, outs = [], [], []
+    for i in range(k):
+        srcs.append(pkg.fill_uniform(m * 8, SEED, 2 * i * m * 8, device=d.dev).view(8, m).double())
+        tars.append(pkg.fill_uniform(m * 8, SEED, (2 * i + 1) * m * 8, device=d.dev).view(8, m).double())
+        outs.append(torch.empty((9, m), dtype=torch.float64, device=d.dev))
+    each = [torch.empty_like(o) for o in outs]
+
+    P = ctypes.c_void_p * k
+    ps, pt, ph = (P(*[x.data_ptr() for x in v]) for v in (srcs, tars, outs))
+    ns = (ctypes.c_int64 * k)(*([m] * k))
+    grouped = pkg.lib().hg_solve_grouped_f64
+    stream = torch.cuda.current_stream(d.dev).cuda_stream
+
+    def f_group():
+        rc = grouped(0, ps, pt, ph, ns, k, 1, 0, stream)
+        if rc:
+            raise pkg.HipError("hg_solve_grouped_f64", rc)
+
+    def f_group_py():
+        pkg.solve_grouped("aca", srcs, tars, normalize=False, layout="soa", outs=outs)
+
+    def f_each():
+        for s, t, o in zip(srcs, tars, each):
+            pkg.solve("aca", s, t, normalize=False, layout="soa", out=o)
+
+    for _ in range(5):
+        f_group()
+        f_group_py()
+        f_each()
+    _, ms_g = timed_region(d, f_group, 200)
+    _, ms_gp = timed_region(d, f_group_py, 20)
+    _, ms_e = timed_region(d, f_each, 20)
+    same = all(torch.equal(a.view(torch.int64), b.view(torch.int64)) for a, b in zip(outs, each))
+    us_g, us_e = ms_g * 1e3 / k, ms_e * 1e3 / k
+    return {"batches": k, "n_per_batch": m, "layout": "soa f64, unnormalised",
+            "grouped_us_per_batch": round(us_g, 3),
+            "grouped_python_wrapper_us_per_batch": round(ms_gp * 1e3 / k, 3),
+            "one_launch_each_us_per_batch": round(us_e, 3),
+            "grouped_speedup": round(us_e / us_g, 1), "table8_us_n1000": 3.20,
+            "speedup_vs_table8": round(3.20 / us_g, 1), "bit_identical": bool(same)}
+
+
 def reference_layout(d: Dist, pkg):
     """Like-for-like with the reference GPU harness (cal_Homo_ACA/SKS,
     GPU_Runtime Test.cu:81-240, timed as cal_ACA does at :1166-1206): FP64, SoA
@@ -800,6 +850,7 @@ def main():
             del bs_h, bt_h, Hb
             line["reference_layout"] = reference_layout(d, pkg)
             line["table8_sweep"] = table8_sweep(d, pkg)
+            line["grouped_small"] = grouped_section(d, pkg)
             line["ransac"] = ransac_section(d, pkg)
             line["host_boundary"] = host_boundary_section(d, pkg, n)
             # f64 AoS (sks::runKernel_ACA_double semantics) on the same inputs

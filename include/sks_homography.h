@@ -198,6 +198,20 @@ int hg_solve_host_f32(int algo, const float* src, const float* tar, float* H, in
 int hg_solve_host_f64(int algo, const double* src, const double* tar, double* H, int64_t n,
                       int layout, int flags, void* stream);
 
+/* Many small batches in one launch: batch i is src[i], tar[i] -> H[i] with n[i] problems
+ * (device pointers; the four arrays themselves are HOST arrays of `count` entries), every
+ * batch in `layout` with `flags`, solved by `algo` (an HG_ALGO_* id; HG_ALGO_GPT binary64
+ * only).  Up to 32 batches travel in one launch's arguments (more are split into further
+ * launches on `stream`; empty batches are skipped).  The bits equal hg_<algo>_* on each
+ * batch.  For callers with many small batches (e.g. a RANSAC per image pair), where one
+ * launch per batch is bound by the ~2.7 us per-launch cost rather than by the work. */
+int hg_solve_grouped_f32(int algo, const float* const* src, const float* const* tar,
+                         float* const* H, const int64_t* n, int count, int layout, int flags,
+                         void* stream);
+int hg_solve_grouped_f64(int algo, const double* const* src, const double* const* tar,
+                         double* const* H, const int64_t* n, int count, int layout, int flags,
+                         void* stream);
+
 /* Deterministic sums of the rows of x (rows, cols), row-major, into out[rows]: a fixed
  * two-level order (chunks of 4096 in order, folded by halving strides), so the bits do
  * not depend on timing.  x is OVERWRITTEN (used as the scratch for the chunk sums).

@@ -50,6 +50,48 @@ __global__ __launch_bounds__(kBlock) void solve_generic(const T* __restrict__ sr
     }
 }
 
+// Many small batches in one launch (hg_solve_grouped_*): up to kGroupMax batches ride in
+// the kernel arguments; block b of the grid belongs to the batch whose block range holds
+// it (a wave-uniform search over the block prefix sums), and within it one lane solves
+// one problem exactly as solve_generic does.  Small batches are bound by the per-launch
+// cost (argument staging, ~1 us of the ~2.7 us a launch costs back to back, §6 of
+// DESIGN.md), so one launch for a group replaces one per batch.
+constexpr int kGroupMax = 32;
+template <typename T>
+struct GroupArgs {
+    const T* src[kGroupMax];
+    const T* tar[kGroupMax];
+    T* H[kGroupMax];
+    int64_t n[kGroupMax];
+    uint32_t first_block[kGroupMax + 1];  // prefix sums of each batch's block count
+    int count;
+};
+
+template <int ALGO, bool NORM, typename T, bool SOA>
+__global__ __launch_bounds__(kBlock) void solve_grouped(GroupArgs<T> g) {
+    const uint32_t blk = blockIdx.x;
+    int b = 0;
+    while (b + 1 < g.count && g.first_block[b + 1] <= blk) ++b;  // uniform: scalar loop
+    const int64_t n = g.n[b];
+    const int64_t p = (int64_t)(blk - g.first_block[b]) * kBlock + threadIdx.x;
+    if (p >= n) return;
+    const T* __restrict__ src = g.src[b];
+    const T* __restrict__ tar = g.tar[b];
+    T* __restrict__ H = g.H[b];
+    T s[8], t[8], h[9];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+        s[k] = SOA ? src[(int64_t)k * n + p] : src[p * 8 + k];
+        t[k] = SOA ? tar[(int64_t)k * n + p] : tar[p * 8 + k];
+    }
+    solve<ALGO, NORM>(s, t, h);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) {
+        if (SOA) H[(int64_t)k * n + p] = h[k];
+        else H[p * 9 + k] = h[k];
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Counter-based uniform generator (bit-identical to oracle_fill_uniform_f32).
 
@@ -253,6 +295,72 @@ int dispatch(const T* src, const T* tar, T* H, int64_t n, int layout, int flags,
     return launch_solver<ALGO, false>(src, tar, H, n, layout, s, host);
 }
 
+// Groups of batches: host arrays of device pointers and sizes, split into launches of at
+// most kGroupMax batches (empty batches skipped).  Same validation as dispatch per batch.
+template <int ALGO, bool NORM, typename T, bool SOA>
+int launch_grouped_chunk(const GroupArgs<T>& g, hipStream_t s) {
+    const uint32_t blocks = g.first_block[g.count];
+    if (blocks == 0) return 0;
+    solve_grouped<ALGO, NORM, T, SOA><<<blocks, kBlock, 0, s>>>(g);
+    return launch_status();
+}
+
+template <typename T>
+int dispatch_grouped(int algo, const T* const* src, const T* const* tar, T* const* H,
+                     const int64_t* n, int count, int layout, int flags, void* stream) {
+    const int max_algo = sizeof(T) == 8 ? kGPT : kGE;
+    if (algo < kACA || algo > max_algo || count < 0) return kErrInvalid;
+    if (layout != HG_LAYOUT_AOS && layout != HG_LAYOUT_SOA) return kErrInvalid;
+    if (flags & ~HG_FLAG_NORMALIZE) return kErrInvalid;
+    if (count == 0) return 0;
+    if (!src || !tar || !H || !n) return kErrInvalid;
+    for (int i = 0; i < count; ++i) {
+        if (n[i] < 0) return kErrInvalid;
+        if (n[i] > 0 && (!src[i] || !tar[i] || !H[i])) return kErrInvalid;
+    }
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool norm = flags & HG_FLAG_NORMALIZE, soa = layout == HG_LAYOUT_SOA;
+    GroupArgs<T> g{};
+    auto flush = [&]() -> int {
+        int rc = 0;
+        if (g.count == 0) return 0;
+#define HG_G(A)                                                                                   \
+    rc = norm ? (soa ? launch_grouped_chunk<A, true, T, true>(g, s) : launch_grouped_chunk<A, true, T, false>(g, s)) \
+              : (soa ? launch_grouped_chunk<A, false, T, true>(g, s) : launch_grouped_chunk<A, false, T, false>(g, s))
+        switch (algo) {
+            case kACA: HG_G(kACA); break;
+            case kSKS: HG_G(kSKS); break;
+            case kGE: HG_G(kGE); break;
+            default:
+                if constexpr (sizeof(T) == 8) { HG_G(kGPT); }
+                break;
+        }
+#undef HG_G
+        g = GroupArgs<T>{};
+        return rc;
+    };
+    for (int i = 0; i < count; ++i) {
+        if (n[i] == 0) continue;
+        const int64_t nb = ceil_div(n[i], kBlock);
+        if (nb > 0x7fffffffLL || (int64_t)g.first_block[g.count] + nb > 0x7fffffffLL) {
+            if (g.count && (int64_t)g.first_block[g.count] + nb > 0x7fffffffLL) {
+                if (int rc = flush()) return rc;
+            }
+            if (nb > 0x7fffffffLL) return kErrInvalid;
+        }
+        const int j = g.count++;
+        g.src[j] = src[i];
+        g.tar[j] = tar[i];
+        g.H[j] = H[i];
+        g.n[j] = n[i];
+        g.first_block[j + 1] = g.first_block[j] + (uint32_t)nb;
+        if (g.count == kGroupMax) {
+            if (int rc = flush()) return rc;
+        }
+    }
+    return flush();
+}
+
 // The square specialisation (ACA_rect.m:28) is taken only where the ratio is known on
 // the host and is exactly 1, so dropping the multiply cannot change a bit.
 inline bool is_unit_ratio(float div) { return div == 1.0f; }
@@ -352,6 +460,18 @@ int hg_ge_f64(const double* src, const double* tar, double* H, int64_t n, int la
 int hg_gpt_f64(const double* src, const double* tar, double* H, int64_t n, int layout,
                int flags, void* stream) {
     return hg::dispatch<hg::kGPT>(src, tar, H, n, layout, flags, stream);
+}
+
+int hg_solve_grouped_f32(int algo, const float* const* src, const float* const* tar,
+                         float* const* H, const int64_t* n, int count, int layout, int flags,
+                         void* stream) {
+    return hg::dispatch_grouped<float>(algo, src, tar, H, n, count, layout, flags, stream);
+}
+
+int hg_solve_grouped_f64(int algo, const double* const* src, const double* const* tar,
+                         double* const* H, const int64_t* n, int count, int layout, int flags,
+                         void* stream) {
+    return hg::dispatch_grouped<double>(algo, src, tar, H, n, count, layout, flags, stream);
 }
 
 // Library-internal: the single-problem launch with a completion word (hg_sks_api.cpp).

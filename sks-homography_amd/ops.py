@@ -135,6 +135,65 @@ def solve_host(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool 
     return out
 
 
+def solve_grouped(algo: str, srcs, tars, normalize: bool = True, layout: str = "aos",
+                  outs=None):
+    """Many small batches in as few launches as possible (hg_solve_grouped_*: up to 32
+    batches per launch): ``srcs[i]``, ``tars[i]`` -> H_i, each batch shaped as for
+    ``solve``.  Returns the list of H (or fills ``outs``).  Same bits as ``solve`` on each
+    batch; for workloads of many small batches, where one launch each costs more than the
+    work."""
+    import ctypes
+
+    algo_id = _ALGO_ID.get(algo)
+    if algo_id is None:
+        raise ValueError(f"algo must be 'aca', 'sks', 'ge' or 'gpt', got {algo!r}")
+    lay = _LAYOUT_ID.get(layout)
+    if lay is None:
+        raise ValueError(f"layout must be 'aos' or 'soa', got {layout!r}")
+    srcs, tars = list(srcs), list(tars)
+    if len(srcs) != len(tars):
+        raise ValueError(f"{len(srcs)} src batches but {len(tars)} tar batches")
+    if not srcs:
+        return []
+    dev = _require_device(*srcs, *tars)
+    dt = srcs[0].dtype
+    if dt not in _DTYPES:
+        raise TypeError(f"batches must be float32 or float64, got {dt}")
+    if algo_id == 3 and dt is not torch.float64:
+        raise TypeError("the GPT-LU baseline (cal_Homo_GPT) is float64 only")
+    ns = []
+    for s, t in zip(srcs, tars):
+        if s.dtype is not dt or t.dtype is not dt:
+            raise TypeError("every batch must have the same dtype")
+        if not (s.is_contiguous() and t.is_contiguous()) or s.shape != t.shape:
+            raise ValueError("each src/tar pair must be contiguous and of equal shape")
+        if lay == 0 and not ((s.dim() == 2 and s.shape[1] == 8) or
+                             (s.dim() == 3 and tuple(s.shape[1:]) == (4, 2))):
+            raise ValueError(f"AoS batches must be (n,8) or (n,4,2), got {tuple(s.shape)}")
+        if lay == 1 and not (s.dim() == 2 and s.shape[0] == 8):
+            raise ValueError(f"SoA batches must be (8,n), got {tuple(s.shape)}")
+        ns.append(s.shape[0] if lay == 0 else s.shape[1])
+    if outs is None:
+        outs = [torch.empty((m, 9) if lay == 0 else (9, m), dtype=dt, device=dev) for m in ns]
+    else:
+        outs = list(outs)
+        if len(outs) != len(srcs):
+            raise ValueError("one out tensor per batch")
+        _require_device(*outs)
+        for o, m in zip(outs, ns):
+            want = (m, 9) if lay == 0 else (9, m)
+            if tuple(o.shape) != want or o.dtype is not dt or not o.is_contiguous():
+                raise ValueError(f"out must be a contiguous {want} {dt} tensor, got {tuple(o.shape)}")
+    k = len(srcs)
+    P = ctypes.c_void_p * k
+    fn = "hg_solve_grouped_f32" if dt is torch.float32 else "hg_solve_grouped_f64"
+    with _guard(dev):
+        _lib.call(fn, algo_id, P(*[x.data_ptr() for x in srcs]), P(*[x.data_ptr() for x in tars]),
+                  P(*[x.data_ptr() for x in outs]), (ctypes.c_int64 * k)(*ns), k, lay,
+                  _lib.HG_FLAG_NORMALIZE if normalize else 0, _stream(dev))
+    return outs
+
+
 def aca(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torch.Tensor:
     return solve("aca", src, tar, normalize, layout, out)
 

@@ -137,6 +137,19 @@ def test_other_entry_validation(pkg):
     assert lib.hg_solve_host_f32(3, None, None, None, 0, 0, 1, None) == 1       # GPT: f64 only
     assert lib.hg_solve_host_f64(3, None, None, None, 0, 0, 1, None) == 0
     assert lib.hg_solve_host_f64(4, None, None, None, 0, 0, 1, None) == 1
+    for f in (lib.hg_solve_grouped_f32, lib.hg_solve_grouped_f64):  # grouped: checks first
+        assert f(0, None, None, None, None, 0, 0, 1, None) == 0                 # no batches
+        assert f(0, None, None, None, None, -1, 0, 1, None) == 1                # count < 0
+        assert f(0, None, None, None, None, 3, 0, 1, None) == 1                 # NULL arrays
+        assert f(9, None, None, None, None, 0, 0, 1, None) == 1                 # algo
+        assert f(0, None, None, None, None, 0, 5, 1, None) == 1                 # layout
+        assert f(0, None, None, None, None, 0, 0, 4, None) == 1                 # flags
+        P = ctypes.c_void_p * 2
+        n = (ctypes.c_int64 * 2)(4, -1)
+        assert f(0, P(1, 1), P(1, 1), P(1, 1), n, 2, 0, 1, None) == 1           # n < 0
+        n = (ctypes.c_int64 * 2)(4, 2)
+        assert f(0, P(1, None), P(1, 1), P(1, 1), n, 2, 0, 1, None) == 1        # NULL batch
+    assert lib.hg_solve_grouped_f32(3, None, None, None, None, 0, 0, 1, None) == 1  # GPT: f64
     assert pkg.version().startswith("sks-homography-amd")
 
 
