@@ -75,6 +75,35 @@ int main() {
         std::fprintf(stderr, "host-vector batch differs from the device batch\n");
         return 12;
     }
+    // many small batches in one grouped call (the C ABI): 40 slices of the device batch,
+    // each of its own size, every row equal to the single call's
+    {
+        const int kGroups = 40;
+        const float* gs[kGroups];
+        const float* gt[kGroups];
+        float* gh[kGroups];
+        int64_t gn[kGroups];
+        int64_t at = 0;
+        for (int i = 0; i < kGroups; ++i) {
+            gn[i] = 1 + 37 * i;
+            gs[i] = ds + at * 8;
+            gt[i] = dt + at * 8;
+            gh[i] = dH + at * 9;
+            at += gn[i];
+        }
+        (void)hipMemset(dH, 0, at * 36);
+        if (check(hg_solve_grouped_f32(HG_ALGO_ACA, gs, gt, gh, gn, kGroups, HG_LAYOUT_AOS,
+                                       HG_FLAG_NORMALIZE, nullptr),
+                  "hg_solve_grouped_f32"))
+            return 13;
+        std::vector<float> gH(at * 9);
+        (void)hipMemcpy(gH.data(), dH, at * 36, hipMemcpyDeviceToHost);
+        for (int64_t i = 0; i < at; ++i)
+            if (std::memcmp(&gH[i * 9], h_aca, sizeof h_aca) != 0) {
+                std::fprintf(stderr, "grouped row %lld differs from the single call\n", (long long)i);
+                return 14;
+            }
+    }
     // device pointers through the single-problem signature too
     if (check(sks::runKernel_SKS(ds, dt, dH), "runKernel_SKS(device ptrs)")) return 7;
     float row[9];
