@@ -32,6 +32,9 @@ import __graft_entry__ as ge  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md, chip table)
 SEED = 11
+# exit status of a run a watchdog ended (a stalled collective or extras section): the JSON
+# line is printed first, but torchrun / CI can tell the stall from a clean finish
+EXIT_STALLED = 3
 
 
 def parse():
@@ -57,6 +60,78 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="gloo only to rehearse N>1 on a one-GPU box")
     return ap.parse_args()
+
+
+def _kfd_gpu_bdfs(base: str = "/sys/class/kfd/kfd/topology/nodes"):
+    """PCI addresses of the node's GPUs in KFD topology order (the order the HIP runtime
+    numbers them), read from /sys without touching the GPU."""
+    out = []
+    try:
+        nodes = sorted(int(x) for x in os.listdir(base) if x.isdigit())
+    except OSError:
+        return out
+    for nd in nodes:
+        props = {}
+        for line in (_read(f"{base}/{nd}/properties") or "").splitlines():
+            k, _, v = line.partition(" ")
+            props[k] = v.strip()
+        try:
+            if int(props.get("simd_count", "0")) == 0:
+                continue  # a CPU node
+            loc, dom = int(props["location_id"]), int(props.get("domain", "0"))
+        except (KeyError, ValueError):
+            continue
+        out.append(f"{dom:04x}:{loc >> 8 & 0xff:02x}:{loc >> 3 & 0x1f:02x}.{loc & 7}")
+    return out
+
+
+def _visible(items, env_names):
+    for name in env_names:
+        v = os.environ.get(name)
+        if v is None or v == "":
+            continue
+        try:
+            return [items[int(x)] for x in v.split(",")]
+        except (ValueError, IndexError):
+            return None  # UUIDs or out of range: mapping unknown
+    return items
+
+
+def bind_numa(local_index: int):
+    """Binds this process to the CPUs of its GPU's NUMA node -- BEFORE any GPU call, so the
+    threads the HIP runtime and torch create afterwards inherit the binding -- and returns
+    what it did.  The GPU is found from /sys (KFD topology order, the visible-devices
+    variables applied), its node from /sys/bus/pci/devices/<bdf>/numa_node.  A host batch's
+    pages then first-touch on the GPU's node (SharedHostBatch), and the PCIe traffic of
+    hg_solve_host_* crosses no socket link.  The pre-binding affinity is kept for the CPU
+    baseline (_ORIGINAL_AFFINITY)."""
+    global _ORIGINAL_AFFINITY
+    _ORIGINAL_AFFINITY = sorted(os.sched_getaffinity(0))
+    rec = {"gpu_index": local_index, "bdf": None, "node": None, "bound_cpus": None}
+    gpus = _visible(_kfd_gpu_bdfs(), ("ROCR_VISIBLE_DEVICES",))
+    gpus = _visible(gpus, ("HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES")) if gpus else gpus
+    if not gpus or local_index >= len(gpus):
+        rec["note"] = "GPU not found in /sys/class/kfd: not bound"
+        return rec
+    bdf = gpus[local_index]
+    rec["bdf"] = bdf
+    try:
+        node = int(_read(f"/sys/bus/pci/devices/{bdf}/numa_node"))
+    except (TypeError, ValueError):
+        node = -1
+    rec["node"] = node
+    if node < 0:
+        rec["note"] = "no NUMA node for the GPU: not bound"
+        return rec
+    cpus = sorted(set(_cpu_list(_read(f"/sys/devices/system/node/node{node}/cpulist"))) &
+                  set(_ORIGINAL_AFFINITY))
+    if cpus:
+        os.sched_setaffinity(0, cpus)
+        rec["bound_cpus"] = len(cpus)
+    return rec
+
+
+_ORIGINAL_AFFINITY = None
 
 
 class Dist:
@@ -100,6 +175,17 @@ class Dist:
         t = torch.tensor([x], dtype=torch.float64, device=dev)
         self.pg.all_reduce(t, op=self.pg.ReduceOp.MAX)
         return float(t.item())
+
+    def gather_rows(self, row):
+        """Every rank's equal-length list of numbers, on every rank (a SUM all-reduce of a
+        zero matrix holding each rank's row: small, control path only)."""
+        if not self.pg:
+            return [list(row)]
+        dev = self.dev if self.backend == "nccl" else "cpu"
+        t = torch.zeros((self.world, len(row)), dtype=torch.float64, device=dev)
+        t[self.rank] = torch.tensor(row, dtype=torch.float64, device=dev)
+        self.pg.all_reduce(t)
+        return t.cpu().tolist()
 
     def close(self):
         if self.pg:
@@ -156,6 +242,63 @@ def reference_statistic(d: Dist, fn):
     return {"loops": loops, "mean_us": round(ms * 1e3, 2)}
 
 
+def _read(path: str):
+    try:
+        with open(path) as f:
+            return f.read().strip()
+    except OSError:
+        return None
+
+
+def _cpu_list(text: str):
+    """'0-3,8,10-11' -> [0, 1, 2, 3, 8, 10, 11]."""
+    out = []
+    for part in (text or "").split(","):
+        if part:
+            a, _, b = part.partition("-")
+            out.extend(range(int(a), int(b or a) + 1))
+    return out
+
+
+def cpu_topology():
+    """The logical CPUs this process may run on, one per physical core (the lowest-numbered
+    of each core's hardware threads), ordered so that any prefix spreads evenly over the
+    NUMA nodes; plus each core's node.  From /sys (topology/thread_siblings_list,
+    /sys/devices/system/node)."""
+    allowed = _ORIGINAL_AFFINITY or sorted(os.sched_getaffinity(0))  # before bind_numa
+    node_of = {}
+    for nd in sorted(int(x[4:]) for x in os.listdir("/sys/devices/system/node")
+                     if x.startswith("node") and x[4:].isdigit()) if os.path.isdir(
+                         "/sys/devices/system/node") else []:
+        for c in _cpu_list(_read(f"/sys/devices/system/node/node{nd}/cpulist")):
+            node_of[c] = nd
+    first = {}
+    for c in allowed:
+        sib = _cpu_list(_read(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list"))
+        key = min(sib) if sib else c
+        first.setdefault(key, c)
+    per_node = {}
+    for c in sorted(first.values()):
+        per_node.setdefault(node_of.get(c, 0), []).append(c)
+    order = []
+    for i in range(max((len(v) for v in per_node.values()), default=0)):
+        for nd in sorted(per_node):
+            if i < len(per_node[nd]):
+                order.append(per_node[nd][i])
+    return {"cores": order, "node_of": {c: node_of.get(c, 0) for c in order},
+            "nodes": len(per_node)}
+
+
+def cgroup_cpu_quota():
+    """CPUs of time per period this job may use (cgroup v2 cpu.max), or None if unlimited."""
+    text = _read("/sys/fs/cgroup/cpu.max")
+    try:
+        q, period = text.split()
+        return None if q == "max" else max(1, int(-(-int(q) // int(period))))
+    except (AttributeError, ValueError):
+        return None
+
+
 def host_info():
     model = None
     try:
@@ -168,15 +311,15 @@ def host_info():
         pass
     tpc = None
     try:  # "0,128" or "0-1" -> 2 hardware threads per core
-        with open("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list") as f:
-            tpc = 0
-            for part in f.read().strip().split(","):
-                a, _, b = part.partition("-")
-                tpc += int(b or a) - int(a) + 1
-    except (OSError, ValueError):
+        tpc = len(_cpu_list(_read("/sys/devices/system/cpu/cpu0/topology/thread_siblings_list")))
+    except (TypeError, ValueError):
         pass
+    topo = cpu_topology()
     return {"cpu_model": model, "nproc": os.cpu_count(),
-            "usable_cpus": len(os.sched_getaffinity(0)), "threads_per_core": tpc}
+            "usable_cpus": len(os.sched_getaffinity(0)), "threads_per_core": tpc,
+            "physical_cores_usable": len(topo["cores"]), "numa_nodes": topo["nodes"],
+            # a cgroup CPU quota ("max" = none) caps what many threads can get
+            "cgroup_cpu_max": _read("/sys/fs/cgroup/cpu.max")}
 
 
 def graph_of(d: Dist, fn, calls: int):
@@ -209,60 +352,109 @@ def pmc_traffic(kernel_key: str):
         return None
 
 
+# Table 5 (imgs/CPU-runtime.png): one 4-point set solved 10 M times on one core,
+# MSVC /O2, us per H (main.cpp:87-114)
+TABLE5_US = {"aca": 0.0145, "sks": 0.0252, "aca_f64": 0.0171, "sks_f64": 0.0256}
+
+
 def cpu_baseline(n_sample: int):
-    """Reference C++ solver bodies (oracle/_ref) if built, else our restatement;
-    streaming AoS f32 batch over all usable host threads.  About 10-30 s of CPU work."""
+    """The reference's own C++ solver bodies (oracle/_ref) on this host's cores, SURVEY 8(d):
+    (iii) the streaming AoS f32 batch of n_sample problems on ALL physical cores -- one thread
+    per core, pinned, each thread first-touching its own slice so its pages are NUMA-local
+    -- is `value`; the sweep 1, 2, 4 ... all cores is methodology (ii)/(iii); (i) is the
+    reference's own single-core same-points method (main.cpp:87-114) in f32 and f64 beside
+    Table 5.  About 10-30 s of CPU time.  If oracle/_ref did not travel to this box the
+    builder's C restatement is timed instead (kind "port") and the record says so loudly."""
     orc = ge.load_oracle()
-    threads = max(1, min(16, len(os.sched_getaffinity(0))))
-    if orc.RefOracle.available():
-        engine, kind = orc.RefOracle(), "reference"
-    else:
-        engine, kind = orc.Oracle(), "port"
+    topo = cpu_topology()
+    cores = topo["cores"]
+    P = len(cores)
+    # A cgroup CPU quota caps the CPU time all threads together get: the GPU boxes give a
+    # one-GPU job 16 CPUs of time (cpu.max 1600000 100000) on a 2 x 64-core host.  `value` is
+    # then measured on that many physical cores (spread over both sockets); the sweep still
+    # runs up to every physical core to show it, and a linear all-core bound is reported.
+    quota = cgroup_cpu_quota()
+    P_eff = min(P, quota) if quota else P
     gen = orc.Oracle()
     src = gen.fill_uniform(n_sample * 8, SEED, 0).reshape(n_sample, 8)
     tar = gen.fill_uniform(n_sample * 8, SEED, n_sample * 8).reshape(n_sample, 8)
     H = np.empty((n_sample, 9), dtype=np.float32)
+    warning = None
+    if orc.RefOracle.available():
+        engine, kind = orc.RefOracle(), "reference"
+
+        def timed(algo, eng, k, reps):
+            return eng.time_pinned(algo, src, tar, cores[:k], reps)
+    else:
+        engine, kind = orc.Oracle(), "port"
+        warning = ("oracle/_ref (the reference's own compiled C++) is missing on this box: the "
+                   "CPU baseline times the builder's C restatement instead, unpinned")
+        print(f"bench.py: WARNING: {warning}", file=sys.stderr, flush=True)
+
+        def timed(algo, eng, k, reps):
+            return eng.time_batch(algo, src, tar, H, k, reps)
+
+    def rate(algo, eng, k, seconds):
+        t1 = timed(algo, eng, k, 1)
+        reps = max(1, int(seconds / max(t1, 1e-6)))
+        return n_sample * reps / timed(algo, eng, k, reps) / 1e6, reps
+
     out = {}
     algos = ("aca", "sks", "ge") if kind == "reference" else ("aca", "sks")
     for algo in algos:
-        t1 = engine.time_batch(algo, src, tar, H, threads, 1)
-        reps = max(1, int(1.5 / max(t1, 1e-6)))
-        t = engine.time_batch(algo, src, tar, H, threads, reps)
-        out[algo] = n_sample * reps / t / 1e6
-        out[algo + "_reps"] = reps
-    # methodology (ii)/(iii) of SURVEY 8(d): the streaming batch on 1, 2, 4 ... threads
+        out[algo], out[algo + "_reps"] = rate(algo, engine, P_eff, 1.5)
+    verified = None
+    if kind == "reference":  # the timed multi-core path computes what the reference computes
+        Hp = np.empty_like(H)
+        engine.time_pinned("aca", src, tar, cores[:P_eff], 1, Hp)
+        verified = bool(np.array_equal(Hp.view(np.uint32), engine.solve("aca", src, tar).view(np.uint32)))
+    # methodology (ii)/(iii) of SURVEY 8(d): the streaming batch on 1, 2, 4 ... all cores
     sweep = {}
-    for t_count in sorted({min(1 << k, threads) for k in range(threads.bit_length() + 1)}):
-        t1 = engine.time_batch("aca", src, tar, H, t_count, 1)
-        reps = max(1, int(0.5 / max(t1, 1e-6)))
-        sweep[str(t_count)] = round(n_sample * reps / engine.time_batch(
-            "aca", src, tar, H, t_count, reps) / 1e6, 1)
+    for k in sorted({min(1 << i, P) for i in range(P.bit_length() + 1)}):
+        sweep[str(k)] = round(rate("aca", engine, k, 0.4)[0], 1)
     native = None
     if kind == "reference" and os.path.exists(orc.REF_NATIVE_SO) and orc.cpu_has_avx512():
         # the reference built for speed (not bit-exact): a stronger CPU yardstick beside the
         # bit-exact one; the GPU is never compared with anything but both
         fast = orc.RefOracle(orc.REF_NATIVE_SO)
-        native = {"flags": "g++ -O3 -march=x86-64-v4 -ffp-contract=fast -flto (not bit-exact)"}
+        native = {"flags": "g++ -O3 -march=x86-64-v4 -ffp-contract=fast -flto (not bit-exact)",
+                  "threads": P_eff}
         for algo in ("aca", "sks"):
-            t1 = fast.time_batch(algo, src, tar, H, threads, 1)
-            reps = max(1, int(1.0 / max(t1, 1e-6)))
-            native[algo + "_value"] = round(
-                n_sample * reps / fast.time_batch(algo, src, tar, H, threads, reps) / 1e6, 1)
+            native[algo + "_value"] = round(rate(algo, fast, P_eff, 1.0)[0], 1)
     single = {}
     if kind == "reference":
-        # the reference's own CPU methodology (main.cpp:87-92): one set, 10 M calls
+        # the reference's own CPU methodology (main.cpp:87-114): one set, 10 M calls, one core
         for algo in algos:
             single[algo] = engine.time_repeat(algo, src[0], tar[0], 10_000_000) / 1e7 * 1e6
-    return {
-        "value": out["aca"], "unit": "M homographies/s", "cores": threads, "kind": kind,
+        for algo in ("aca", "sks"):
+            single[algo + "_f64"] = engine.time_repeat(
+                algo, src[0].astype(np.float64), tar[0].astype(np.float64), 10_000_000) / 1e7 * 1e6
+        single = {k: round(v, 5) for k, v in single.items()}
+        single["table5_us_msvc_O2"] = TABLE5_US
+    quota_note = (f"{P_eff} = this job's cgroup CPU quota (cpu.max); the host has {P} physical "
+                  f"cores, but more threads only share the same {P_eff} CPUs of time (see the "
+                  f"sweep)") if P_eff < P else f"all {P} physical cores"
+    rec = {
+        "value": out["aca"], "unit": "M homographies/s", "cores": P_eff, "kind": kind,
         "sks_value": out["sks"], "ge_value": out.get("ge"),
         "sample": (f"AoS f32 normalised batch of {n_sample} problems (seed {SEED}, U[0,1024)), "
-                   f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, {threads} std::threads"),
+                   f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, one std::thread per "
+                   f"physical core, pinned, spread over the NUMA nodes, NUMA-local first-touch "
+                   f"slices; cores: {quota_note}"),
+        "physical_cores": P, "cgroup_cpu_quota": quota,
+        # every physical core at the measured per-core rate: an upper bound, not a measurement
+        # (it ignores the DRAM bandwidth 100 B/H would need at that rate)
+        "all_physical_cores_linear_bound": round(out["aca"] / P_eff * P, 1),
+        "all_core_output_bit_exact": verified,
         "single_core_same_points_us_per_H": single or None,
         "aca_thread_sweep_M_per_s": sweep,
+        "sixteen_thread_aca_value": sweep.get("16"),
         "native_march": native,
         "host": host_info(),
     }
+    if warning:
+        rec["warning"] = warning
+    return rec
 
 
 def torch_tensor_aca_rect(src, tar, scale, div):
@@ -492,7 +684,10 @@ def host_sharded_section(d: Dist, pkg, src, tar, H, n: int, n_total: int):
     name = f"sks_hg_bench_{os.environ.get('MASTER_PORT', '0')}_{n_total}"
     batch, err = None, None
     try:
-        batch = shard.SharedHostBatch(name, n_total, d.rank, d.barrier)
+        # every rank allocates the pages of its own block (NUMA-local: the rank is bound to
+        # its GPU's node, bind_numa); a failure anywhere reaches every rank through `agree`
+        batch = shard.SharedHostBatch(name, n_total, d.rank, d.barrier, world=d.world,
+                                      agree=lambda ok: d.max(0.0 if ok else 1.0) == 0.0)
     except OSError as e:
         err = str(e)
     if d.max(0.0 if batch is not None else 1.0) != 0.0:  # all ranks leave together
@@ -646,15 +841,37 @@ def split_gather_section(d: Dist, pkg, src, tar, H, n: int, n_total: int, step_m
     return out
 
 
+def rank_block_inputs(pkg, dev, n: int, n_total: int, rank: int):
+    """Rank `rank`'s block of the global batch (weak scaling: every rank owns n problems of
+    n_total = n * world, rows [rank*n, (rank+1)*n)).  The global batch is src = the stream's
+    values [0, 8 n_total) and tar = values [8 n_total, 16 n_total) (seed SEED), so the
+    blocks of all ranks concatenate to exactly the batch one device would generate whole
+    (tests/test_gpu_config5.py checks this for the 80 M batch of BASELINE configs[4])."""
+    lo = rank * n
+    src = pkg.fill_uniform(n * 8, SEED, lo * 8, device=dev).view(n, 8)
+    tar = pkg.fill_uniform(n * 8, SEED, (n_total + lo) * 8, device=dev).view(n, 8)
+    return src, tar
+
+
 def main():
     args = parse()
+    # before anything touches the GPU: this rank's CPUs and first-touch pages on its GPU's
+    # NUMA node (the device index is LOCAL_RANK, as Dist picks it)
+    ndev = torch.cuda.device_count()  # counts devices without initialising HIP
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    numa = bind_numa(local if args.dist_backend == "nccl" else local % max(ndev, 1))
     d = Dist(args.dist_backend)
+    numa["rank"] = d.rank
+    try:  # the device HIP gave this rank is the one bound to
+        pr = torch.cuda.get_device_properties(d.dev)
+        got = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+        numa["bdf_matches_device"] = bool(numa["bdf"]) and numa["bdf"].startswith(got)
+    except (AttributeError, RuntimeError):
+        numa["bdf_matches_device"] = None
     pkg = ge.load_package()
     n = args.n
     n_total = n * d.world
-    lo = d.rank * n  # weak scaling: every rank owns an n-problem block of the global batch
-    src = pkg.fill_uniform(n * 8, SEED, lo * 8, device=d.dev).view(n, 8)
-    tar = pkg.fill_uniform(n * 8, SEED, (n_total + lo) * 8, device=d.dev).view(n, 8)
+    src, tar = rank_block_inputs(pkg, d.dev, n, n_total, d.rank)
     H = torch.empty((n, 9), dtype=torch.float32, device=d.dev)
     bpp = pkg.BYTES_PER_PROBLEM["f32"]
 
@@ -697,6 +914,16 @@ def main():
         },
         "launch_stats": per_launch,
     }
+    m = numa.get("bdf_matches_device")
+    rows = d.gather_rows([numa["node"] if numa["node"] is not None else -1,
+                          numa["bound_cpus"] or 0, -1 if m is None else int(m)])
+    line["numa"] = {
+        "per_rank": [{"rank": r, "node": int(a), "bound_cpus": int(b),
+                      "bdf_matches_device": None if c < 0 else bool(c)}
+                     for r, (a, b, c) in enumerate(rows)],
+        "rank0_gpu_bdf": numa["bdf"],
+        "note": numa.get("note", "each rank bound to its GPU's NUMA node before GPU init"),
+    }
 
     # Everything after the headline is reported beside it.  A global watchdog and a
     # per-section guard keep any failure there from costing the measured line: an
@@ -726,7 +953,7 @@ def main():
         emit()
         sys.stdout.flush()
         sys.stderr.flush()
-        os._exit(0)
+        os._exit(EXIT_STALLED)  # the line is out; the exit code still says the run stalled
 
     threading.Thread(target=extras_watchdog, daemon=True).start()
     if not args.no_extras:
@@ -885,7 +1112,7 @@ def main():
             emit()
             sys.stdout.flush()
             sys.stderr.flush()
-            os._exit(0)
+            os._exit(EXIT_STALLED)
 
         threading.Thread(target=watchdog, daemon=True).start()
         try:
@@ -901,6 +1128,8 @@ def main():
             # the speed-up is quoted against the multi-threaded host baseline
             line["cpu_baseline"]["gpu_speedup"] = round(
                 line["value"] / line["cpu_baseline"]["value"], 1)
+            line["cpu_baseline"]["gpu_speedup_vs_all_core_linear_bound"] = round(
+                line["value"] / line["cpu_baseline"]["all_physical_cores_linear_bound"], 1)
             nat = line["cpu_baseline"].get("native_march")
             if nat:
                 nat["gpu_speedup"] = round(line["value"] / nat["aca_value"], 1)

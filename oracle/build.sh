@@ -16,28 +16,45 @@
 # baseline) gets the same treatment: its only include is GE.hpp -> opencv2/core.hpp,
 # and its body (OpenCV rho.cpp hFuncRefC) uses no OpenCV symbol.  No stand-in
 # header is written and no reference text is copied into this repository.
+#
+# SKS_ORACLE_SANITIZE=<dir>: instead, build both checkers with AddressSanitizer and
+# UndefinedBehaviorSanitizer into <dir> (libhg_oracle.so, libsks_ref.so; no speed build),
+# for tests/test_sanitizers.py (the CPU restatement under ASan/UBSan).
 set -euo pipefail
 HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REF_ROOT="${SKS_REFERENCE_ROOT:-/root/reference}"
 REF_SRC="$REF_ROOT/C++ Codes/modules/ACA_SKS.cpp"
 REF_GE="$REF_ROOT/C++ Codes/modules/GE.cpp"   # RHO-GE baseline (includes only GE.hpp -> OpenCV)
 CFLAGS=(-O2 -fPIC -ffp-contract=off -fno-fast-math)
+OUT_BUILD="$HERE/_build"
+OUT_REF="$HERE/_ref"
+SAN="${SKS_ORACLE_SANITIZE:-}"
+if [[ -n "$SAN" ]]; then
+    CFLAGS=(-O1 -g -fPIC -ffp-contract=off -fno-fast-math -fno-omit-frame-pointer
+            -fsanitize=address,undefined -fno-sanitize-recover=all)
+    OUT_BUILD="$SAN"
+    OUT_REF="$SAN"
+fi
 
-mkdir -p "$HERE/_build"
-gcc -std=c11 -D_POSIX_C_SOURCE=200809L "${CFLAGS[@]}" -shared -o "$HERE/_build/libhg_oracle.so" \
+mkdir -p "$OUT_BUILD"
+gcc -std=c11 -D_POSIX_C_SOURCE=200809L "${CFLAGS[@]}" -shared -o "$OUT_BUILD/libhg_oracle.so" \
     "$HERE/hg_oracle.c" -lm -lpthread
 
 if [[ -f "$REF_SRC" ]]; then
-    mkdir -p "$HERE/_ref"
+    mkdir -p "$OUT_REF"
     sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_SRC" |
-        g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/aca_sks_ref.o"
+        g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$OUT_REF/aca_sks_ref.o"
     sed '/^[[:space:]]*#[[:space:]]*include/d' "$REF_GE" |
-        g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$HERE/_ref/ge_ref.o"
-    g++ -std=c++17 "${CFLAGS[@]}" -c "$HERE/ref_batch.cpp" -o "$HERE/_ref/ref_batch.o"
-    g++ -shared -o "$HERE/_ref/libsks_ref.so" "$HERE/_ref/aca_sks_ref.o" "$HERE/_ref/ge_ref.o" \
-        "$HERE/_ref/ref_batch.o" -lpthread
-    rm -f "$HERE/_ref/"*.o
-    echo "built oracle/_ref/libsks_ref.so from $REF_SRC"
+        g++ -std=c++17 "${CFLAGS[@]}" -x c++ -c - -o "$OUT_REF/ge_ref.o"
+    g++ -std=c++17 "${CFLAGS[@]}" -c "$HERE/ref_batch.cpp" -o "$OUT_REF/ref_batch.o"
+    g++ "${CFLAGS[@]}" -shared -o "$OUT_REF/libsks_ref.so" "$OUT_REF/aca_sks_ref.o" \
+        "$OUT_REF/ge_ref.o" "$OUT_REF/ref_batch.o" -lpthread
+    rm -f "$OUT_REF/"*.o
+    echo "built $OUT_REF/libsks_ref.so from $REF_SRC"
+    if [[ -n "$SAN" ]]; then
+        echo "built sanitized checkers in $SAN"
+        exit 0
+    fi
     # The same sources built for speed, for bench.py's CPU baseline only (never a checker):
     # -O3, AVX-512 (x86-64-v4, which the GPU boxes' EPYC 9575F has; bench checks the CPU
     # flags before loading it), FMA contraction on, LTO so the batch loop can inline the
@@ -55,4 +72,4 @@ if [[ -f "$REF_SRC" ]]; then
 else
     echo "reference source absent; oracle/_ref not rebuilt"
 fi
-echo "built oracle/_build/libhg_oracle.so"
+echo "built $OUT_BUILD/libhg_oracle.so"

@@ -16,8 +16,10 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ORACLE_SO = os.path.join(HERE, "_build", "libhg_oracle.so")
-REF_SO = os.path.join(HERE, "_ref", "libsks_ref.so")
+# SKS_ORACLE_SO / SKS_REF_SO: alternative builds of the same checkers (the ASan/UBSan builds
+# of tests/test_sanitizers.py)
+ORACLE_SO = os.environ.get("SKS_ORACLE_SO", os.path.join(HERE, "_build", "libhg_oracle.so"))
+REF_SO = os.environ.get("SKS_REF_SO", os.path.join(HERE, "_ref", "libsks_ref.so"))
 # the same reference sources built for speed (-O3, AVX-512, FMA contraction, LTO): a CPU
 # baseline for bench.py only, never a checker -- its outputs are not bit-exact
 REF_NATIVE_SO = os.path.join(HERE, "_ref", "libsks_ref_native.so")
@@ -163,6 +165,11 @@ class RefOracle:
         lib.ref_time_f32.restype = ctypes.c_double
         lib.ref_time_repeat_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64]
         lib.ref_time_repeat_f32.restype = ctypes.c_double
+        lib.ref_time_repeat_f64.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, _i64]
+        lib.ref_time_repeat_f64.restype = ctypes.c_double
+        lib.ref_time_pinned_f32.argtypes = [ctypes.c_int, _f32p, _f32p, _f32p, _i64,
+                                            ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
+        lib.ref_time_pinned_f32.restype = ctypes.c_double
         self.lib = lib
 
     @staticmethod
@@ -187,9 +194,27 @@ class RefOracle:
                                      _ptr(H, _f32p), src.shape[0], threads, reps)
 
     def time_repeat(self, algo: str, src8, tar8, iters: int) -> float:
+        """One 4-point set solved `iters` times on one core (main.cpp:87-114); float32 or
+        float64 by the inputs' dtype.  Wall seconds."""
+        if np.asarray(src8).dtype == np.float64:
+            src8 = np.ascontiguousarray(src8, np.float64)
+            tar8 = np.ascontiguousarray(tar8, np.float64)
+            H9 = np.empty(9, dtype=np.float64)
+            return self.lib.ref_time_repeat_f64(ALGOS[algo], _ptr(src8, _f64p), _ptr(tar8, _f64p),
+                                                _ptr(H9, _f64p), iters)
         H9 = np.empty(9, dtype=np.float32)
         return self.lib.ref_time_repeat_f32(ALGOS[algo], _ptr(src8, _f32p), _ptr(tar8, _f32p),
                                             _ptr(H9, _f32p), iters)
+
+    def time_pinned(self, algo: str, src, tar, cpus, reps: int, H=None) -> float:
+        """The streaming batch on len(cpus) threads, thread k pinned to logical CPU cpus[k],
+        each first-touching its own slice (NUMA-local pages); wall seconds of `reps` passes.
+        With H given, the results are copied there afterwards (untimed)."""
+        cpu_arr = (ctypes.c_int * len(cpus))(*cpus)
+        hp = _ptr(H, _f32p) if H is not None else None
+        return self.lib.ref_time_pinned_f32(ALGOS[algo], _ptr(src, _f32p), _ptr(tar, _f32p), hp,
+                                            src.shape[0], ctypes.cast(cpu_arr, ctypes.c_void_p),
+                                            len(cpus), reps)
 
 
 def same_bits(a: np.ndarray, b: np.ndarray) -> np.ndarray:

@@ -7,14 +7,18 @@
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <mutex>
 #include <unistd.h>
 #include <vector>
 
+#include "hg_host_ranges.hpp"
 #include "sks_homography.h"
 
 namespace {
+
+namespace host = hg::host;
 
 constexpr int kInvalid = (int)hipErrorInvalidValue;
 
@@ -62,50 +66,103 @@ int classify(View& v) {
     return 0;
 }
 
-// Registers the pages under the pageable views (overlapping or adjacent ranges merged,
-// so buffers cut from one allocation share a registration) and fills in their device
-// addresses.  The ranges registered are returned for hipHostUnregister.
-int register_pageable(std::vector<View*>& pageable, std::vector<char*>& registered) {
-    const uintptr_t pg = (uintptr_t)sysconf(_SC_PAGESIZE);
-    struct Range {
-        uintptr_t lo, hi;
-    };
-    std::vector<Range> r;
-    for (View* v : pageable) {
-        const uintptr_t p = reinterpret_cast<uintptr_t>(v->host);
-        r.push_back({p & ~(pg - 1), (p + v->bytes + pg - 1) & ~(pg - 1)});
+// Library-owned registrations of pageable host memory, shared between concurrent calls.
+//
+// Two calls may solve buffers that share pages (two threads, each with half of one numpy
+// or torch allocation).  A page the library registered for call A reads as pinned memory
+// (hipMemoryTypeHost) to call B, so B must not take it for user-pinned memory: B would
+// launch on it unprotected while A unregisters it under B's kernel.  Instead every call
+// classifies its buffers under the registry's mutex, treats a buffer that touches a
+// library-owned range as pageable, and holds a reference on each registration it uses
+// until its kernel has finished; the last reference unregisters.  A needed range that
+// overlaps registrations without lying inside one waits until they are released.
+struct Registration {
+    host::Range r;
+    char* dev;  // device address of r.lo
+    int refs;
+};
+
+struct Registry {
+    std::mutex mu;
+    std::condition_variable released;
+    std::vector<Registration> regs;
+
+    std::vector<host::Range> ranges() const {
+        std::vector<host::Range> out;
+        out.reserve(regs.size());
+        for (const Registration& x : regs) out.push_back(x.r);
+        return out;
     }
-    std::sort(r.begin(), r.end(), [](const Range& a, const Range& b) { return a.lo < b.lo; });
-    std::vector<Range> merged;
-    for (const Range& x : r) {
-        if (!merged.empty() && x.lo <= merged.back().hi)
-            merged.back().hi = std::max(merged.back().hi, x.hi);
-        else
-            merged.push_back(x);
+    bool owns_any(const void* p, size_t bytes) const {
+        const uintptr_t lo = reinterpret_cast<uintptr_t>(p);
+        const host::Range r{lo, lo + bytes};
+        for (const Registration& x : regs)
+            if (host::overlaps(r, x.r)) return true;
+        return false;
     }
-    for (const Range& m : merged) {
-        char* base = reinterpret_cast<char*>(m.lo);
-        hipError_t e = hipHostRegister(base, m.hi - m.lo, hipHostRegisterMapped);
-        if (e != hipSuccess) {
-            (void)hipGetLastError();
-            return (int)e;
+    // Drops one reference on each registration in `held` (their bases); the last one
+    // unregisters.  Caller holds `mu`.
+    void release(const std::vector<uintptr_t>& held) {
+        for (uintptr_t base : held) {
+            for (size_t j = 0; j < regs.size(); ++j) {
+                if (regs[j].r.lo != base) continue;
+                if (--regs[j].refs == 0) {
+                    (void)hipHostUnregister(reinterpret_cast<void*>(regs[j].r.lo));
+                    regs.erase(regs.begin() + (long)j);
+                }
+                break;
+            }
         }
-        registered.push_back(base);
-        void* d = nullptr;
-        if ((e = hipHostGetDevicePointer(&d, base, 0)) != hipSuccess) return (int)e;
+        released.notify_all();
+    }
+    // Registers (or shares) the pages under the pageable views and fills in their device
+    // addresses; `held` receives the registrations referenced.  Caller holds `lock`.
+    int acquire(std::vector<View*>& pageable, std::vector<uintptr_t>& held,
+                std::unique_lock<std::mutex>& lock) {
+        std::vector<host::Range> bytes;
         for (View* v : pageable) {
             const uintptr_t p = reinterpret_cast<uintptr_t>(v->host);
-            if (p >= m.lo && p < m.hi) v->dev = static_cast<char*>(d) + (p - m.lo);
+            bytes.push_back({p, p + v->bytes});
         }
+        std::vector<host::Range> need;
+        if (!host::page_ranges(bytes, (uintptr_t)sysconf(_SC_PAGESIZE), need)) return kInvalid;
+        std::vector<long> plan = host::plan(need, ranges());
+        while (host::any_conflict(plan)) {
+            released.wait(lock);
+            plan = host::plan(need, ranges());
+        }
+        for (size_t i = 0; i < need.size(); ++i) {
+            long j = plan[i];
+            if (j == host::kNew) {
+                char* base = reinterpret_cast<char*>(need[i].lo);
+                hipError_t e = hipHostRegister(base, need[i].hi - need[i].lo, hipHostRegisterMapped);
+                void* d = nullptr;
+                if (e == hipSuccess && (e = hipHostGetDevicePointer(&d, base, 0)) != hipSuccess)
+                    (void)hipHostUnregister(base);
+                if (e != hipSuccess) {
+                    release(held);
+                    held.clear();
+                    return (int)e;
+                }
+                regs.push_back({need[i], static_cast<char*>(d), 1});
+                j = (long)regs.size() - 1;
+            } else {
+                ++regs[(size_t)j].refs;
+            }
+            held.push_back(regs[(size_t)j].r.lo);
+            const Registration& g = regs[(size_t)j];
+            for (View* v : pageable) {
+                const uintptr_t p = reinterpret_cast<uintptr_t>(v->host);
+                if (p >= need[i].lo && p < need[i].hi) v->dev = g.dev + (p - g.r.lo);
+            }
+        }
+        return 0;
     }
-    return 0;
-}
+};
 
-// One registration at a time: two calls sharing pageable pages must not unregister
-// them under each other.  Calls on pinned or device memory never take it.
-std::mutex& registration_mutex() {
-    static std::mutex mu;
-    return mu;
+Registry& registry() {
+    static Registry r;
+    return r;
 }
 
 // The solvers with the host-memory cache policy (hg_kernels.hip, library-internal).
@@ -154,8 +211,14 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
     View v[3] = {{src, (size_t)n * 8 * sizeof(T)},
                  {tar, (size_t)n * 8 * sizeof(T)},
                  {H, (size_t)n * 9 * sizeof(T)}};
+    Registry& reg = registry();
+    std::unique_lock<std::mutex> lock(reg.mu);
     std::vector<View*> pageable;
     for (View& x : v) {
+        if (reg.owns_any(x.host, x.bytes)) {  // pages another call registered: pageable
+            pageable.push_back(&x);
+            continue;
+        }
         const int rc = classify(x);
         if (rc) return rc;
         if (!x.dev) pageable.push_back(&x);
@@ -172,12 +235,17 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
         const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
         return rc ? rc : (int)e;
     };
-    if (pageable.empty()) return run();
-    std::lock_guard<std::mutex> lock(registration_mutex());
-    std::vector<char*> registered;
-    int rc = register_pageable(pageable, registered);
-    if (!rc) rc = run();
-    for (char* base : registered) (void)hipHostUnregister(base);
+    std::vector<uintptr_t> held;
+    if (!pageable.empty()) {
+        const int rc = reg.acquire(pageable, held, lock);
+        if (rc) return rc;
+    }
+    lock.unlock();  // the solve itself runs unlocked: other calls may share the registrations
+    const int rc = run();
+    if (!held.empty()) {
+        lock.lock();
+        reg.release(held);
+    }
     return rc;
 }
 

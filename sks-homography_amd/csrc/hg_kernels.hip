@@ -18,6 +18,7 @@
 #include <cstdint>
 
 #include "hg_aos.hpp"
+#include "hg_launch.hpp"
 #include "hg_rect.hpp"
 #include "hg_soa.hpp"
 #include "hg_solvers.hpp"
@@ -238,8 +239,6 @@ inline unsigned generic_grid(int64_t n) {
     return (unsigned)(want < 8192 ? (want > 0 ? want : 1) : 8192);
 }
 
-inline int launch_status() { return (int)hipGetLastError(); }
-
 // host = the buffers are host memory read and written over PCIe (hg_solve_host_*): the
 // non-temporal hints are about HBM / MALL residency and buy nothing there, so host batches
 // take the default policy -- which also keeps their 12 ms launches apart from the
@@ -254,32 +253,34 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
             aligned16(tar) && aligned16(H)) {
             // binary64, MALL-resident, mid-size: the 16-B register form (8 % ahead at 100 K)
             const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
-            solve_soa_vec<ALGO, NORM, T, kSoaG, false, false><<<g, kBlock, 0, s>>>(src, tar, H, n);
-        } else if (aligned_to<sizeof(T)>(src) && aligned_to<sizeof(T)>(tar) &&
-                   aligned_to<sizeof(T)>(H)) {
+            return launch(solve_soa_vec<ALGO, NORM, T, kSoaG, false, false>, g, kBlock, 0, s, src,
+                          tar, H, n);
+        }
+        if (aligned_to<sizeof(T)>(src) && aligned_to<sizeof(T)>(tar) && aligned_to<sizeof(T)>(H)) {
             // one problem per lane, one element-wide access per component row
             const int64_t blocks = ceil_div(n, kBlock);
             if (blocks > 0x7fffffffLL) return kErrInvalid;
             if (cached)
-                solve_soa_narrow<ALGO, NORM, T, sizeof(T), false>
-                    <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
-            else
-                solve_soa_narrow<ALGO, NORM, T, sizeof(T), true>
-                    <<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
-        } else
-            solve_generic<ALGO, NORM, T, true><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
-    } else if (aligned16(src) && aligned16(tar) && aligned16(H)) {
+                return launch(solve_soa_narrow<ALGO, NORM, T, sizeof(T), false>, (unsigned)blocks,
+                              kBlock, 0, s, src, tar, H, n);
+            return launch(solve_soa_narrow<ALGO, NORM, T, sizeof(T), true>, (unsigned)blocks,
+                          kBlock, 0, s, src, tar, H, n);
+        }
+        return launch(solve_generic<ALGO, NORM, T, true>, generic_grid(n), kBlock, 0, s, src, tar,
+                      H, n);
+    }
+    if (aligned16(src) && aligned16(tar) && aligned16(H)) {
         constexpr int P = kAosP<T>;
         const int64_t blocks = aos_grid<T, P, kAosFlags>(n);
         if (blocks > 0x7fffffffLL) return kErrInvalid;
         if (cached)
-            solve_aos<ALGO, NORM, T, P, kAosCachedFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
-        else
-            solve_aos<ALGO, NORM, T, P, kAosFlags><<<(unsigned)blocks, kBlock, 0, s>>>(src, tar, H, n);
-    } else {
-        solve_generic<ALGO, NORM, T, false><<<generic_grid(n), kBlock, 0, s>>>(src, tar, H, n);
+            return launch(solve_aos<ALGO, NORM, T, P, kAosCachedFlags>, (unsigned)blocks, kBlock, 0,
+                          s, src, tar, H, n);
+        return launch(solve_aos<ALGO, NORM, T, P, kAosFlags>, (unsigned)blocks, kBlock, 0, s, src,
+                      tar, H, n);
     }
-    return launch_status();
+    return launch(solve_generic<ALGO, NORM, T, false>, generic_grid(n), kBlock, 0, s, src, tar, H,
+                  n);
 }
 
 template <int ALGO, typename T>
@@ -301,8 +302,7 @@ template <int ALGO, bool NORM, typename T, bool SOA>
 int launch_grouped_chunk(const GroupArgs<T>& g, hipStream_t s) {
     const uint32_t blocks = g.first_block[g.count];
     if (blocks == 0) return 0;
-    solve_grouped<ALGO, NORM, T, SOA><<<blocks, kBlock, 0, s>>>(g);
-    return launch_status();
+    return launch(solve_grouped<ALGO, NORM, T, SOA>, blocks, kBlock, 0, s, g);
 }
 
 template <typename T>
@@ -381,17 +381,20 @@ int launch_rect(const float* src, const float* tar, float* H, int64_t B, const f
     const bool cached = B * 132 <= kMallResidentBytes;
     const bool vec = aligned16(src) && aligned16(tar) && aligned16(H);
     const unsigned g = (unsigned)blocks;
-#define HG_RECT(SQ, NT) \
-    tensor_aca_rect_kernel<P, true, SCALAR, SQ, NT><<<g, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv)
+#define HG_RECT(SQ, NT)                                                                       \
+    launch(tensor_aca_rect_kernel<P, true, SCALAR, SQ, NT>, g, kBlock, 0, s, src, tar, H, B, sp, \
+           dp, sv, dv)
+    int rc;
     if (vec && SCALAR && is_unit_ratio(dv)) {
-        if (cached) HG_RECT(true, false); else HG_RECT(true, true);
+        rc = cached ? HG_RECT(true, false) : HG_RECT(true, true);
     } else if (vec) {
-        if (cached) HG_RECT(false, false); else HG_RECT(false, true);
+        rc = cached ? HG_RECT(false, false) : HG_RECT(false, true);
     } else {  // unaligned views: per-lane loads and stores
-        tensor_aca_rect_kernel<P, false, SCALAR><<<g, kBlock, 0, s>>>(src, tar, H, B, sp, dp, sv, dv);
+        rc = launch(tensor_aca_rect_kernel<P, false, SCALAR>, g, kBlock, 0, s, src, tar, H, B, sp,
+                    dp, sv, dv);
     }
 #undef HG_RECT
-    return launch_status();
+    return rc;
 }
 
 template <typename T>
@@ -406,18 +409,12 @@ int launch_one(int algo, const T* src, const T* tar, T* H, int flags, void* stre
     }
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool norm = flags & HG_FLAG_NORMALIZE;
-#define HG_ONE(A, N)                                                                  \
-    do {                                                                              \
-        if (done) solve_one_signal_kernel<A, N, T><<<1, kWave, 0, s>>>(q, H, done, seq); \
-        else solve_one_kernel<A, N, T><<<1, kWave, 0, s>>>(q, H);                     \
-    } while (0)
-    if (algo == kACA) {
-        if (norm) HG_ONE(kACA, true); else HG_ONE(kACA, false);
-    } else {
-        if (norm) HG_ONE(kSKS, true); else HG_ONE(kSKS, false);
-    }
+#define HG_ONE(A, N)                                                                         \
+    (done ? launch(solve_one_signal_kernel<A, N, T>, 1, kWave, 0, s, q, H, done, seq)       \
+          : launch(solve_one_kernel<A, N, T>, 1, kWave, 0, s, q, H))
+    if (algo == kACA) return norm ? HG_ONE(kACA, true) : HG_ONE(kACA, false);
+    return norm ? HG_ONE(kSKS, true) : HG_ONE(kSKS, false);
 #undef HG_ONE
-    return launch_status();
 }
 
 }  // namespace hg
@@ -535,32 +532,29 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
         const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
         const bool nt = B * 232 > hg::kMallResidentBytes;
 #define HG_RB(A, Bf, NT)                                                                      \
-    hg::tensor_aca_rect_backward_staged<A, Bf, NT><<<g, hg::kBlock, 0, s>>>(                  \
-        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
+    hg::launch(hg::tensor_aca_rect_backward_staged<A, Bf, NT>, g, hg::kBlock, 0, s, src, tar,   \
+               grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
         if (nt) {
-            if (ws && wd) HG_RB(true, true, true);
-            else if (ws) HG_RB(true, false, true);
-            else if (wd) HG_RB(false, true, true);
-            else HG_RB(false, false, true);
-        } else {
-            if (ws && wd) HG_RB(true, true, false);
-            else if (ws) HG_RB(true, false, false);
-            else if (wd) HG_RB(false, true, false);
-            else HG_RB(false, false, false);
+            if (ws && wd) return HG_RB(true, true, true);
+            if (ws) return HG_RB(true, false, true);
+            if (wd) return HG_RB(false, true, true);
+            return HG_RB(false, false, true);
         }
+        if (ws && wd) return HG_RB(true, true, false);
+        if (ws) return HG_RB(true, false, false);
+        if (wd) return HG_RB(false, true, false);
+        return HG_RB(false, false, false);
 #undef HG_RB
-        return hg::launch_status();
     }
     const unsigned g = hg::generic_grid(B);
 #define HG_RECT_BWD(A, Bf)                                                                    \
-    hg::tensor_aca_rect_backward_kernel<A, Bf><<<g, hg::kBlock, 0, s>>>(                      \
-        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
-    if (ws && wd) HG_RECT_BWD(true, true);
-    else if (ws) HG_RECT_BWD(true, false);
-    else if (wd) HG_RECT_BWD(false, true);
-    else HG_RECT_BWD(false, false);
+    hg::launch(hg::tensor_aca_rect_backward_kernel<A, Bf>, g, hg::kBlock, 0, s, src, tar, grad_H, \
+               B, scale, div, grad_src, grad_tar, grad_scale_div)
+    if (ws && wd) return HG_RECT_BWD(true, true);
+    if (ws) return HG_RECT_BWD(true, false);
+    if (wd) return HG_RECT_BWD(false, true);
+    return HG_RECT_BWD(false, false);
 #undef HG_RECT_BWD
-    return hg::launch_status();
 }
 
 int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,
@@ -577,17 +571,12 @@ int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* 
     const bool square = width == height && width != 0.f && std::isfinite(width);
     const bool cached = B * 76 <= hg::kMallResidentBytes;  // policy by size, as launch_solver
 #define HG_OFFSETS(V, SQ, NT)                                                                 \
-    hg::tensor_aca_offsets_kernel<P, V, SQ, NT><<<(unsigned)blocks, hg::kBlock, 0, s>>>(      \
-        corner, offsets, H, B, width, height)
-    if (vec && square) {
-        if (cached) HG_OFFSETS(true, true, false); else HG_OFFSETS(true, true, true);
-    } else if (vec) {
-        if (cached) HG_OFFSETS(true, false, false); else HG_OFFSETS(true, false, true);
-    } else {
-        HG_OFFSETS(false, false, true);  // unaligned views: per-lane loads and stores
-    }
+    hg::launch(hg::tensor_aca_offsets_kernel<P, V, SQ, NT>, (unsigned)blocks, hg::kBlock, 0, s, \
+               corner, offsets, H, B, width, height)
+    if (vec && square) return cached ? HG_OFFSETS(true, true, false) : HG_OFFSETS(true, true, true);
+    if (vec) return cached ? HG_OFFSETS(true, false, false) : HG_OFFSETS(true, false, true);
+    return HG_OFFSETS(false, false, true);  // unaligned views: per-lane loads and stores
 #undef HG_OFFSETS
-    return hg::launch_status();
 }
 
 int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets,
@@ -604,21 +593,18 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
         const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
         const bool nt = B * 116 > hg::kMallResidentBytes;
 #define HG_OB(C, NT)                                                                          \
-    hg::tensor_aca_offsets_backward_staged<C, NT><<<g, hg::kBlock, 0, s>>>(                   \
-        corner, offsets, grad_H, B, width, height, grad_offsets, grad_corner)
-        if (grad_corner) { if (nt) HG_OB(true, true); else HG_OB(true, false); }
-        else { if (nt) HG_OB(false, true); else HG_OB(false, false); }
+    hg::launch(hg::tensor_aca_offsets_backward_staged<C, NT>, g, hg::kBlock, 0, s, corner,      \
+               offsets, grad_H, B, width, height, grad_offsets, grad_corner)
+        if (grad_corner) return nt ? HG_OB(true, true) : HG_OB(true, false);
+        return nt ? HG_OB(false, true) : HG_OB(false, false);
 #undef HG_OB
-        return hg::launch_status();
     }
     const unsigned g = hg::generic_grid(B);
     if (grad_corner)
-        hg::tensor_aca_offsets_backward_kernel<true><<<g, hg::kBlock, 0, s>>>(
-            corner, offsets, grad_H, B, width, height, grad_offsets, grad_corner);
-    else
-        hg::tensor_aca_offsets_backward_kernel<false><<<g, hg::kBlock, 0, s>>>(
-            corner, offsets, grad_H, B, width, height, grad_offsets, nullptr);
-    return hg::launch_status();
+        return hg::launch(hg::tensor_aca_offsets_backward_kernel<true>, g, hg::kBlock, 0, s, corner,
+                          offsets, grad_H, B, width, height, grad_offsets, grad_corner);
+    return hg::launch(hg::tensor_aca_offsets_backward_kernel<false>, g, hg::kBlock, 0, s, corner,
+                      offsets, grad_H, B, width, height, grad_offsets, nullptr);
 }
 
 int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
@@ -626,10 +612,8 @@ int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offse
     if (count < 0) return hg::kErrInvalid;
     if (count == 0) return 0;
     if (!out) return hg::kErrInvalid;
-    hg::fill_uniform_kernel<<<hg::generic_grid(count), hg::kBlock, 0,
-                              reinterpret_cast<hipStream_t>(stream)>>>(out, count, seed, offset,
-                                                                       lo, hi);
-    return hg::launch_status();
+    return hg::launch(hg::fill_uniform_kernel, hg::generic_grid(count), hg::kBlock, 0,
+                      reinterpret_cast<hipStream_t>(stream), out, count, seed, offset, lo, hi);
 }
 
 int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
@@ -639,9 +623,9 @@ int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream) {
     const int64_t n16 = bytes / 16;
     const int64_t want = hg::ceil_div(n16, hg::kBlock * 4);
     const unsigned g = (unsigned)(want < 16384 ? (want > 0 ? want : 1) : 16384);
-    hg::stream_copy_kernel<<<g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        reinterpret_cast<const hg::u32x4*>(src), reinterpret_cast<hg::u32x4*>(dst), n16);
-    return hg::launch_status();
+    return hg::launch(hg::stream_copy_kernel, g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream),
+                      reinterpret_cast<const hg::u32x4*>(src), reinterpret_cast<hg::u32x4*>(dst),
+                      n16);
 }
 
 int hg_solve_one_f32(int algo, const float* src, const float* tar, float* H, int flags,
@@ -661,10 +645,12 @@ int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stre
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const int64_t chunks = hg::ceil_div(cols, hg::kSumChunk);
     if (chunks > 0x7fffffffLL) return hg::kErrInvalid;
-    if (chunks > 0)
-        hg::sum_rows_pass1<<<dim3((unsigned)chunks, (unsigned)rows), hg::kBlock, 0, s>>>(x, cols);
-    hg::sum_rows_pass2<<<(unsigned)rows, hg::kBlock, 0, s>>>(x, cols, chunks, out);
-    return hg::launch_status();
+    if (chunks > 0) {
+        const int rc = hg::launch(hg::sum_rows_pass1, dim3((unsigned)chunks, (unsigned)rows),
+                                  hg::kBlock, 0, s, x, cols);
+        if (rc) return rc;
+    }
+    return hg::launch(hg::sum_rows_pass2, (unsigned)rows, hg::kBlock, 0, s, x, cols, chunks, out);
 }
 
 const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }

@@ -21,9 +21,8 @@ int hg_fill_bits_u32(uint32_t* out, int64_t count, uint64_t seed, uint64_t offse
     if (!out) return (int)hipErrorInvalidValue;
     const int64_t want = (count + hg::kBlock - 1) / hg::kBlock;
     const unsigned g = (unsigned)(want < 8192 ? want : 8192);
-    hg::fill_bits_kernel<<<g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        out, count, seed, offset);
-    return (int)hipGetLastError();
+    return hg::launch(hg::fill_bits_kernel, g, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream),
+                      out, count, seed, offset);
 }
 
 int hg_sample_solve_f32(const float* pool_src, const float* pool_tar, uint32_t npool,
@@ -72,10 +71,10 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
     const int64_t blocks = (n + 2 * hg::kBlock - 1) / (2 * hg::kBlock);
     if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
     const float t2 = thresh * thresh;
-    hg::ransac_score_sgpr_kernel<8><<<(unsigned)blocks, hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream)>>>(
-        H, n, reinterpret_cast<const float2*>(pool_src), reinterpret_cast<const float2*>(pool_tar),
-        npool, t2, counts);
-    return (int)hipGetLastError();
+    return hg::launch(hg::ransac_score_sgpr_kernel<8>, (unsigned)blocks, hg::kBlock, 0,
+                      reinterpret_cast<hipStream_t>(stream), H, n,
+                      reinterpret_cast<const float2*>(pool_src),
+                      reinterpret_cast<const float2*>(pool_tar), npool, t2, counts);
 }
 
 }  // extern "C"

@@ -12,6 +12,7 @@
 #include <vector>
 
 #include "hg_aos.hpp"
+#include "hg_launch.hpp"
 #include "hg_solvers.hpp"
 #include "sks_homography.h"
 
@@ -325,12 +326,13 @@ inline int launch_sample_wide(const float2* ps, const float2* pt, uint32_t npool
     do {                                                                                       \
         auto k = sample_solve_lds_kernel<A, N, P, 1, WPB>;                                     \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;           \
-        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, ix, H, n, 0, 0);                   \
+        rc = launch(k, g, WPB * kWave, lds, s, ps, pt, npool, magic, ix, H, n, 0, 0);          \
     } while (0)
+    int rc;
     if (algo == 0) { if (norm) HG_SW(kACA, true); else HG_SW(kACA, false); }
     else { if (norm) HG_SW(kSKS, true); else HG_SW(kSKS, false); }
 #undef HG_SW
-    return (int)hipGetLastError();
+    return rc;
 }
 
 // Inlier test of one (hypothesis, correspondence) pair, division-free:
@@ -502,11 +504,11 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
         const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
         if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         const unsigned g = (unsigned)blocks;
-#define HG_SS(A, N) sample_solve_kernel<A, N, P><<<g, kBlock, 0, s>>>(ps, pt, npool, ix, H, n)
-        if (algo == 0) { if (norm) HG_SS(kACA, true); else HG_SS(kACA, false); }
-        else { if (norm) HG_SS(kSKS, true); else HG_SS(kSKS, false); }
+#define HG_SS(A, N) \
+    launch(sample_solve_kernel<A, N, P>, g, kBlock, 0, s, ps, pt, npool, ix, H, n, 0, 0)
+        if (algo == 0) return norm ? HG_SS(kACA, true) : HG_SS(kACA, false);
+        return norm ? HG_SS(kSKS, true) : HG_SS(kSKS, false);
 #undef HG_SS
-        return (int)hipGetLastError();
     }
     // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
     const int64_t tiles = (n + (int64_t)kWave * use_p - 1) / ((int64_t)kWave * use_p);
@@ -516,30 +518,32 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
     const uint64_t magic = mod64 ? fastmod64_magic(npool) : fastmod_magic(npool);
-#define HG_SL(PP, A, N) \
-    sample_solve_lds_kernel<A, N, PP><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
+#define HG_SL(PP, A, N)                                                                      \
+    launch(sample_solve_lds_kernel<A, N, PP>, g, kBlock, lds, s, ps, pt, npool, magic, ix, H, n, \
+           0, 0)
     if (use_p == 1) {
-        if (algo == 0) { if (norm) HG_SL(1, kACA, true); else HG_SL(1, kACA, false); }
-        else { if (norm) HG_SL(1, kSKS, true); else HG_SL(1, kSKS, false); }
-    } else if (mod64) {
-#define HG_SL64(A, N)                                                                        \
-    sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, true><<<g, kBlock, lds, s>>>( \
-        ps, pt, npool, magic, ix, H, n, 0)
-        if (algo == 0) { if (norm) HG_SL64(kACA, true); else HG_SL64(kACA, false); }
-        else { if (norm) HG_SL64(kSKS, true); else HG_SL64(kSKS, false); }
-#undef HG_SL64
-    } else if (!pf2) {
-        if (algo == 0) { if (norm) HG_SL(2, kACA, true); else HG_SL(2, kACA, false); }
-        else { if (norm) HG_SL(2, kSKS, true); else HG_SL(2, kSKS, false); }
-    } else {
-#define HG_SL2(A, N) \
-    sample_solve_lds_kernel<A, N, 2, 2><<<g, kBlock, lds, s>>>(ps, pt, npool, magic, ix, H, n)
-        if (algo == 0) { if (norm) HG_SL2(kACA, true); else HG_SL2(kACA, false); }
-        else { if (norm) HG_SL2(kSKS, true); else HG_SL2(kSKS, false); }
-#undef HG_SL2
+        if (algo == 0) return norm ? HG_SL(1, kACA, true) : HG_SL(1, kACA, false);
+        return norm ? HG_SL(1, kSKS, true) : HG_SL(1, kSKS, false);
     }
+    if (mod64) {
+#define HG_SL64(A, N)                                                                            \
+    launch(sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, true>, g, kBlock, lds, \
+           s, ps, pt, npool, magic, ix, H, n, 0, 0)
+        if (algo == 0) return norm ? HG_SL64(kACA, true) : HG_SL64(kACA, false);
+        return norm ? HG_SL64(kSKS, true) : HG_SL64(kSKS, false);
+#undef HG_SL64
+    }
+    if (!pf2) {
+        if (algo == 0) return norm ? HG_SL(2, kACA, true) : HG_SL(2, kACA, false);
+        return norm ? HG_SL(2, kSKS, true) : HG_SL(2, kSKS, false);
+    }
+#define HG_SL2(A, N)                                                                              \
+    launch(sample_solve_lds_kernel<A, N, 2, 2>, g, kBlock, lds, s, ps, pt, npool, magic, ix, H, n, 0, \
+           0)
+    if (algo == 0) return norm ? HG_SL2(kACA, true) : HG_SL2(kACA, false);
+    return norm ? HG_SL2(kSKS, true) : HG_SL2(kSKS, false);
+#undef HG_SL2
 #undef HG_SL
-    return (int)hipGetLastError();
 }
 
 // The seeded sampler's launcher.  Shipped shape: the LDS-pool kernel with P = 1 and 16 waves
@@ -562,13 +566,12 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
         const int64_t blocks = (n + (int64_t)kBlock * PG - 1) / ((int64_t)kBlock * PG);
         if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         const unsigned g = (unsigned)blocks;
-#define HG_SG(A, N)                                                                       \
-    sample_solve_kernel<A, N, PG, DRAWS><<<g, kBlock, 0, s>>>(ps, pt, npool, nullptr, H, n, \
-                                                              bits_base, odd)
-        if (algo == 0) { if (norm) HG_SG(kACA, true); else HG_SG(kACA, false); }
-        else { if (norm) HG_SG(kSKS, true); else HG_SG(kSKS, false); }
+#define HG_SG(A, N)                                                                          \
+    launch(sample_solve_kernel<A, N, PG, DRAWS>, g, kBlock, 0, s, ps, pt, npool, nullptr, H, n, \
+           bits_base, odd)
+        if (algo == 0) return norm ? HG_SG(kACA, true) : HG_SG(kACA, false);
+        return norm ? HG_SG(kSKS, true) : HG_SG(kSKS, false);
 #undef HG_SG
-        return (int)hipGetLastError();
     }
     // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
     const int64_t tiles = (n + (int64_t)kWave * P - 1) / ((int64_t)kWave * P);
@@ -582,12 +585,14 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     do {                                                                                    \
         auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64>;                   \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
-        k<<<g, WPB * kWave, lds, s>>>(ps, pt, npool, magic, nullptr, H, n, bits_base, odd); \
+        rc = launch(k, g, WPB * kWave, lds, s, ps, pt, npool, magic, nullptr, H, n, bits_base, \
+                    odd);                                                                   \
     } while (0)
+    int rc;
     if (algo == 0) { if (norm) HG_SD(kACA, true); else HG_SD(kACA, false); }
     else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }
 #undef HG_SD
-    return (int)hipGetLastError();
+    return rc;
 }
 
 // Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice

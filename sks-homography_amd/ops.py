@@ -179,7 +179,9 @@ def solve_grouped(algo: str, srcs, tars, normalize: bool = True, layout: str = "
         outs = list(outs)
         if len(outs) != len(srcs):
             raise ValueError("one out tensor per batch")
-        _require_device(*outs)
+        if _require_device(*outs) != dev:
+            # a kernel launched on `dev` writing another GPU's memory is a peer write or a fault
+            raise ValueError(f"out tensors must be on {dev}, the inputs' device")
         for o, m in zip(outs, ns):
             want = (m, 9) if lay == 0 else (9, m)
             if tuple(o.shape) != want or o.dtype is not dt or not o.is_contiguous():

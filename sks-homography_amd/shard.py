@@ -97,26 +97,41 @@ def scatter_blocks(full: Optional[torch.Tensor], n_total: int, world: int, rank:
 
 class SharedHostBatch:
     """An (n, 8) src, (n, 8) tar and (n, 9) H float32 batch in one shared-memory file
-    (``/dev/shm/<name>``) that every rank of the node maps.  Rank ``owner`` creates it
-    (``posix_fallocate`` reserves the pages up front, so a full /dev/shm fails here with
-    OSError instead of a SIGBUS later), the others attach after ``barrier()``.  Each rank
-    then solves its block with ``solve_block`` (the GPU reads and writes the shared pages
-    directly).  ``close()`` unmaps; the owner also unlinks."""
+    (``/dev/shm/<name>``) that every rank of the node maps.  Rank ``owner`` creates it; the
+    others attach after ``barrier()``.  Each rank then solves its block with ``solve_block``
+    (the GPU reads and writes the shared pages directly).  ``close()`` unmaps; the owner
+    also unlinks.
+
+    Page placement.  With ``world`` given, the owner only sizes the file and every rank
+    allocates the pages of its OWN block (its src, tar and H rows) with ``posix_fallocate``
+    -- on tmpfs the pages are allocated by the calling process, so under the default
+    first-touch policy they land on that rank's NUMA node (bench.py binds each rank to its
+    GPU's node before anything else).  A full /dev/shm fails there with OSError, not a
+    SIGBUS later; ``agree(ok) -> all_ok`` (e.g. a max-reduction over ranks) lets every rank
+    learn of another's failure.  Without ``world`` the owner allocates the whole file (one
+    process, or placement does not matter)."""
 
     def __init__(self, name: str, n: int, rank: int, barrier: Callable[[], None],
-                 owner: int = 0, directory: str = "/dev/shm"):
+                 owner: int = 0, directory: str = "/dev/shm", world: Optional[int] = None,
+                 agree: Optional[Callable[[bool], bool]] = None):
         if n < 0:
             raise ValueError(f"n must be >= 0, got {n}")
+        if world is not None and not 0 <= rank < world:
+            raise ValueError(f"rank {rank} outside world {world}")
         self.n, self.rank, self.owner = n, rank, owner
         self.path = os.path.join(directory, name)
         nbytes = max(n * (8 + 8 + 9) * 4, 4096)
+        self.nbytes = nbytes
         self._mm = None
         err = None
         if rank == owner:
             try:
                 fd = os.open(self.path, os.O_RDWR | os.O_CREAT | os.O_TRUNC, 0o600)
                 try:
-                    os.posix_fallocate(fd, 0, nbytes)
+                    if world is None:
+                        os.posix_fallocate(fd, 0, nbytes)
+                    else:
+                        os.ftruncate(fd, nbytes)  # sized, no pages yet: each rank allocates its own
                     self._mm = mmap.mmap(fd, nbytes)
                 finally:
                     os.close(fd)
@@ -128,19 +143,54 @@ class SharedHostBatch:
                     pass
         barrier()
         if rank == owner and err is not None:
+            if world is not None and agree is not None:
+                agree(False)
             raise err
         if rank != owner:
-            fd = os.open(self.path, os.O_RDWR)
+            try:
+                fd = os.open(self.path, os.O_RDWR)
+            except OSError:
+                if world is not None and agree is not None:
+                    agree(False)
+                raise
             try:
                 if os.fstat(fd).st_size < nbytes:
                     raise OSError(f"{self.path} holds fewer than {nbytes} bytes")
                 self._mm = mmap.mmap(fd, nbytes)
             finally:
                 os.close(fd)
+        if world is not None:
+            ok, err = True, None
+            try:
+                self.allocate_block(world)
+            except OSError as e:
+                ok, err = False, e
+            if agree is not None and not agree(ok) and ok:
+                err = OSError("another rank could not allocate its block of the shared batch")
+            if err is not None:
+                self.close()
+                raise err
         flat = torch.frombuffer(self._mm, dtype=torch.float32, count=nbytes // 4)
         self.src = flat[:n * 8].view(n, 8)
         self.tar = flat[n * 8:n * 16].view(n, 8)
         self.H = flat[n * 16:n * 25].view(n, 9)
+
+    def block_byte_ranges(self, world: int, rank: Optional[int] = None) -> List[Tuple[int, int]]:
+        """The file byte ranges of a rank's block: its src, tar and H rows."""
+        lo, hi = self.block(world, rank)
+        n = self.n
+        return [(lo * 32, hi * 32), (n * 32 + lo * 32, n * 32 + hi * 32),
+                (n * 64 + lo * 36, n * 64 + hi * 36)]
+
+    def allocate_block(self, world: int) -> None:
+        """Allocates the pages under this rank's block (posix_fallocate from this process)."""
+        fd = os.open(self.path, os.O_RDWR)
+        try:
+            for a, b in self.block_byte_ranges(world):
+                if b > a:
+                    os.posix_fallocate(fd, a, b - a)
+        finally:
+            os.close(fd)
 
     def block(self, world: int, rank: Optional[int] = None) -> Tuple[int, int]:
         return shard_range(self.n, world, self.rank if rank is None else rank)

@@ -100,7 +100,12 @@ def _shm_worker(rank, world, port, n_total, name, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     ge.load_package()
     from sks_homography_amd.shard import SharedHostBatch
-    b = SharedHostBatch(name, n_total, rank, dist.barrier)
+    def agree(ok):
+        t = torch.tensor([0.0 if ok else 1.0])
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return t.item() == 0.0
+
+    b = SharedHostBatch(name, n_total, rank, dist.barrier, world=world, agree=agree)
     lo, hi = b.block(world)
     # each rank writes its own block (as the GPU writes its H rows), rank 0 reads them all
     b.src[lo:hi] = torch.arange(lo, hi, dtype=torch.float32).unsqueeze(1)
@@ -121,7 +126,8 @@ def _shm_worker(rank, world, port, n_total, name, q):
 
 def test_shared_host_batch_gloo():
     """bench.py's host-resident batch: rank 0 creates the /dev/shm file, the others map
-    it, every rank's writes land in the one file, and it is gone after close()."""
+    it, each allocates its own block's pages, every rank's writes land in the one file, and
+    it is gone after close()."""
     world, n_total = 3, 1001
     name = f"sks_hg_test_{os.getpid()}"
     ctx = mp.get_context("spawn")
@@ -148,3 +154,97 @@ def test_shared_host_batch_full_shm_fails_cleanly(tmp_path):
     from sks_homography_amd.shard import SharedHostBatch
     with pytest.raises(OSError):
         SharedHostBatch("x", 1 << 40, 0, lambda: None, directory=str(tmp_path / "missing"))
+
+
+def _allocated(path):
+    """Bytes of memory a (tmpfs) file holds (st_blocks: fallocated pages count, holes not)."""
+    return os.stat(path).st_blocks * 512
+
+
+def _page_cover(ranges, page=4096):
+    """Page-rounded union of byte ranges, as sorted merged extents."""
+    r = sorted((a // page * page, -(-b // page) * page) for a, b in ranges if b > a)
+    out = []
+    for a, b in r:
+        if out and a <= out[-1][1]:
+            out[-1] = (out[-1][0], max(out[-1][1], b))
+        else:
+            out.append((a, b))
+    return out
+
+
+def _size(extents):
+    return sum(b - a for a, b in extents)
+
+
+def test_shared_host_batch_ranks_allocate_only_their_blocks():
+    """VERDICT r01 (do-this 8): with `world` given, the owner only sizes the file and each
+    rank allocates (first-touches) the pages of its own block -- src, tar and H rows -- so
+    on the GPU box those pages sit on the rank's NUMA node.  Ranks 0 and 1 of a world of 3
+    attach in turn: after each, the memory the file holds is exactly the pages under the
+    blocks attached so far (rank 2's pages are not allocated)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from sks_homography_amd.shard import SharedHostBatch
+    world, n = 3, 300_007
+    name = f"sks_hg_alloc_{os.getpid()}"
+    path = os.path.join("/dev/shm", name)
+    b0 = SharedHostBatch(name, n, 0, lambda: None, world=world)
+    try:
+        assert os.stat(path).st_size == n * 100
+        r0 = b0.block_byte_ranges(world, 0)
+        assert _allocated(path) == _size(_page_cover(r0))
+        b1 = SharedHostBatch(name, n, 1, lambda: None, world=world)
+        r1 = b0.block_byte_ranges(world, 1)
+        assert _allocated(path) == _size(_page_cover(r0 + r1))
+        assert _allocated(path) < n * 100 * 0.7  # rank 2's third is still unallocated
+        # the ranks see each other's writes through the one file
+        b1.H[n // 2] = 7.0
+        assert float(b0.H[n // 2][0]) == 7.0
+        b1.close()
+    finally:
+        b0.close()
+    assert not os.path.exists(path)
+
+
+def test_shared_host_batch_no_room_reaches_every_rank(tmp_path):
+    """A rank that cannot allocate its block raises OSError, and `agree` tells the others."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from sks_homography_amd.shard import SharedHostBatch
+    votes = []
+    with pytest.raises(OSError):
+        SharedHostBatch("x", 1 << 40, 0, lambda: None, directory=str(tmp_path / "missing"),
+                        world=2, agree=lambda ok: votes.append(ok) or False)
+    assert votes == [False]
+    # a healthy rank told by `agree` that a peer failed raises too, and leaves no file
+    name = f"sks_hg_agree_{os.getpid()}"
+    with pytest.raises(OSError, match="another rank"):
+        SharedHostBatch(name, 1000, 0, lambda: None, world=2, agree=lambda ok: False)
+    assert not os.path.exists(os.path.join("/dev/shm", name))
+
+
+def test_bind_numa_reads_kfd_topology(tmp_path, monkeypatch):
+    """bench.bind_numa's GPU lookup: GPUs in KFD node order (CPU nodes skipped), the PCI
+    address decoded from location_id/domain, visible-devices variables applied."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    base = tmp_path / "nodes"
+    props = [("cpu", 0, 0, 0), ("gpu", 304, 0x0500, 0), ("gpu", 304, 0x7500, 0),
+             ("gpu", 304, 0x8508, 1)]
+    for i, (_, simd, loc, dom) in enumerate(props):
+        (base / str(i)).mkdir(parents=True)
+        (base / str(i) / "properties").write_text(
+            f"cpu_cores_count 64\nsimd_count {simd}\nlocation_id {loc}\ndomain {dom}\n")
+    gpus = bench._kfd_gpu_bdfs(str(base))
+    assert gpus == ["0000:05:00.0", "0000:75:00.0", "0001:85:01.0"]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "2,0")
+    assert bench._visible(gpus, ("HIP_VISIBLE_DEVICES",)) == ["0001:85:01.0", "0000:05:00.0"]
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-abc")
+    assert bench._visible(gpus, ("HIP_VISIBLE_DEVICES",)) is None
+    assert bench._cpu_list("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]

@@ -1,17 +1,45 @@
 """A native C++ program (examples/dropin_main.cpp) calls the reference's sks::
-interface against the library on the GPU: single-problem calls on host and device
-pointers, the batch overload, and 8 host threads calling at once, all bit-consistent."""
+interface against the library on the GPU: every problem of a golden file (the reference's
+own outputs) through all four single-problem functions and the four batch overloads,
+bit for bit; then single-problem calls on host and device pointers, the batch overload,
+and 8 host threads calling at once, all bit-consistent."""
 import os
 import subprocess
 
+import numpy as np
 import pytest
 
-from conftest import ROOT
+from conftest import ROOT, load_golden
 
 pytestmark = pytest.mark.gpu
 
 
+def write_golden_bin(path, n_uniform=64):
+    """int64 n, then src/tar/aca/sks in f32, then the same in f64 (dropin_main.cpp's format):
+    the first n_uniform problems of cpp_uniform.npz and all 64 edge cases of cpp_edge.npz
+    (duplicates, collinear, +-Inf, NaN, subnormals), outputs of the compiled reference."""
+    u = load_golden("cpp_uniform.npz")
+    e = load_golden("cpp_edge.npz")
+    k = n_uniform
+    parts32 = [np.concatenate([u["src_f32"][:k], e["src"]]), np.concatenate([u["tar_f32"][:k], e["tar"]]),
+               np.concatenate([u["aca_f32"][:k], e["aca"]]), np.concatenate([u["sks_f32"][:k], e["sks"]])]
+    parts64 = [np.concatenate([u["src_f64"][:k], e["src_f64"]]),
+               np.concatenate([u["tar_f64"][:k], e["tar_f64"]]),
+               np.concatenate([u["aca_f64"][:k], e["aca_f64"]]),
+               np.concatenate([u["sks_f64"][:k], e["sks_f64"]])]
+    n = parts32[0].shape[0]
+    with open(path, "wb") as f:
+        f.write(np.int64(n).tobytes())
+        for a in parts32:
+            f.write(np.ascontiguousarray(a, np.float32).tobytes())
+        for a in parts64:
+            f.write(np.ascontiguousarray(a, np.float64).tobytes())
+    return n
+
+
 def test_cpp_dropin_program(pkg, dev, tmp_path):
+    gold = tmp_path / "golden.bin"
+    n = write_golden_bin(gold)
     libdir = os.path.dirname(pkg._lib.LIB_PATH)
     exe = tmp_path / "dropin"
     subprocess.run(["g++", "-std=c++17", f"-I{ROOT}/include", "-I/opt/rocm/include",
@@ -19,8 +47,9 @@ def test_cpp_dropin_program(pkg, dev, tmp_path):
                     f"-L{libdir}", "-lsks_homography_amd", f"-Wl,-rpath,{libdir}",
                     "-L/opt/rocm/lib", "-lamdhip64", "-Wl,-rpath,/opt/rocm/lib", "-pthread", "-o", str(exe)],
                    check=True)
-    r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120)
+    r = subprocess.run([str(exe), str(gold)], capture_output=True, text=True, timeout=120)
     assert r.returncode == 0, r.stdout + r.stderr
+    assert f"golden ok: {n} problems" in r.stdout
     assert "dropin ok" in r.stdout
 
 

@@ -130,6 +130,51 @@ def test_host_threads_at_once(pkg, dev):
     assert not bad
 
 
+def test_host_threads_share_one_pageable_allocation(pkg, dev):
+    """threads solving slices of ONE pageable allocation.  Neighbouring
+    slices share the pages at their boundaries, so one call finds pages another call
+    registered (they read as pinned memory); the library must treat them as its own
+    registration -- shared, reference-counted, unregistered only after the last kernel that
+    uses them has finished -- and never as user-pinned memory.  Each thread also checks its
+    neighbours' rows stay untouched, and the pages are unregistered at the end."""
+    k, n = 8, 20011  # 20011 * 32 B and * 36 B: slice edges fall inside pages
+    ds, dt = _inputs(pkg, dev, k * n, torch.float32, "aos", off=555)
+    want = pkg.solve("aca", ds, dt).cpu()
+    src, tar = ds.cpu(), dt.cpu()  # one pageable allocation each
+    H = torch.full((k * n, 9), float("nan"))
+    bad = []
+    start = threading.Barrier(k)
+
+    def work(i):
+        lo, hi = i * n, (i + 1) * n
+        start.wait()
+        for it in range(12):
+            # alternate the slice shape so registrations overlap in changing ways: the
+            # whole slice, then its two halves in turn
+            if it % 3 == 0:
+                pkg.solve_host("aca", src[lo:hi], tar[lo:hi], out=H[lo:hi])
+            else:
+                mid = lo + n // 2 + (it % 2)
+                pkg.solve_host("aca", src[lo:mid], tar[lo:mid], out=H[lo:mid])
+                pkg.solve_host("aca", src[mid:hi], tar[mid:hi], out=H[mid:hi])
+            if not torch.equal(_bits(H[lo:hi]), _bits(want[lo:hi])):
+                bad.append((i, it))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(k)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad
+    assert torch.equal(_bits(H), _bits(want))
+    hip = _hip()
+    attrs = ctypes.create_string_buffer(256)
+    for p in (src.data_ptr(), tar.data_ptr() + 4096 * 7, H.data_ptr() + 36 * n):
+        rc = hip.hipPointerGetAttributes(attrs, ctypes.c_void_p(p))
+        hip.hipGetLastError()
+        assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the calls"
+
+
 def test_host_full_size(pkg, dev):
     """BASELINE configs[1] size, 10 M problems, from pageable memory."""
     n = 10_000_000

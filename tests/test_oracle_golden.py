@@ -126,8 +126,31 @@ def test_uniform_stream_known_values(oracle):
     b = oracle.fill_uniform(8, 11, 8)
     np.testing.assert_array_equal(a[8:], b)
     assert a.dtype == np.float32 and (a >= 0).all() and (a < 1024).all()
-    # a pinned value so the generator cannot drift silently
-    assert a[:4].tolist() == pytest.approx(oracle.fill_uniform(4, 11, 0).tolist())
+
+
+@pytest.mark.parametrize("seed", [11, 3])
+@pytest.mark.parametrize("offset", [0, 2**33 + 7])
+def test_uniform_stream_vs_independent_restatement(oracle, seed, offset):
+    """The input stream of every bench and parity batch (oracle_fill_uniform_f32, the GPU's
+    hg_fill_uniform_f32) against tests/restate_streams.py, which shares no code with it:
+    the first 10**5 values bit for bit (numpy uint64 restatement), the first 2000 also
+    through the literal Python-integer statement; then lo/hi other than the default."""
+    import restate_streams as rs
+    got = oracle.fill_uniform(100_000, seed, offset)
+    np.testing.assert_array_equal(got.view(np.uint32), rs.uniform_f32(100_000, seed, offset).view(np.uint32))
+    np.testing.assert_array_equal(got[:2000].view(np.uint32),
+                                  rs.uniform_f32_pyint(2000, seed, offset).view(np.uint32))
+    got = oracle.fill_uniform(4099, seed, offset, -3000.0, 3000.0)
+    np.testing.assert_array_equal(got.view(np.uint32),
+                                  rs.uniform_f32(4099, seed, offset, -3000.0, 3000.0).view(np.uint32))
+
+
+def test_uniform_stream_counter_wraps(oracle):
+    """Counters wrap mod 2**64 (offsets near the top of the range)."""
+    import restate_streams as rs
+    off = (1 << 64) - 5 - (11 * rs.K_UNIFORM) % (1 << 64)
+    got = oracle.fill_uniform(64, 11, off % (1 << 64))
+    np.testing.assert_array_equal(got.view(np.uint32), rs.uniform_f32(64, 11, off % (1 << 64)).view(np.uint32))
 
 
 def _functional_rect(src, tar, scale, div):

@@ -31,7 +31,13 @@ lscpu > "$OUT/lscpu.txt" 2>&1 || true
 for step in $STEPS; do
     case "$step" in
         smoke) run smoke 300 python __graft_entry__.py smoke ;;
-        tests) run pytest_gpu 900 python -m pytest tests -m gpu -q -p no:cacheprovider ;;
+        lasterror) run lasterror 60 tools/_build/probe_lasterror ;;
+        cpuprobe) run cpuprobe 60 bash tools/cpu_probe.sh ;;
+        cpubase) run cpubase 300 python -c "import bench, json; print(json.dumps(bench.cpu_baseline(10_000_000)))" ;;
+        newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_kat.py \
+                tests/test_gpu_config5.py tests/test_gpu_host.py tests/test_gpu_cpp_api.py -m gpu -v \
+                -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         bench) run bench 600 python bench.py ;;
         prof)
             run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
