@@ -26,6 +26,18 @@ def _t(a, dev):
     return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
 
 
+def test_reference_build_travelled(orc):
+    """oracle/_ref (the reference's own ACA_SKS.cpp / GE.cpp, compiled in the build container
+    and shipped as a .so) must be present on the GPU box: the direct GPU-vs-reference
+    comparisons below and bench.py's `cpu_baseline` (kind "reference") depend on it.  Fails
+    loudly instead of letting them fall back to the restatement unnoticed."""
+    assert orc.RefOracle.available(), f"{orc.REF_SO} missing on this box"
+    ref = orc.RefOracle()
+    s = np.array([[0, 0, 200, 0, 50, 139, 181, 93]], np.float32)
+    t = np.array([[10, 12, 220, 5, 40, 160, 190, 110]], np.float32)
+    assert ref.solve("aca", s, t)[0, 8] == 1.0
+
+
 # ----------------------------------------------------------- golden fixtures
 @pytest.mark.parametrize("algo", ["aca", "sks"])
 @pytest.mark.parametrize("fixture,sk,tk,hk", [
