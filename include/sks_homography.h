@@ -8,9 +8,11 @@
  *     stream) and returns without synchronising,
  *   - returns 0 on success, otherwise a hipError_t code: hipErrorInvalidValue (1)
  *     for bad arguments (n < 0, NULL pointer with n > 0, unknown layout/flags),
- *     or the launch error.  Per-problem numerics are never checked: a degenerate
- *     quad yields Inf/NaN exactly as the reference does (ACA_SKS.cpp:101 always
- *     returns 0),
+ *     or the status of this call's own launch (hipLaunchKernel's return).  An error an
+ *     earlier, unrelated HIP call left pending on the calling thread is neither returned
+ *     nor cleared: it stays for its owner's hipGetLastError().  Per-problem numerics are
+ *     never checked: a degenerate quad yields Inf/NaN exactly as the reference does
+ *     (ACA_SKS.cpp:101 always returns 0),
  *   - is thread-safe (no global mutable state) and safe to capture in a hipGraph.
  *
  * A "problem" is 4 source + 4 target points ordered M, N, P, Q.
@@ -183,9 +185,12 @@ int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, 
  * there directly (zero-copy: both link directions busy at once, no device buffer): pinned
  * memory (hipHostMalloc / hipHostRegister with a device mapping) is used as it is;
  * pageable memory is registered (hipHostRegisterMapped, whole pages, overlapping buffers
- * merged) for the call and unregistered before it returns -- such calls are serialised
- * process-wide, and fail (hipErrorHostMemoryAlreadyRegistered ...) if the caller holds a
- * registration over part of those pages.  Device or managed pointers are accepted too.
+ * merged) for the call and unregistered once no call uses it any more: concurrent calls on
+ * buffers that share pages (slices of one allocation) share the library's registration,
+ * reference-counted, and run at once; a call whose pages only partly overlap another's
+ * registration waits for it.  A call fails (hipErrorHostMemoryAlreadyRegistered ...) if the
+ * caller itself holds a registration over part of those pages.  Device or managed pointers
+ * are accepted too.
  * SYNCHRONOUS, unlike every other entry point: H is complete on return.  stream NULL =
  * hipStreamPerThread when any buffer is host memory, else the legacy default stream.
  * Same layouts, flags, validation and bits as hg_<algo>_*; algo is an HG_ALGO_* id

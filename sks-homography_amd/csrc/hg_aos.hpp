@@ -26,6 +26,9 @@ enum : int {
     kLdsDma = 32,    // with kLdsLoad: global_load_lds_dwordx4 (LDS-DMA, no VGPR staging)
     kXcdMap = 64,    // one-shot grid: each XCD's blocks take one contiguous range of tiles
     kStSc1 = 128,    // staged H stores as buffer stores with sc1 (| nt with kNtStore); tune only
+    kLdSc0 = 256,    // LDS-DMA input loads with sc0 added to their cache policy; tune only
+    kLdSc1 = 512,    // ... with sc1 added; tune only
+    kSlabMajor = 1024,  // issue all of src's DMA pieces, then all of tar's (not interleaved); tune only
 };
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
@@ -74,19 +77,30 @@ __device__ __forceinline__ void wave_lds_sync() {
 // all loads of all slabs are issued before the single wait.  DMA: global_load_lds
 // _dwordx4 (no VGPR round trip); else global_load_dwordx4 + ds_write_b128.
 // Ends with the slabs visible to every lane of the wave.
-template <int kBytes, int NS, bool DMA, bool NT>
+// AUXX: extra cache-policy bits for the DMA (gfx950: sc0 = 1, nt = 2, sc1 = 16); SLAB_MAJOR:
+// issue slab 0's pieces, then slab 1's, instead of interleaving them piece by piece.
+template <int kBytes, int NS, bool DMA, bool NT, int AUXX = 0, bool SLAB_MAJOR = false>
 __device__ __forceinline__ void slabs_to_lds(const char* const (&g)[NS], char* const (&l)[NS],
                                              int lane) {
     static_assert(kBytes % (16 * kWave) == 0, "slab must be whole 1 KiB pieces");
     constexpr int kPieces = kBytes / (16 * kWave);
+    constexpr int kAux = (NT ? 2 : 0) | AUXX;
     if constexpr (DMA) {
-#pragma unroll
-        for (int c = 0; c < kPieces; ++c)
+        if constexpr (SLAB_MAJOR) {
 #pragma unroll
             for (int s = 0; s < NS; ++s)
-                __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g[s] + 16 * (c * kWave + lane)),
-                                                 (lds_ptr_t)(l[s] + 16 * c * kWave), 16, 0,
-                                                 NT ? 2 : 0);
+#pragma unroll
+                for (int c = 0; c < kPieces; ++c)
+                    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g[s] + 16 * (c * kWave + lane)),
+                                                     (lds_ptr_t)(l[s] + 16 * c * kWave), 16, 0, kAux);
+        } else {
+#pragma unroll
+            for (int c = 0; c < kPieces; ++c)
+#pragma unroll
+                for (int s = 0; s < NS; ++s)
+                    __builtin_amdgcn_global_load_lds((gbl_ptr_t)(g[s] + 16 * (c * kWave + lane)),
+                                                     (lds_ptr_t)(l[s] + 16 * c * kWave), 16, 0, kAux);
+        }
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else {
         u32x4 v[NS][kPieces];
@@ -227,7 +241,9 @@ __device__ __forceinline__ void aos_wave_tile(const T* __restrict__ src, const T
         const char* gt = reinterpret_cast<const char*>(tar + base * 8);
         const char* const gsrc[2] = {gs, gt};
         char* const lsrc[2] = {lds, lds + kSlab};
-        slabs_to_lds<kSlab, 2, (FL & kLdsDma) != 0, NTL>(gsrc, lsrc, lane);
+        constexpr int kAuxx = ((FL & kLdSc0) ? 1 : 0) | ((FL & kLdSc1) ? 16 : 0);
+        slabs_to_lds<kSlab, 2, (FL & kLdsDma) != 0, NTL, kAuxx, (FL & kSlabMajor) != 0>(gsrc, lsrc,
+                                                                                         lane);
 #pragma unroll
         for (int j = 0; j < P; ++j) {
             const int row = j * kWave + lane;

@@ -37,8 +37,10 @@ int classify(View& v) {
     hipPointerAttribute_t a{}, b{};
     const char* first = static_cast<const char*>(v.host);
     const char* last = first + v.bytes - 1;
+    // (ROCm 7 answers unregistered memory with success and type 0; an older runtime's failed
+    // probe leaves its own sticky error, cleared here -- see hg_sks_api.cpp)
     const bool ka = hipPointerGetAttributes(&a, first) == hipSuccess;
-    if (!ka) (void)hipGetLastError();  // unregistered host memory: clear the sticky error
+    if (!ka) (void)hipGetLastError();
     const bool kb = hipPointerGetAttributes(&b, last) == hipSuccess;
     if (!kb) (void)hipGetLastError();
     auto visible = [](bool known, const hipPointerAttribute_t& x) {

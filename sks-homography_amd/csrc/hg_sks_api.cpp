@@ -15,10 +15,15 @@ extern "C" int hg_internal_solve_one_signal_f64(int, const double*, const double
 
 namespace {
 
+// Pointer probes.  On ROCm 7 hipPointerGetAttributes succeeds on unregistered host memory
+// (type hipMemoryTypeUnregistered) and touches no error state, so an error the caller left
+// pending stays pending (tools/probe_lasterror.cpp, tests/test_gpu_errors.py).  Runtimes
+// that fail the probe instead (hipErrorInvalidValue) leave that error sticky: it is
+// cleared here, because it is the probe's own, not the caller's.
 bool is_device_pointer(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-        (void)hipGetLastError();  // unregistered host memory: clear the sticky error
+        (void)hipGetLastError();  // the failed probe's own error (older runtimes)
         return false;
     }
     return attr.type == hipMemoryTypeDevice || attr.type == hipMemoryTypeManaged;
@@ -143,7 +148,7 @@ int solve_one(T* src, T* tar, T* result) {
 bool is_pageable(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
-        (void)hipGetLastError();
+        (void)hipGetLastError();  // the failed probe's own error (older runtimes)
         return true;
     }
     return attr.type != hipMemoryTypeDevice && attr.type != hipMemoryTypeManaged &&

@@ -74,6 +74,13 @@ const Variant kVariants[] = {
     {"P2 lds-dma plain (cached)", launch_variant<2, kLdsLoad | kLdsDma>},
     {"P2 nt lds-dma, sc1|nt buffer stores", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kStSc1>},
     {"P2 nt lds-dma, sc1 buffer stores", launch_variant<2, kNtLoad | kLdsLoad | kLdsDma | kStSc1>},
+    // round 2: the input DMA's cache policy and issue order
+    {"P2 nt lds-dma, loads sc0|nt", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kLdSc0>},
+    {"P2 nt lds-dma, loads sc1|nt", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kLdSc1>},
+    {"P2 nt lds-dma, loads sc0|sc1|nt", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kLdSc0 | kLdSc1>},
+    {"P2 lds-dma, loads sc1, nt-st", launch_variant<2, kNtStore | kLdsLoad | kLdsDma | kLdSc1>},
+    {"P2 nt lds-dma, slab-major issue", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kSlabMajor>},
+    {"P4 nt lds-dma, slab-major issue", launch_variant<4, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kSlabMajor>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.
