@@ -25,6 +25,10 @@ HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
 REF_ROOT="${SKS_REFERENCE_ROOT:-/root/reference}"
 REF_SRC="$REF_ROOT/C++ Codes/modules/ACA_SKS.cpp"
 REF_GE="$REF_ROOT/C++ Codes/modules/GE.cpp"   # RHO-GE baseline (includes only GE.hpp -> OpenCV)
+# The reference's GPU kernels (cal_Homo_ACA/SKS/GPT/GE) are lines 81-507 of its CUDA harness;
+# the rest of that file needs OpenCV, cuRAND and nvcc's host toolchain and is not compiled.
+REF_CU="$REF_ROOT/C++ Codes/Runtime Test/GPU_Runtime Test/GPU_Runtime Test.cu"
+REF_CU_LINES="81,507p"
 CFLAGS=(-O2 -fPIC -ffp-contract=off -fno-fast-math)
 OUT_BUILD="$HERE/_build"
 OUT_REF="$HERE/_ref"
@@ -69,6 +73,33 @@ if [[ -f "$REF_SRC" ]]; then
         "$HERE/_ref/ge_native.o" "$HERE/_ref/ref_batch_native.o" -lpthread
     rm -f "$HERE/_ref/"*.o
     echo "built oracle/_ref/libsks_ref_native.so (speed build, not bit-exact)"
+fi
+
+# The reference's own CUDA kernels, compiled by hipcc for gfx950 straight from the file
+# (sed picks the kernel lines, oracle/ref_cu_driver.hip follows them in the same
+# translation unit and launches them as the reference's host code does).  -ffp-contract=off:
+# the reference's statements evaluated in order, every operation rounded on its own --
+# the convention of the C++ checker above.  Needs only hipcc; runs on the GPU box.
+if [[ -f "$REF_CU" && -z "$SAN" ]] && command -v hipcc > /dev/null; then
+    mkdir -p "$OUT_REF"
+    HIPCC="$(command -v hipcc)"
+    # the kernel section must still start and end where this recipe expects
+    if sed -n '81p' "$REF_CU" | grep -q '__global__ void cal_Homo_ACA' &&
+       sed -n '359p' "$REF_CU" | grep -q '__global__ void cal_Homo_GE' &&
+       sed -n '509p' "$REF_CU" | grep -q 'PYTHAG'; then
+        # one translation unit, assembled in a scratch file outside the repository:
+        # the HIP runtime header, the reference's kernel lines as they are, the driver
+        TU="$(mktemp -d)/refcu.hip"
+        { echo '#include <hip/hip_runtime.h>'; echo "#line 81 \"$REF_CU\"";
+          sed -n "$REF_CU_LINES" "$REF_CU"; echo '#line 1 "ref_cu_driver.hip"';
+          cat "$HERE/ref_cu_driver.hip"; } > "$TU"
+        "$HIPCC" --offload-arch="${SKS_AMD_ARCH:-gfx950}" -O2 -fPIC -shared -ffp-contract=off \
+            -fno-fast-math "$TU" -o "$OUT_REF/libsks_ref_cu.so"
+        rm -rf "$(dirname "$TU")"
+        echo "built oracle/_ref/libsks_ref_cu.so from $REF_CU (lines ${REF_CU_LINES%p})"
+    else
+        echo "reference CUDA file changed shape: oracle/_ref/libsks_ref_cu.so not built"
+    fi
 else
     echo "reference source absent; oracle/_ref not rebuilt"
 fi

@@ -217,6 +217,43 @@ class RefOracle:
                                             len(cpus), reps)
 
 
+REF_CU_SO = os.environ.get("SKS_REF_CU_SO", os.path.join(HERE, "_ref", "libsks_ref_cu.so"))
+
+
+class RefCuOracle:
+    """The reference's own GPU kernels -- cal_Homo_ACA / _SKS / _GE / _GPT, lines 81-507 of
+    "GPU_Runtime Test.cu" -- compiled by hipcc from the file where it lies
+    (oracle/build.sh, oracle/ref_cu_driver.hip; -ffp-contract=off) and launched as the
+    reference's host code launches them.  SoA binary64, unnormalised (GE/GPT: H[8] = 1).
+    Runs on the GPU (a checker: tests only)."""
+
+    ALGO = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
+
+    def __init__(self, path: str = REF_CU_SO):
+        if not os.path.exists(path):
+            raise FileNotFoundError(f"{path} missing (reference CUDA kernels not built here)")
+        lib = ctypes.CDLL(path)
+        lib.refcu_solve_f64.argtypes = [ctypes.c_int, _f64p, _f64p, _f64p, ctypes.c_int]
+        lib.refcu_solve_f64.restype = ctypes.c_int
+        self.lib = lib
+
+    @staticmethod
+    def available(path: str = REF_CU_SO) -> bool:
+        return os.path.exists(path)
+
+    def solve(self, algo: str, src: np.ndarray, tar: np.ndarray) -> np.ndarray:
+        """src/tar (8, n) float64 -> H (9, n) float64."""
+        src = np.ascontiguousarray(src, np.float64)
+        tar = np.ascontiguousarray(tar, np.float64)
+        n = src.shape[1]
+        H = np.empty((9, n), np.float64)
+        rc = self.lib.refcu_solve_f64(self.ALGO[algo], _ptr(src, _f64p), _ptr(tar, _f64p),
+                                      _ptr(H, _f64p), n)
+        if rc != 0:
+            raise RuntimeError(f"refcu_solve_f64({algo}) failed with hipError_t {rc}")
+        return H
+
+
 def same_bits(a: np.ndarray, b: np.ndarray) -> np.ndarray:
     """Elementwise bit equality with every NaN equal to every NaN (payloads differ
     between x86 and CDNA: x86 propagates an operand's payload, the GPU may return
