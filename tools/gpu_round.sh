@@ -112,6 +112,13 @@ for step in $STEPS; do
             run dist2_deadline 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
                 --master-addr 127.0.0.1 --master-port 29523 bench.py --gpus 2 --steps 20 \
                 --warmup 2 --no-extras --dist-backend gloo --gather-deadline 0.001 ;;
+        dist8_small)
+            # eight gloo ranks sharing the one GPU, every section on, 1 M problems per rank: the
+            # N = 8 control path end to end (NUMA records, split / gather with 7 peers, the
+            # host-sharded batch allocated by 8 ranks) in a few minutes
+            run dist8_small 600 python -m torch.distributed.run --nnodes=1 --nproc-per-node 8 \
+                --master-addr 127.0.0.1 --master-port 29531 bench.py --gpus 8 --steps 20 \
+                --warmup 2 --problems-per-gpu 1000000 --dist-backend gloo --extras-deadline 500 ;;
         torchrun1)
             run torchrun1 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 1 \
                 --master-addr 127.0.0.1 --master-port 29519 bench.py --gpus 1 --steps 50 \
