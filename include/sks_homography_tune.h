@@ -4,6 +4,10 @@
  * kernel's memory schedule, the HBM ceiling streams, and cal_ACA's launch loop
  * (GPU_Runtime Test.cu:1166-1206) in native code.  Not part of the drop-in boundary
  * (include/sks_homography.h); every solver variant produces the shipped kernel's bits.
+ * Error reporting differs from the product library: these launchers return
+ * hipGetLastError() after a <<<>>> launch, so an error left pending by an earlier HIP
+ * call is reported (and consumed) here -- acceptable for measurement tools, which check
+ * every call; the product's launches return only their own status (csrc/hg_launch.hpp).
  */
 #ifndef SKS_HOMOGRAPHY_TUNE_H
 #define SKS_HOMOGRAPHY_TUNE_H
