@@ -475,6 +475,10 @@ def torch_tensor_aca_rect(src, tar, scale, div):
     return H
 
 
+# TensorACA rect in the reference's (B,3,4) layout: 48 B tar + 48 B src (whole records: the
+# two floats used, src[:,0,0] and src[:,1,0], touch every 32-B sector) + 36 B H
+RECT_LAYOUT_MIN_BYTES = 132
+
 # imgs/GPU-runtime.png (Table 8), N = 1M, FP64 SoA, unnamed CUDA GPU
 TABLE8_US = {"aca": 245.0, "sks": 436.0, "gpt": 8390.0, "ge": 589.0}
 # the same table's full rows, N = 1 .. 1M
@@ -870,7 +874,17 @@ def main():
         pr = torch.cuda.get_device_properties(d.dev)
         got = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
         numa["bdf_matches_device"] = bool(numa["bdf"]) and numa["bdf"].startswith(got)
-    except (AttributeError, RuntimeError):
+        if not numa["bdf_matches_device"]:
+            # /sys and HIP numbered the GPUs differently: bind this thread (and every thread
+            # started from now on) to the node of the device HIP actually gave the rank
+            node = _read(f"/sys/bus/pci/devices/{got}.0/numa_node")
+            cpus = sorted(set(_cpu_list(_read(f"/sys/devices/system/node/node{node}/cpulist")))
+                          & set(_ORIGINAL_AFFINITY or [])) if node and int(node) >= 0 else []
+            if cpus:
+                os.sched_setaffinity(0, cpus)
+                numa.update(node=int(node), bound_cpus=len(cpus), bdf=f"{got}.0",
+                            note="rebound after GPU init: /sys order differed from HIP's")
+    except (AttributeError, RuntimeError, ValueError):
         numa["bdf_matches_device"] = None
     pkg = ge.load_package()
     n = args.n
@@ -1078,6 +1092,11 @@ def main():
                 "large_batch": big, "large_us_per_call": round(ms_b * 1e3, 2),
                 "large_achieved_gbps": round(big * rb / (ms_b * 1e-3) / 1e9, 1),
                 "large_frac": round(big * rb / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                # the (B,3,4) contract's floor: the 2 src floats used sit 16 B apart in every
+                # 48-B record, so every 32-B sector of src is fetched (PMC: 1.0x of this count)
+                "layout_min_bytes_per_problem": RECT_LAYOUT_MIN_BYTES,
+                "large_layout_min_frac": round(
+                    big * RECT_LAYOUT_MIN_BYTES / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             }
             del bs_h, bt_h, Hb
             line["reference_layout"] = reference_layout(d, pkg)

@@ -149,16 +149,16 @@ class SharedHostBatch:
         if rank != owner:
             try:
                 fd = os.open(self.path, os.O_RDWR)
+                try:
+                    if os.fstat(fd).st_size < nbytes:
+                        raise OSError(f"{self.path} holds fewer than {nbytes} bytes")
+                    self._mm = mmap.mmap(fd, nbytes)
+                finally:
+                    os.close(fd)
             except OSError:
                 if world is not None and agree is not None:
-                    agree(False)
+                    agree(False)  # every rank votes exactly once, failure or not
                 raise
-            try:
-                if os.fstat(fd).st_size < nbytes:
-                    raise OSError(f"{self.path} holds fewer than {nbytes} bytes")
-                self._mm = mmap.mmap(fd, nbytes)
-            finally:
-                os.close(fd)
         if world is not None:
             ok, err = True, None
             try:

@@ -248,3 +248,24 @@ def test_bind_numa_reads_kfd_topology(tmp_path, monkeypatch):
     monkeypatch.setenv("HIP_VISIBLE_DEVICES", "GPU-abc")
     assert bench._visible(gpus, ("HIP_VISIBLE_DEVICES",)) is None
     assert bench._cpu_list("0-3,8,10-11") == [0, 1, 2, 3, 8, 10, 11]
+
+
+def test_shared_host_batch_attach_failures_vote_once(tmp_path):
+    """Every failure path of a non-owner rank still takes part in `agree` exactly once (a
+    missing vote would leave the other ranks waiting in the collective)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as ge
+    ge.load_package()
+    from sks_homography_amd.shard import SharedHostBatch
+    votes = []
+    with pytest.raises(OSError):  # the owner never created the file
+        SharedHostBatch("absent", 100, 1, lambda: None, directory=str(tmp_path), world=2,
+                        agree=lambda ok: votes.append(ok) or False)
+    assert votes == [False]
+    (tmp_path / "short").write_bytes(b"\0" * 16)  # a stale file too small for the batch
+    votes.clear()
+    with pytest.raises(OSError, match="fewer"):
+        SharedHostBatch("short", 100, 1, lambda: None, directory=str(tmp_path), world=2,
+                        agree=lambda ok: votes.append(ok) or False)
+    assert votes == [False]
