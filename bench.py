@@ -398,33 +398,38 @@ def cpu_baseline(n_sample: int):
         def timed(algo, eng, k, reps):
             return eng.time_batch(algo, src, tar, H, k, reps)
 
-    def rate(algo, eng, k, seconds):
+    def rate(algo, eng, k, seconds, tries=1):
+        """Best of `tries` timed runs of about `seconds` each (the host is shared: another
+        tenant's load only ever slows a run down)."""
         t1 = timed(algo, eng, k, 1)
         reps = max(1, int(seconds / max(t1, 1e-6)))
-        return n_sample * reps / timed(algo, eng, k, reps) / 1e6, reps
+        best = max(n_sample * reps / timed(algo, eng, k, reps) / 1e6 for _ in range(tries))
+        return best, reps
 
+    # methodology (ii)/(iii) of SURVEY 8(d): the streaming batch on 1, 2, 4 ... all cores
+    counts = sorted({min(1 << i, P) for i in range(P.bit_length() + 1)} | {P_eff})
+    sweep_f = {k: rate("aca", engine, k, 0.3, tries=2)[0] for k in counts}
+    sweep = {str(k): round(v, 1) for k, v in sweep_f.items()}
+    k_best = max(counts, key=lambda k: (sweep_f[k], -k))  # fastest thread count (fewest on ties)
     out = {}
     algos = ("aca", "sks", "ge") if kind == "reference" else ("aca", "sks")
     for algo in algos:
-        out[algo], out[algo + "_reps"] = rate(algo, engine, P_eff, 1.5)
+        out[algo], out[algo + "_reps"] = rate(algo, engine, k_best, 0.5, tries=3)
+    out["aca"] = max(out["aca"], sweep_f[k_best])
     verified = None
     if kind == "reference":  # the timed multi-core path computes what the reference computes
         Hp = np.empty_like(H)
-        engine.time_pinned("aca", src, tar, cores[:P_eff], 1, Hp)
+        engine.time_pinned("aca", src, tar, cores[:k_best], 1, Hp)
         verified = bool(np.array_equal(Hp.view(np.uint32), engine.solve("aca", src, tar).view(np.uint32)))
-    # methodology (ii)/(iii) of SURVEY 8(d): the streaming batch on 1, 2, 4 ... all cores
-    sweep = {}
-    for k in sorted({min(1 << i, P) for i in range(P.bit_length() + 1)}):
-        sweep[str(k)] = round(rate("aca", engine, k, 0.4)[0], 1)
     native = None
     if kind == "reference" and os.path.exists(orc.REF_NATIVE_SO) and orc.cpu_has_avx512():
         # the reference built for speed (not bit-exact): a stronger CPU yardstick beside the
         # bit-exact one; the GPU is never compared with anything but both
         fast = orc.RefOracle(orc.REF_NATIVE_SO)
         native = {"flags": "g++ -O3 -march=x86-64-v4 -ffp-contract=fast -flto (not bit-exact)",
-                  "threads": P_eff}
+                  "threads": k_best}
         for algo in ("aca", "sks"):
-            native[algo + "_value"] = round(rate(algo, fast, P_eff, 1.0)[0], 1)
+            native[algo + "_value"] = round(rate(algo, fast, k_best, 0.5, tries=2)[0], 1)
     single = {}
     if kind == "reference":
         # the reference's own CPU methodology (main.cpp:87-114): one set, 10 M calls, one core
@@ -435,20 +440,21 @@ def cpu_baseline(n_sample: int):
                 algo, src[0].astype(np.float64), tar[0].astype(np.float64), 10_000_000) / 1e7 * 1e6
         single = {k: round(v, 5) for k, v in single.items()}
         single["table5_us_msvc_O2"] = TABLE5_US
-    quota_note = (f"{P_eff} = this job's cgroup CPU quota (cpu.max); the host has {P} physical "
-                  f"cores, but more threads only share the same {P_eff} CPUs of time (see the "
-                  f"sweep)") if P_eff < P else f"all {P} physical cores"
+    quota_note = (f"the fastest point of the sweep 1 ... {P} threads; this job's cgroup CPU quota "
+                  f"(cpu.max) is {P_eff} CPUs of time on a host of {P} physical cores, so more "
+                  f"threads share the same time (a run may briefly burst past it)"
+                  ) if P_eff < P else f"the fastest point of the sweep 1 ... all {P} physical cores"
     rec = {
-        "value": out["aca"], "unit": "M homographies/s", "cores": P_eff, "kind": kind,
+        "value": out["aca"], "unit": "M homographies/s", "cores": k_best, "kind": kind,
         "sks_value": out["sks"], "ge_value": out.get("ge"),
         "sample": (f"AoS f32 normalised batch of {n_sample} problems (seed {SEED}, U[0,1024)), "
-                   f"{out['aca_reps']} passes ACA / {out['sks_reps']} SKS, one std::thread per "
-                   f"physical core, pinned, spread over the NUMA nodes, NUMA-local first-touch "
-                   f"slices; cores: {quota_note}"),
+                   f"best of 3 runs of {out['aca_reps']} passes ACA / {out['sks_reps']} SKS, one "
+                   f"std::thread per physical core, pinned, spread over the NUMA nodes, NUMA-local "
+                   f"first-touch slices; cores: {quota_note}"),
         "physical_cores": P, "cgroup_cpu_quota": quota,
         # every physical core at the measured per-core rate: an upper bound, not a measurement
         # (it ignores the DRAM bandwidth 100 B/H would need at that rate)
-        "all_physical_cores_linear_bound": round(out["aca"] / P_eff * P, 1),
+        "all_physical_cores_linear_bound": round(sweep_f[P_eff] / P_eff * P, 1),
         "all_core_output_bit_exact": verified,
         "single_core_same_points_us_per_H": single or None,
         "aca_thread_sweep_M_per_s": sweep,
