@@ -15,6 +15,9 @@ and the CPU oracle's restatement of the same four, on uniform, wall-pool and edg
 import numpy as np
 import pytest
 import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+from hypothesis.extra.numpy import arrays
 
 from conftest import load_golden
 
@@ -93,3 +96,20 @@ def test_reference_kernels_large_batch(orc, pkg, dev, refcu):
         want = refcu.solve(algo, s, t)
         got = pkg.solve(algo, ds, dt, normalize=False, layout="soa").cpu().numpy()
         assert orc.same_bits(got, want).all(), algo
+
+
+@settings(max_examples=20, deadline=None, suppress_health_check=list(HealthCheck))
+@given(arrays(np.float64, (16, 257), elements=st.floats(width=64, allow_nan=True,
+                                                        allow_infinity=True, allow_subnormal=True)))
+def test_arbitrary_doubles_equal_reference_kernels(orc, pkg, dev, refcu, batch):
+    """Arbitrary binary64 bit patterns (NaN, +-Inf, subnormals, huge and tiny values drawn by
+    hypothesis), 257 problems a draw: every solver's SoA output equals the reference
+    kernel's, NaN for NaN."""
+    s = np.ascontiguousarray(batch[:8])
+    t = np.ascontiguousarray(batch[8:])
+    ds, dt = torch.from_numpy(s).to(dev), torch.from_numpy(t).to(dev)
+    for algo in ALGOS:
+        want = refcu.solve(algo, s, t)
+        got = pkg.solve(algo, ds, dt, normalize=False, layout="soa").cpu().numpy()
+        ok = orc.same_bits(got, want)
+        assert ok.all(), f"{algo}: {int((~ok).sum())} differ"
