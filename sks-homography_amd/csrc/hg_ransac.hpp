@@ -55,12 +55,8 @@ static __global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __re
 
 // Where a hypothesis' four draws come from.
 constexpr int kDrawsIndexed = 0;  // row p of the (n,4) index array
-constexpr int kDrawsPaired = 1;   // seeded: fill_bits' stream generated in place, parity of
-                                  // the offset tested in the kernel (launchers dispatch it to
-                                  // one of the two below)
+constexpr int kDrawsPaired = 1;   // seeded: fill_bits' stream generated in place (shipped)
 constexpr int kDrawsSingle = 2;   // seeded, tune only: one hash per draw (the earlier stream)
-constexpr int kDrawsPairedEven = 3;  // kDrawsPaired with an even offset known at compile time
-constexpr int kDrawsPairedOdd = 4;   // ... an odd one (shipped: one instantiation per parity)
 
 // The 4 draws of hypothesis p: row p of the (n,4) index array, or -- seeded -- the same
 // four words generated in place: words offset + 4p ... + 3 of the stream, i.e. out[4p ..
@@ -69,17 +65,7 @@ constexpr int kDrawsPairedOdd = 4;   // ... an odd one (shipped: one instantiati
 // an odd offset shifts the four words across three hashes (a wave-uniform branch).
 template <int DRAWS>
 __device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, bool odd, int64_t p) {
-    if constexpr (DRAWS == kDrawsPairedEven || DRAWS == kDrawsPairedOdd) {
-        // the parity as a template constant: no branch, so no register merges after it
-        const uint64_t b = bits_base + 2 * (uint64_t)p;
-        const uint64_t z0 = mix64(b), z1 = mix64(b + 1);
-        if constexpr (DRAWS == kDrawsPairedEven)
-            return u32x4{word_half(z0, false), word_half(z0, true), word_half(z1, false),
-                         word_half(z1, true)};
-        const uint64_t z2 = mix64(b + 2);
-        return u32x4{word_half(z0, true), word_half(z1, false), word_half(z1, true),
-                     word_half(z2, false)};
-    } else if constexpr (DRAWS == kDrawsPaired) {
+    if constexpr (DRAWS == kDrawsPaired) {
         const uint64_t b = bits_base + 2 * (uint64_t)p;
         const uint64_t z0 = mix64(b), z1 = mix64(b + 1);
         if (!odd)
@@ -568,12 +554,11 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // seed * kBitsMul (draws4).  P, WPB, DRAWS, MOD64 and PF are open for the variant sweep
 // (hg_tune_sample_seeded).
 template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0>
-inline int launch_sample_seeded_impl(const float2* ps, const float2* pt, uint32_t npool,
-                                     uint64_t seed, uint64_t offset, float* H, int64_t n,
-                                     int algo, bool norm, hipStream_t s) {
+inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
+                                uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
+                                bool norm, hipStream_t s) {
     const uint64_t bits_base = DRAWS == kDrawsSingle ? seed * kBitsMul + offset
                                                      : seed * kBitsMul + (offset >> 1);
-    // (kDrawsPairedEven / Odd ignore `odd`: their parity is a template constant)
     const uint32_t odd = DRAWS == kDrawsSingle ? 0u : (uint32_t)(offset & 1);
     const size_t lds = sample_lds_bytes<P, WPB>(npool);
     if (lds > kSampleLdsOptIn) {
@@ -608,24 +593,6 @@ inline int launch_sample_seeded_impl(const float2* ps, const float2* pt, uint32_
     else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }
 #undef HG_SD
     return rc;
-}
-
-// Paired draws go to the instantiation for the offset's parity (kDrawsPairedEven / Odd):
-// same words, same bits, and the kernel carries no parity branch.
-template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0>
-inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
-                                uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
-                                bool norm, hipStream_t s) {
-    if constexpr (DRAWS == kDrawsPaired) {
-        if (offset & 1)
-            return launch_sample_seeded_impl<P, WPB, kDrawsPairedOdd, MOD64, PF>(
-                ps, pt, npool, seed, offset, H, n, algo, norm, s);
-        return launch_sample_seeded_impl<P, WPB, kDrawsPairedEven, MOD64, PF>(
-            ps, pt, npool, seed, offset, H, n, algo, norm, s);
-    } else {
-        return launch_sample_seeded_impl<P, WPB, DRAWS, MOD64, PF>(ps, pt, npool, seed, offset, H,
-                                                                   n, algo, norm, s);
-    }
 }
 
 // Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice

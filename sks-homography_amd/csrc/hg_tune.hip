@@ -624,8 +624,6 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 7: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 8: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 9: return launch_sample_seeded<2, 8, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        // round 2: the shipped shape with the offset's parity tested in the kernel (round 1)
-        case 10: return launch_sample_seeded_impl<1, 16, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -26,8 +26,7 @@ SEEDED = {0: "seeded P1, 16 waves/block, draws in place (shipped)", 1: "seeded P
           4: "seeded P2, 8 waves/block, 64-bit remainder",
           5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw",
           7: "seeded P2, 8 waves/block, draws in place", 8: "seeded P2, 4 waves/block, draws in place",
-          9: "seeded P2, 8 waves/block (previous shipped)",
-          10: "seeded P1, 16 waves/block, parity tested in the kernel (round-1 shipped)"}
+          9: "seeded P2, 8 waves/block (previous shipped)"}
 # KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
 SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
 OTHER_STREAM = (5, 6)  # one hash per draw: a different stream, not comparable bit for bit
@@ -52,9 +51,7 @@ def main():
     out = {}
     for n in ((1 << 22, 1 << 24) if SEEDED_ONLY else (1 << 20, 1 << 22, 1 << 24)):
         idx = pkg.fill_bits(n * 4, 11, 0, dev).view(n, 4)
-        only = os.environ.get("KB_SEEDED_VARIANTS")
-        seeded = [int(x) for x in only.split(",")] if only else list(SEEDED)
-        keys = ([0] if SEEDED_ONLY else list(NAMES)) + [("s", v) for v in seeded]
+        keys = ([0] if SEEDED_ONLY else list(NAMES)) + [("s", v) for v in SEEDED]
         outs = {v: torch.empty((n, 9), device=dev) for v in keys}
         st = torch.cuda.current_stream(dev).cuda_stream
 
