@@ -871,9 +871,11 @@ def main():
     args = parse()
     # before anything touches the GPU: this rank's CPUs and first-touch pages on its GPU's
     # NUMA node (the device index is LOCAL_RANK, as Dist picks it)
-    ndev = torch.cuda.device_count()  # counts devices without initialising HIP
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    numa = bind_numa(local if args.dist_backend == "nccl" else local % max(ndev, 1))
+    if args.dist_backend == "nccl":  # one GPU per rank: device index = LOCAL_RANK
+        numa = bind_numa(local)
+    else:  # gloo rehearsal: ranks share the devices (device_count does not initialise HIP here)
+        numa = bind_numa(local % max(torch.cuda.device_count(), 1))
     d = Dist(args.dist_backend)
     numa["rank"] = d.rank
     try:  # the device HIP gave this rank is the one bound to
