@@ -29,7 +29,22 @@ enum : int {
     kLdSc0 = 256,    // LDS-DMA input loads with sc0 added to their cache policy; tune only
     kLdSc1 = 512,    // ... with sc1 added; tune only
     kSlabMajor = 1024,  // issue all of src's DMA pieces, then all of tar's (not interleaved); tune only
+    kNoSolve = 2048,    // same loads and stores, no solver: H row = src row + tar[0] (the memory
+                        // pattern's own ceiling); tune only
 };
+
+// The solve of one problem, or -- with kNoSolve -- a copy with the same traffic and a
+// dependence on every loaded value (tune-only yardstick).
+template <int ALGO, bool NORM, int FL, typename T>
+__device__ __forceinline__ void tile_solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
+    if constexpr ((FL & kNoSolve) != 0) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) h[k] = s[k] + t[k];
+        h[8] = t[0];
+    } else {
+        solve<ALGO, NORM>(s, t, h);
+    }
+}
 
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 typedef __attribute__((address_space(1))) const void* gbl_ptr_t;
@@ -250,7 +265,7 @@ __device__ __forceinline__ void aos_wave_tile(const T* __restrict__ src, const T
             T s[8], t[8];
             __builtin_memcpy(s, lds + row * 8 * sizeof(T), 8 * sizeof(T));
             __builtin_memcpy(t, lds + kSlab + row * 8 * sizeof(T), 8 * sizeof(T));
-            solve<ALGO, NORM>(s, t, h[j]);
+            tile_solve<ALGO, NORM, FL>(s, t, h[j]);
         }
         wave_lds_sync();  // the output staging below reuses these bytes
     } else {
@@ -265,7 +280,7 @@ __device__ __forceinline__ void aos_wave_tile(const T* __restrict__ src, const T
 #pragma unroll
                 for (int k = 0; k < 8; ++k) s[k] = t[k] = T(0);
             }
-            solve<ALGO, NORM>(s, t, h[j]);
+            tile_solve<ALGO, NORM, FL>(s, t, h[j]);
         }
     }
 

@@ -81,6 +81,8 @@ const Variant kVariants[] = {
     {"P2 lds-dma, loads sc1, nt-st", launch_variant<2, kNtStore | kLdsLoad | kLdsDma | kLdSc1>},
     {"P2 nt lds-dma, slab-major issue", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kSlabMajor>},
     {"P4 nt lds-dma, slab-major issue", launch_variant<4, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kSlabMajor>},
+    // the shipped kernel's memory pattern with the solver replaced by a copy (not bit-exact by design)
+    {"P2 nt lds-dma, NO SOLVE (pattern ceiling)", launch_variant<2, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kNoSolve>},
 };
 
 // Streaming-copy variants for the bandwidth yardstick.
