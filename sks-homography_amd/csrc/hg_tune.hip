@@ -429,7 +429,8 @@ int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
 }
 
 // binary64 AoS sweep (tools/kbench_f64.py): 0 = P1 nt LDS-DMA (shipped), 1 = P2 nt LDS-DMA,
-// 2 = P1 nt register-staged loads, 3 = P1 LDS-DMA default cache policy.
+// 2 = P1 nt register-staged loads, 3 = P1 LDS-DMA default cache policy, 4 = variant 0's memory
+// pattern with the solver replaced by a copy (kNoSolve; not bit-exact by design).
 int hg_tune_aos_f64(int algo, int variant, const double* src, const double* tar, double* H,
                     int64_t n, void* stream) {
     if (n <= 0 || (algo != 0 && algo != 1)) return (int)hipErrorInvalidValue;
@@ -445,6 +446,7 @@ int hg_tune_aos_f64(int algo, int variant, const double* src, const double* tar,
         case 1: HG_F64(2, kNtLoad | kNtStore | kLdsLoad | kLdsDma); break;
         case 2: HG_F64(1, kNtLoad | kNtStore | kLdsLoad); break;
         case 3: HG_F64(1, kLdsLoad | kLdsDma); break;
+        case 4: HG_F64(1, kNtLoad | kNtStore | kLdsLoad | kLdsDma | kNoSolve); break;  // pattern only
         default: return (int)hipErrorInvalidValue;
     }
 #undef HG_F64

@@ -13,7 +13,7 @@ sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
 NAMES = {0: "P1 nt lds-dma (shipped)", 1: "P2 nt lds-dma", 2: "P1 nt register-staged",
-         3: "P1 lds-dma default policy"}
+         3: "P1 lds-dma default policy", 4: "P1 nt lds-dma, NO SOLVE (pattern ceiling)"}
 
 
 def main():
