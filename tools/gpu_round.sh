@@ -34,6 +34,7 @@ for step in $STEPS; do
         lasterror) run lasterror 60 tools/_build/probe_lasterror ;;
         cpuprobe) run cpuprobe 60 bash tools/cpu_probe.sh ;;
         crossover) run crossover 400 python tools/crossover.py ;;
+        chunk_probe) run chunk_probe 300 python tools/chunk_probe.py ;;
         cpubase) run cpubase 300 python -c "import bench, json; print(json.dumps(bench.cpu_baseline(10_000_000)))" ;;
         newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_kat.py \
                 tests/test_gpu_config5.py tests/test_gpu_host.py tests/test_gpu_cpp_api.py -m gpu -v \
