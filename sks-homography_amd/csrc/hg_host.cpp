@@ -80,7 +80,6 @@ int classify(View& v) {
 // overlaps registrations without lying inside one waits until they are released.
 struct Registration {
     host::Range r;
-    char* dev;  // device address of r.lo
     int refs;
 };
 
@@ -136,26 +135,35 @@ struct Registry {
         for (size_t i = 0; i < need.size(); ++i) {
             long j = plan[i];
             if (j == host::kNew) {
+                // portable: a registration may be shared with a call on another device
                 char* base = reinterpret_cast<char*>(need[i].lo);
-                hipError_t e = hipHostRegister(base, need[i].hi - need[i].lo, hipHostRegisterMapped);
-                void* d = nullptr;
-                if (e == hipSuccess && (e = hipHostGetDevicePointer(&d, base, 0)) != hipSuccess)
-                    (void)hipHostUnregister(base);
+                const hipError_t e = hipHostRegister(base, need[i].hi - need[i].lo,
+                                                     hipHostRegisterMapped | hipHostRegisterPortable);
                 if (e != hipSuccess) {
                     release(held);
                     held.clear();
                     return (int)e;
                 }
-                regs.push_back({need[i], static_cast<char*>(d), 1});
+                regs.push_back({need[i], 1});
                 j = (long)regs.size() - 1;
             } else {
                 ++regs[(size_t)j].refs;
             }
             held.push_back(regs[(size_t)j].r.lo);
-            const Registration& g = regs[(size_t)j];
+            // the address the CURRENT device uses for this registration (asked per call: the
+            // registration may have been made while another device was current)
+            void* d = nullptr;
+            const hipError_t e =
+                hipHostGetDevicePointer(&d, reinterpret_cast<void*>(regs[(size_t)j].r.lo), 0);
+            if (e != hipSuccess) {
+                release(held);
+                held.clear();
+                return (int)e;
+            }
             for (View* v : pageable) {
                 const uintptr_t p = reinterpret_cast<uintptr_t>(v->host);
-                if (p >= need[i].lo && p < need[i].hi) v->dev = g.dev + (p - g.r.lo);
+                if (p >= need[i].lo && p < need[i].hi)
+                    v->dev = static_cast<char*>(d) + (p - regs[(size_t)j].r.lo);
             }
         }
         return 0;
