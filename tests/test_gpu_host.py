@@ -175,6 +175,48 @@ def test_host_threads_share_one_pageable_allocation(pkg, dev):
         assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the calls"
 
 
+def test_host_threads_random_overlapping_slices(pkg, dev):
+    """Stress of the shared registrations: 6 threads, each solving 40 random (possibly
+    overlapping in pages, never in rows) slices of one pageable allocation, sizes from 1
+    problem to 40 K, f32 AoS; every row written equals the device solve, untouched rows
+    stay NaN, and no registration survives."""
+    import random
+    n = 300_007
+    ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=4242)
+    want = pkg.solve("aca", ds, dt).cpu()
+    src, tar = ds.cpu(), dt.cpu()
+    H = torch.full((n, 9), float("nan"))
+    k = 6
+    per = n // k
+    bad = []
+
+    def work(i):
+        rng = random.Random(i)
+        lo0, hi0 = i * per, (i + 1) * per if i < k - 1 else n
+        for _ in range(40):
+            a = rng.randrange(lo0, hi0)
+            b = min(hi0, a + rng.choice((1, 7, 100, 4096, 40_000)))
+            pkg.solve_host("aca", src[a:b], tar[a:b], out=H[a:b])
+            if not torch.equal(_bits(H[a:b]), _bits(want[a:b])):
+                bad.append((i, a, b))
+
+    th = [threading.Thread(target=work, args=(i,)) for i in range(k)]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad[:5]
+    done = ~torch.isnan(H[:, 0])
+    assert torch.equal(_bits(H[done]), _bits(want[done]))
+    assert done.sum() > 0
+    hip = _hip()
+    attrs = ctypes.create_string_buffer(256)
+    for p in (src.data_ptr(), tar.data_ptr() + 4096 * 100, H.data_ptr() + 36 * (n // 2)):
+        rc = hip.hipPointerGetAttributes(attrs, ctypes.c_void_p(p))
+        hip.hipGetLastError()
+        assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the calls"
+
+
 def test_host_full_size(pkg, dev):
     """BASELINE configs[1] size, 10 M problems, from pageable memory."""
     n = 10_000_000
