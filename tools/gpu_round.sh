@@ -35,6 +35,13 @@ for step in $STEPS; do
         cpuprobe) run cpuprobe 60 bash tools/cpu_probe.sh ;;
         crossover) run crossover 400 python tools/crossover.py ;;
         chunk_probe) run chunk_probe 300 python tools/chunk_probe.py ;;
+        pmc_tlb)
+            # translation-cache counters of the headline kernel at 1 GB and 2 GB (one pass, no tracing)
+            run pmc_tlb 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum \
+                GRBM_UTCL2_BUSY GRBM_GUI_ACTIVE --output-format csv -d "$OUT/pmc_tlb_$TAG" -o run -- \
+                python3 tools/pmc_tlb.py
+            python3 tools/pmc_tlb.py --reduce "$OUT/pmc_tlb_$TAG/run_counter_collection.csv" \
+                "$OUT/pmc_tlb_$TAG.json" > /dev/null || true ;;
         cpubase) run cpubase 300 python -c "import bench, json; print(json.dumps(bench.cpu_baseline(10_000_000)))" ;;
         newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_kat.py \
                 tests/test_gpu_config5.py tests/test_gpu_host.py tests/test_gpu_cpp_api.py -m gpu -v \
