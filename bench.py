@@ -194,11 +194,13 @@ class Dist:
 
 
 def timed_region(d: Dist, fn, steps: int):
-    """barrier + sync, K steps, sync + barrier; returns (wall_s max over ranks,
-    mean per-launch device time in ms from HIP events on the launch stream).  Each rank's
-    clock runs from the opening barrier's release to its own final synchronize -- its K
-    steps -- and the job's time is the max over ranks; the closing barrier only keeps the
-    ranks in step (its own latency is not work, and at N = 1 there is none)."""
+    """barrier + sync, K steps, sync + barrier; returns (the job's wall seconds, mean
+    per-launch device time in ms from HIP events on the launch stream).  Each rank stamps
+    its start (after the opening barrier's release) and its end (after its final
+    synchronize) on CLOCK_MONOTONIC (time.perf_counter on Linux: one clock for every process
+    of the node), and the job's time is the latest end minus the earliest start over ranks --
+    release skew included, the closing barrier's own latency not (it is no work; at N = 1
+    there is none)."""
     stream = torch.cuda.current_stream(d.dev)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
@@ -210,9 +212,9 @@ def timed_region(d: Dist, fn, steps: int):
         fn()
     e1.record(stream)
     torch.cuda.synchronize(d.dev)
-    wall = time.perf_counter() - t0
+    t1 = time.perf_counter()
     d.barrier()
-    return d.max(wall), e0.elapsed_time(e1) / steps
+    return d.max(t1) + d.max(-t0), e0.elapsed_time(e1) / steps
 
 
 def launch_stats(d: Dist, fn, groups: int = 40, per_group: int = 10):
