@@ -602,6 +602,47 @@ def test_concurrent_streams(orc, oracle, pkg, dev):
               f"{algo} {layout} on its own stream")
 
 
+def test_c_abi_from_many_threads(orc, oracle, pkg, dev):
+    """The C ABI called from 8 host threads at once (ctypes releases the GIL), each with its
+    own stream, batch, solver and layout, 30 calls each: every result has the oracle's bits
+    (the entry points keep no shared mutable state; include/sks_homography.h)."""
+    import threading
+    lib = pkg.lib()
+    n = 50_021
+    jobs = []
+    for k in range(8):
+        algo = ("aca", "sks")[k % 2]
+        soa = k % 4 >= 2
+        s = pkg.fill_uniform(n * 8, 300 + k, 0, device=dev).view(n, 8)
+        t = pkg.fill_uniform(n * 8, 300 + k, n * 8, device=dev).view(n, 8)
+        if soa:
+            s, t = s.T.contiguous(), t.T.contiguous()
+        H = torch.empty((9, n) if soa else (n, 9), device=dev)
+        st = torch.cuda.Stream(dev)
+        s_h, t_h = s.cpu().numpy(), t.cpu().numpy()
+        want = oracle.solve(algo, s_h, t_h, layout="soa" if soa else "aos")
+        jobs.append((getattr(lib, f"hg_{algo}_f32"), s, t, H, st, int(soa), want))
+    torch.cuda.synchronize(dev)
+    errors = []
+
+    def work(job):
+        fn, s, t, H, st, lay, _ = job
+        for _ in range(30):
+            rc = fn(s.data_ptr(), t.data_ptr(), H.data_ptr(), n, lay, 1, st.cuda_stream)
+            if rc:
+                errors.append(rc)
+        st.synchronize()
+
+    th = [threading.Thread(target=work, args=(j,)) for j in jobs]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not errors
+    for fn, s, t, H, st, lay, want in jobs:
+        _bits(orc, H, want, f"thread job layout={lay}")
+
+
 @pytest.mark.parametrize("algo", ["aca", "sks"])
 def test_soa_f64_beyond_mall_vs_oracle(orc, oracle, pkg, dev, algo):
     """f64 SoA batches past the cache-policy threshold take the non-temporal narrow kernel;
