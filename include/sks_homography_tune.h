@@ -29,7 +29,8 @@ int hg_tune_aos_f32(int algo, int variant, const float* src, const float* tar, f
  * 2 = 4x16 B/lane plain, 3 = LDS-DMA 8 KiB per wave (bytes % 32 KiB == 0). */
 int hg_tune_copy(int variant, const void* src, void* dst, int64_t bytes, void* stream);
 
-/* SoA (reference GPU layout), unnormalised; each variant fixes its dtype. */
+/* SoA (reference GPU layout), unnormalised; each variant fixes its dtype.  algo: 0 ACA,
+ * 1 SKS; binary64 variants of the 16-B register and narrow forms also 2 GE, 3 GPT-LU. */
 int hg_tune_num_soa_variants(void);
 const char* hg_tune_soa_variant_name(int variant);
 int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H, int64_t n,

@@ -249,8 +249,17 @@ int launch_solver(const T* src, const T* tar, T* H, int64_t n, int layout, hipSt
     const bool cached = host || n <= kMallResidentBytes / (25 * (int64_t)sizeof(T));  // 25 values/problem
     if (layout == HG_LAYOUT_SOA) {
         constexpr int V = 16 / sizeof(T);
-        if (sizeof(T) == 8 && cached && n >= kSoaWideMinN && n % V == 0 && aligned16(src) &&
-            aligned16(tar) && aligned16(H)) {
+        const bool wide = sizeof(T) == 8 && n >= kSoaWideMinN && n % V == 0 && aligned16(src) &&
+                          aligned16(tar) && aligned16(H);
+        if (wide && ALGO == kGPT && !host) {
+            // GPT-LU is VALU-bound (~1000 instructions a problem): two problems per lane in
+            // 16-B registers with non-temporal access at every size from 32 K, 5 % ahead of
+            // the narrow form at 10 M and level at 1 M (tools/kbench_gpt.py)
+            const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
+            return launch(solve_soa_vec<ALGO, NORM, T, kSoaG, false, true>, g, kBlock, 0, s, src,
+                          tar, H, n);
+        }
+        if (wide && cached) {
             // binary64, MALL-resident, mid-size: the 16-B register form (8 % ahead at 100 K)
             const unsigned g = (unsigned)soa_grid<kSoaG, false>(n / V);
             return launch(solve_soa_vec<ALGO, NORM, T, kSoaG, false, false>, g, kBlock, 0, s, src,

@@ -130,7 +130,11 @@ int launch_soa(int algo, const void* s, const void* t, void* H, int64_t n, int p
     const T* b = (const T*)t;
     T* h = (T*)H;
     if (algo == 0) solve_soa_vec<kACA, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
-    else solve_soa_vec<kSKS, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else if (algo == 1) solve_soa_vec<kSKS, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else if constexpr (sizeof(T) == 8) {  // the baselines (tools/kbench_gpt.py)
+        if (algo == 2) solve_soa_vec<kGE, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+        else solve_soa_vec<kGPT, false, T, G, PERSIST, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    } else return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
 }
 
@@ -159,7 +163,11 @@ int launch_soa_narrow(int algo, const void* s, const void* t, void* H, int64_t n
     const T* b = (const T*)t;
     T* h = (T*)H;
     if (algo == 0) solve_soa_narrow<kACA, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
-    else solve_soa_narrow<kSKS, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else if (algo == 1) solve_soa_narrow<kSKS, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    else if constexpr (sizeof(T) == 8) {
+        if (algo == 2) solve_soa_narrow<kGE, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+        else solve_soa_narrow<kGPT, false, T, W, NT><<<g, kBlock, 0, st>>>(a, b, h, n);
+    } else return (int)hipErrorInvalidValue;
     return (int)hipGetLastError();
 }
 

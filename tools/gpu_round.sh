@@ -35,6 +35,10 @@ for step in $STEPS; do
         cpuprobe) run cpuprobe 60 bash tools/cpu_probe.sh ;;
         crossover) run crossover 400 python tools/crossover.py ;;
         chunk_probe) run chunk_probe 300 python tools/chunk_probe.py ;;
+        kbench_gpt) run kbench_gpt 300 python tools/kbench_gpt.py ;;
+        gpt_tests) run pytest_gpt 600 python -u -m pytest tests/test_gpu_refcu.py tests/test_gpu_parity.py \
+                tests/test_gpu_grouped.py -m gpu -q -k "gpt or refcu or reference_kernels or ge" \
+                -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         pmc_tlb)
             # translation-cache counters of the headline kernel at 1 GB and 2 GB (one pass, no tracing)
             run pmc_tlb 120 rocprofv3 --pmc TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_REQUEST_sum \
