@@ -98,6 +98,44 @@ def test_reference_kernels_large_batch(orc, pkg, dev, refcu):
         assert orc.same_bits(got, want).all(), algo
 
 
+def _special_mixtures(n, seed):
+    """(8, n) SoA sets whose every coordinate is drawn from a small set of special values:
+    signed zeros, ties of equal magnitude (+-1, +-2), +-Inf, NaN, subnormals and near-overflow
+    magnitudes.  Pivot searches meet exact ties and all-zero / NaN columns on almost every
+    problem, which is where a register-resident partial pivoting (the first row of strictly
+    larger magnitude wins) and any structural shortcut in it would show."""
+    vals = np.array([0.0, -0.0, 1.0, -1.0, 2.0, -2.0, 0.5, 3.0, 1024.0,
+                     np.inf, -np.inf, np.nan, 5e-324, -2.5e-310, 1e308, -1e308])
+    w = np.array([8, 6, 8, 6, 6, 4, 4, 4, 4, 1, 1, 1, 1, 1, 1, 1], dtype=np.float64)
+    rng = np.random.default_rng(seed)
+    s = rng.choice(vals, size=(8, n), p=w / w.sum())
+    t = rng.choice(vals, size=(8, n), p=w / w.sum())
+    # a third of the problems keep ordinary source points, so the target side alone is special
+    k = n // 3
+    s[:, :k] = rng.integers(-4, 5, size=(8, k)).astype(np.float64)
+    return np.ascontiguousarray(s), np.ascontiguousarray(t)
+
+
+@pytest.mark.parametrize("n", [65_536, 65_537])
+def test_special_value_mixtures_equal_reference_kernels(orc, oracle, pkg, dev, refcu, n):
+    """Every solver, both SoA kernel forms (even n from 32 K: two problems per lane in 16-B
+    registers; odd n: one per lane), the AoS form, and the CPU restatement, against the
+    reference kernels on special-value mixtures -- NaN for NaN, signed zeros included."""
+    s, t = _special_mixtures(n, 7 + n)
+    ds, dt = torch.from_numpy(s).to(dev), torch.from_numpy(t).to(dev)
+    for algo in ALGOS:
+        want = refcu.solve(algo, s, t)
+        got = pkg.solve(algo, ds, dt, normalize=False, layout="soa").cpu().numpy()
+        ok = orc.same_bits(got, want)
+        assert ok.all(), f"{algo} GPU: {int((~ok).sum())}/{ok.size} differ"
+        aos = pkg.solve(algo, ds.T.contiguous(), dt.T.contiguous(), normalize=False,
+                        layout="aos").cpu().numpy()
+        ok = orc.same_bits(aos, want.T)
+        assert ok.all(), f"{algo} GPU AoS: {int((~ok).sum())}/{ok.size} differ"
+        ok = orc.same_bits(oracle.solve(algo, s, t, normalize=False, layout="soa"), want)
+        assert ok.all(), f"{algo} oracle: {int((~ok).sum())}/{ok.size} differ"
+
+
 @settings(max_examples=20, deadline=None, suppress_health_check=list(HealthCheck))
 @given(arrays(np.float64, (16, 257), elements=st.floats(width=64, allow_nan=True,
                                                         allow_infinity=True, allow_subnormal=True)))
