@@ -44,7 +44,8 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
                  float b, void* stream);
 
 /* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2), 3 P = 2 with
- * two-tile prefetch, 4-6 wider blocks, 7 P = 2 with the 64-bit remainder. */
+ * two-tile prefetch, 4-6 wider blocks, 7 P = 2 with the 64-bit remainder, 8 P = 2 solved as
+ * packed f32x2 pairs. */
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
 
@@ -66,11 +67,14 @@ int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void*
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
                     int64_t pitch_bytes, void* stream);
 
-/* Seeded fused sampler, (P, waves per block[, draws in place]): 0 shipped (1, 16, in place),
+/* Seeded fused sampler, (P, waves per block[, draws in place]): 0 shipped (packed pairs:
+ * SKS (2, 8); ACA (2, 4) from 4 M hypotheses, (1, 16) below), 13 (1, 16, in place) -- the
+ * round-1 shipped form,
  * 1 (2, 4), 2 (1, 16), 3 (2, 16), 4 (2, 8) with the 64-bit remainder, 5 / 6 one hash per draw
  * (a different stream) at (2, 4) / (2, 8), 7 (2, 8, in place), 8 (2, 4, in place), 9 (2, 8)
- * -- the previous shipped form.  "In place": each tile's draws made where they are used
- * rather than one tile ahead. */
+ * -- the previous shipped form; 10 / 11 / 12 (2, 8 / 16 / 4, in place) with the two
+ * hypotheses of a lane solved as packed f32x2 pairs.  "In place": each tile's draws made
+ * where they are used rather than one tile ahead. */
 int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
                           uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
                           int algo, int flags, void* stream);

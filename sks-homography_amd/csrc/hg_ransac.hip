@@ -52,7 +52,7 @@ int hg_sample_solve_seeded_f32(const float* pool_src, const float* pool_tar, uin
     if ((reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
         (reinterpret_cast<uintptr_t>(pool_tar) & 7u))
         return (int)hipErrorInvalidValue;
-    return hg::launch_sample_seeded(reinterpret_cast<const float2*>(pool_src),
+    return hg::launch_sample_seeded_shipped(reinterpret_cast<const float2*>(pool_src),
                                     reinterpret_cast<const float2*>(pool_tar), npool,
                                     seed, offset, H, n, algo,
                                     (flags & HG_FLAG_NORMALIZE) != 0,

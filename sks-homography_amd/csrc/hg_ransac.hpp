@@ -22,6 +22,9 @@ namespace hg {
 
 constexpr uint64_t kBitsMul = 0xA0761D6478BD642Full;
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef int i32x2 __attribute__((ext_vector_type(2)));
+
 // Word w of stream S = seed * kBitsMul is one half of the splitmix64 finaliser of counter
 // S + w/2: the high 32 bits for even w, the low 32 for odd w -- one 64-bit hash per two
 // draws (each finaliser costs six quarter-rate 32-bit multiplies; taking both halves
@@ -88,7 +91,7 @@ __device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, bo
 // (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
 // LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
 // does (.cu:56-59, modulo bias and duplicates included).
-template <int ALGO, bool NORM, int P, int DRAWS = kDrawsIndexed>
+template <int ALGO, bool NORM, int P, int DRAWS = kDrawsIndexed, bool PAIR = false>
 __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     const uint4* __restrict__ idx, float* __restrict__ H, int64_t n, uint64_t bits_base = 0,
@@ -124,17 +127,38 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
         }
     }
     float h[P][9];
+    if constexpr (PAIR) {  // as sample_solve_lds_kernel's PAIR: packed f32x2 pairs
+        static_assert(P % 2 == 0, "paired solve takes hypotheses two at a time");
 #pragma unroll
-    for (int j = 0; j < P; ++j) {
-        const uint32_t id[4] = {r[j].x % npool, r[j].y % npool, r[j].z % npool, r[j].w % npool};
-        float s[8], t[8];
+        for (int j = 0; j < P; j += 2) {
+            f32x2 s[8], t[8], hp[9];
+            const uint32_t ra[4] = {r[j].x, r[j].y, r[j].z, r[j].w};
+            const uint32_t rb[4] = {r[j + 1].x, r[j + 1].y, r[j + 1].z, r[j + 1].w};
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
-            s[2 * k] = a.x; s[2 * k + 1] = a.y;
-            t[2 * k] = b.x; t[2 * k + 1] = b.y;
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t ia = ra[k] % npool, ib = rb[k] % npool;
+                const float2 as = pool_src[ia], at = pool_tar[ia];
+                const float2 bs = pool_src[ib], bt = pool_tar[ib];
+                s[2 * k] = f32x2{as.x, bs.x}; s[2 * k + 1] = f32x2{as.y, bs.y};
+                t[2 * k] = f32x2{at.x, bt.x}; t[2 * k + 1] = f32x2{at.y, bt.y};
+            }
+            solve<ALGO, NORM>(s, t, hp);
+#pragma unroll
+            for (int k = 0; k < 9; ++k) { h[j][k] = hp[k].x; h[j + 1][k] = hp[k].y; }
         }
-        solve<ALGO, NORM>(s, t, h[j]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < P; ++j) {
+            const uint32_t id[4] = {r[j].x % npool, r[j].y % npool, r[j].z % npool, r[j].w % npool};
+            float s[8], t[8];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float2 a = pool_src[id[k]], b = pool_tar[id[k]];
+                s[2 * k] = a.x; s[2 * k + 1] = a.y;
+                t[2 * k] = b.x; t[2 * k + 1] = b.y;
+            }
+            solve<ALGO, NORM>(s, t, h[j]);
+        }
     }
     if (full) {
         store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
@@ -196,8 +220,11 @@ __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uin
 // the next tile's index rows already in flight (per-lane 16-B loads, lane-consecutive),
 // and the H rows leave through the LDS-staged 16-B stores.  Requires the pool plus the
 // staging to fit the block's LDS (checked on the host).
+// PAIR (P even): hypotheses j and j+1 of a lane are solved together as the two halves of
+// packed f32x2 values, so each v_pk_mul_f32 / v_pk_add_f32 does the same IEEE operation
+// for both (the same bits as two scalar solves); the divisions stay scalar per half.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
-          int DRAWS = kDrawsIndexed, bool MOD64 = false>
+          int DRAWS = kDrawsIndexed, bool MOD64 = false, bool PAIR = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -238,20 +265,38 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
         if constexpr (PF == 0) load(t, cur);
         else if (t + PF * stride < tiles) load(t + PF * stride, nxt);
         float h[P][9];
+        if constexpr (PAIR) {
+            static_assert(P % 2 == 0, "paired solve takes hypotheses two at a time");
 #pragma unroll
-        for (int j = 0; j < P; ++j) {
-            const uint32_t id[4] = {reduce_index<MOD64>(cur[j].x, magic, npool),
-                                    reduce_index<MOD64>(cur[j].y, magic, npool),
-                                    reduce_index<MOD64>(cur[j].z, magic, npool),
-                                    reduce_index<MOD64>(cur[j].w, magic, npool)};
-            float s[8], tt[8];
+            for (int j = 0; j < P; j += 2) {
+                f32x2 s[8], tt[8], hp[9];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const float4 q = pool[id[k]];
-                s[2 * k] = q.x; s[2 * k + 1] = q.y;
-                tt[2 * k] = q.z; tt[2 * k + 1] = q.w;
+                for (int k = 0; k < 4; ++k) {
+                    const float4 a = pool[reduce_index<MOD64>(cur[j][k], magic, npool)];
+                    const float4 b = pool[reduce_index<MOD64>(cur[j + 1][k], magic, npool)];
+                    s[2 * k] = f32x2{a.x, b.x}; s[2 * k + 1] = f32x2{a.y, b.y};
+                    tt[2 * k] = f32x2{a.z, b.z}; tt[2 * k + 1] = f32x2{a.w, b.w};
+                }
+                solve<ALGO, NORM>(s, tt, hp);
+#pragma unroll
+                for (int k = 0; k < 9; ++k) { h[j][k] = hp[k].x; h[j + 1][k] = hp[k].y; }
             }
-            solve<ALGO, NORM>(s, tt, h[j]);
+        } else {
+#pragma unroll
+            for (int j = 0; j < P; ++j) {
+                const uint32_t id[4] = {reduce_index<MOD64>(cur[j].x, magic, npool),
+                                        reduce_index<MOD64>(cur[j].y, magic, npool),
+                                        reduce_index<MOD64>(cur[j].z, magic, npool),
+                                        reduce_index<MOD64>(cur[j].w, magic, npool)};
+                float s[8], tt[8];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    const float4 q = pool[id[k]];
+                    s[2 * k] = q.x; s[2 * k + 1] = q.y;
+                    tt[2 * k] = q.z; tt[2 * k + 1] = q.w;
+                }
+                solve<ALGO, NORM>(s, tt, h[j]);
+            }
         }
         const int64_t base = t * kTile;
         if (base + kTile <= n) {
@@ -384,9 +429,6 @@ static __global__ __launch_bounds__(kBlock) void ransac_score_kernel(
 // Two hypotheses per lane, evaluated as packed pairs (v_pk_fma_f32 / v_pk_mul_f32:
 // one instruction serves both), every LDS point read shared by both.  Same per-pair
 // arithmetic (and bits) as is_inlier.
-typedef float f32x2 __attribute__((ext_vector_type(2)));
-typedef int i32x2 __attribute__((ext_vector_type(2)));
-
 template <int UNROLL>
 __global__ __launch_bounds__(kBlock) void ransac_score2_kernel(
     const float* __restrict__ H, int64_t n, const float2* __restrict__ pool_src,
@@ -489,14 +531,16 @@ inline int cu_count() {
 
 // variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
 // P = 1 / 2; 3 = LDS-pool P = 2 with the index rows two tiles ahead; 4 = LDS-pool P = 2
-// with the 64-bit remainder (fastmod64_u32).  The LDS forms fall back to 0 when the pool
-// does not fit.
+// with the 64-bit remainder (fastmod64_u32); 5 = LDS-pool P = 2, the two hypotheses of a
+// lane solved as packed f32x2 pairs.  The LDS forms fall back to 0 when the pool does not
+// fit.
 inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
                         const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
     constexpr int kShippedP = 2;
     const bool pf2 = variant == 3;
     const bool mod64 = variant == 4;
-    int use_p = variant == -1 ? kShippedP : (pf2 || mod64 ? 2 : variant);
+    const bool pair = variant == 5 || variant == -1;  // shipped: P = 2 packed pairs
+    int use_p = variant == -1 ? kShippedP : (pf2 || mod64 || pair ? 2 : variant);
     const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
     if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
     if (use_p == 0) {
@@ -504,10 +548,15 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
         const int64_t blocks = (n + (int64_t)kBlock * P - 1) / ((int64_t)kBlock * P);
         if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         const unsigned g = (unsigned)blocks;
-#define HG_SS(A, N) \
-    launch(sample_solve_kernel<A, N, P>, g, kBlock, 0, s, ps, pt, npool, ix, H, n, 0, 0)
-        if (algo == 0) return norm ? HG_SS(kACA, true) : HG_SS(kACA, false);
-        return norm ? HG_SS(kSKS, true) : HG_SS(kSKS, false);
+#define HG_SS(A, N, PR)                                                                          \
+    launch(sample_solve_kernel<A, N, P, kDrawsIndexed, PR>, g, kBlock, 0, s, ps, pt, npool, ix, H, n, \
+           0, 0)
+        if (pair) {
+            if (algo == 0) return norm ? HG_SS(kACA, true, true) : HG_SS(kACA, false, true);
+            return norm ? HG_SS(kSKS, true, true) : HG_SS(kSKS, false, true);
+        }
+        if (algo == 0) return norm ? HG_SS(kACA, true, false) : HG_SS(kACA, false, false);
+        return norm ? HG_SS(kSKS, true, false) : HG_SS(kSKS, false, false);
 #undef HG_SS
     }
     // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
@@ -533,6 +582,14 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
         return norm ? HG_SL64(kSKS, true) : HG_SL64(kSKS, false);
 #undef HG_SL64
     }
+    if (pair) {
+#define HG_SLP(A, N)                                                                             \
+    launch(sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, false, true>, g,     \
+           kBlock, lds, s, ps, pt, npool, magic, ix, H, n, 0, 0)
+        if (algo == 0) return norm ? HG_SLP(kACA, true) : HG_SLP(kACA, false);
+        return norm ? HG_SLP(kSKS, true) : HG_SLP(kSKS, false);
+#undef HG_SLP
+    }
     if (!pf2) {
         if (algo == 0) return norm ? HG_SL(2, kACA, true) : HG_SL(2, kACA, false);
         return norm ? HG_SL(2, kSKS, true) : HG_SL(2, kSKS, false);
@@ -546,14 +603,15 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 #undef HG_SL
 }
 
-// The seeded sampler's launcher.  Shipped shape: the LDS-pool kernel with P = 1 and 16 waves
-// per block (the pool copy shared by 16 waves; LDS opt-in past 64 KiB; 2 blocks = 32 waves
-// per CU), each tile's draws made where they are used (PF = 0: nothing to hide when the
-// draws are computed), while the pool plus staging fit the CU's 160 KiB, else the
-// global-gather form.  The draws are made in the kernel from word `offset` of stream
-// seed * kBitsMul (draws4).  P, WPB, DRAWS, MOD64 and PF are open for the variant sweep
-// (hg_tune_sample_seeded).
-template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0>
+// The seeded sampler's launcher: the LDS-pool kernel with P problems per lane and WPB waves
+// per block sharing one pool copy (LDS opt-in past 64 KiB), persistent grid, while the pool
+// plus staging fit the CU's 160 KiB, else the global-gather form.  The draws are made in
+// the kernel from word `offset` of stream seed * kBitsMul (draws4); PF = 0 makes each
+// tile's draws where they are used (nothing to hide when the draws are computed).  The
+// shipped shapes are launch_sample_seeded_shipped's; every parameter is open for the
+// variant sweep (hg_tune_sample_seeded).
+template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0,
+          bool PAIR = false>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
                                 bool norm, hipStream_t s) {
@@ -567,8 +625,8 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
         if (blocks > 0x7fffffffLL) return (int)hipErrorInvalidValue;
         const unsigned g = (unsigned)blocks;
 #define HG_SG(A, N)                                                                          \
-    launch(sample_solve_kernel<A, N, PG, DRAWS>, g, kBlock, 0, s, ps, pt, npool, nullptr, H, n, \
-           bits_base, odd)
+    launch(sample_solve_kernel<A, N, PG, DRAWS, PAIR>, g, kBlock, 0, s, ps, pt, npool, nullptr, H, \
+           n, bits_base, odd)
         if (algo == 0) return norm ? HG_SG(kACA, true) : HG_SG(kACA, false);
         return norm ? HG_SG(kSKS, true) : HG_SG(kSKS, false);
 #undef HG_SG
@@ -583,7 +641,7 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     const uint64_t magic = MOD64 ? fastmod64_magic(npool) : fastmod_magic(npool);
 #define HG_SD(A, N)                                                                         \
     do {                                                                                    \
-        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64>;                   \
+        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64, PAIR>;             \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
         rc = launch(k, g, WPB * kWave, lds, s, ps, pt, npool, magic, nullptr, H, n, bits_base, \
                     odd);                                                                   \
@@ -593,6 +651,27 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     else { if (norm) HG_SD(kSKS, true); else HG_SD(kSKS, false); }
 #undef HG_SD
     return rc;
+}
+
+// The shipped seeded shapes, all solving two hypotheses per lane as packed f32x2 pairs
+// (the indexed sampler's arithmetic, so a seeded launch equals fill_bits + an indexed one
+// to the NaN bit): SKS with 8 waves per block; ACA with 4 from kSeededPairMinN hypotheses
+// (fewer resident waves, fewer concurrent write streams: the launch is within ~7 % of the
+// write-only HBM ceiling there), below it the P = 1, 16-wave form, which keeps more waves
+// in flight for a short launch.  16 M: ACA 109-113 vs 118-126 us, SKS 131-133 vs 147-155
+// (tools/kbench_sample.py, profiles/r02/kbench_pair*.json).
+constexpr int64_t kSeededPairMinN = int64_t(1) << 22;
+inline int launch_sample_seeded_shipped(const float2* ps, const float2* pt, uint32_t npool,
+                                        uint64_t seed, uint64_t offset, float* H, int64_t n,
+                                        int algo, bool norm, hipStream_t s) {
+    if (algo != 0)
+        return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset,
+                                                                         H, n, algo, norm, s);
+    if (n >= kSeededPairMinN)
+        return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset,
+                                                                         H, n, algo, norm, s);
+    return launch_sample_seeded<1, 16, kDrawsPaired, false, 0, false>(ps, pt, npool, seed, offset,
+                                                                       H, n, algo, norm, s);
 }
 
 // Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice

@@ -586,7 +586,7 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
 // same argument checks as hg_sample_solve_f32.
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
-    if (n <= 0 || npool == 0 || variant < 0 || variant > 7 || (algo != 0 && algo != 1))
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 8 || (algo != 0 && algo != 1))
         return (int)hipErrorInvalidValue;
     if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
         (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
@@ -602,6 +602,7 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
         case 5: return hg::launch_sample_wide<1, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
         case 6: return hg::launch_sample_wide<2, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
         case 7: return hg::launch_sample_solve(4, ps, pt, npool, ix, H, n, algo, norm, st);
+        case 8: return hg::launch_sample_solve(5, ps, pt, npool, ix, H, n, algo, norm, st);
         default: break;
     }
     return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
@@ -626,7 +627,8 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
     hipStream_t st = reinterpret_cast<hipStream_t>(stream);
     using namespace hg;
     switch (variant) {
-        case 0: return launch_sample_seeded<>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 0: return launch_sample_seeded_shipped(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 13: return launch_sample_seeded<1, 16, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 1: return launch_sample_seeded<2, 4, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 2: return launch_sample_seeded<1, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 3: return launch_sample_seeded<2, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
@@ -636,6 +638,10 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 7: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 8: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 9: return launch_sample_seeded<2, 8, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // two hypotheses per lane solved as packed f32x2 pairs
+        case 10: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 11: return launch_sample_seeded<2, 16, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 12: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -152,6 +152,25 @@ def test_sample_solve_seeded_vs_oracle(orc, oracle, pkg, dev, npool):
                 assert ok.all(), f"npool {npool} n {n} {algo} norm={norm}: {(~ok).sum()} differ"
 
 
+def test_sample_solve_seeded_packed_shapes_vs_indexed(orc, oracle, pkg, dev):
+    """Past kSeededPairMinN (4 M) the seeded ACA launch switches to the 4-wave packed-pair
+    shape (SKS uses packed pairs at every size): still fill_bits + the indexed sampler bit
+    for bit, NaN bits included, and the oracle NaN for NaN, on the reference's wall pool,
+    a ragged batch and an odd stream offset."""
+    g = load_golden("cpp_wall.npz")
+    ps, pt = g["pool_src"], g["pool_tar"]
+    dps, dpt = torch.from_numpy(ps).to(dev), torch.from_numpy(pt).to(dev)
+    n, seed, off = (1 << 22) + 129, 11, 3
+    bits = pkg.fill_bits(n * 4, seed, off, dev).view(n, 4)
+    s, t = oracle.sample_problems(ps, pt, bits.cpu().numpy())
+    for algo in ("aca", "sks"):
+        H = pkg.sample_solve_seeded(dps, dpt, n, seed, off, algo=algo)
+        ref = pkg.sample_solve(dps, dpt, bits, algo=algo)
+        assert torch.equal(H.view(torch.int32), ref.view(torch.int32)), algo
+        ok = orc.same_bits(H.cpu().numpy(), oracle.solve(algo, s, t, normalize=True))
+        assert ok.all(), f"{algo}: {(~ok).sum()} differ"
+
+
 def test_sample_solve_seeded_zero_and_errors(pkg, dev):
     ps = torch.rand(10, 2, device=dev)
     assert pkg.sample_solve_seeded(ps, ps, 0, 1).shape == (0, 9)

@@ -36,6 +36,8 @@ for step in $STEPS; do
         crossover) run crossover 400 python tools/crossover.py ;;
         chunk_probe) run chunk_probe 300 python tools/chunk_probe.py ;;
         kbench_gpt) run kbench_gpt 300 python tools/kbench_gpt.py ;;
+        ransac_tests) run pytest_ransac 600 python -u -m pytest tests/test_gpu_ransac.py tests/test_gpu_large.py \
+                -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         gpt_tests) run pytest_gpt 600 python -u -m pytest tests/test_gpu_refcu.py tests/test_gpu_parity.py \
                 tests/test_gpu_grouped.py -m gpu -q -k "gpt or refcu or reference_kernels or ge" \
                 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
@@ -86,6 +88,14 @@ for step in $STEPS; do
         kbench_rect) run kbench_rect 300 python tools/kbench_rect.py ;;
         kbench_sample) run kbench_sample 300 python tools/kbench_sample.py ;;
         kbench_seeded) KB_SEEDED_ONLY=1 run kbench_seeded 300 python tools/kbench_sample.py ;;
+        kbench_pair)  # the packed-pair seeded forms against the shipped one, ACA then SKS
+            KB_ROUNDS=11 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,7,8,10,11,12 run kbench_pair 300 python tools/kbench_sample.py
+            KB_ROUNDS=11 KB_ALGO=1 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,7,8,10,11,12 run kbench_pair_sks 300 \
+                python tools/kbench_sample.py ;;
+        kbench_pair_idx)  # the packed-pair indexed form against the shipped one, ACA then SKS
+            KB_ROUNDS=11 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx 300 python tools/kbench_sample.py
+            KB_ROUNDS=11 KB_ALGO=1 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx_sks 300 \
+                python tools/kbench_sample.py ;;
         kbench_soa_small) run kbench_soa_small 300 python tools/kbench_soa_small.py ;;
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
         kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;

@@ -18,18 +18,28 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 import __graft_entry__ as ge  # noqa: E402
 
-NAMES = {0: "global gather P2", 1: "LDS pool P1", 2: "LDS pool P2", 3: "LDS pool P2 prefetch 2",
+NAMES = {0: "global gather P2 (scalar)", 1: "LDS pool P1", 2: "LDS pool P2 (round-1 shipped)", 3: "LDS pool P2 prefetch 2",
          4: "LDS pool P1, 8 waves/block", 5: "LDS pool P1, 16 waves/block",
-         6: "LDS pool P2, 16 waves/block", 7: "LDS pool P2, 64-bit remainder"}
-SEEDED = {0: "seeded P1, 16 waves/block, draws in place (shipped)", 1: "seeded P2, 4 waves/block",
+         6: "LDS pool P2, 16 waves/block", 7: "LDS pool P2, 64-bit remainder",
+         8: "LDS pool P2, packed f32x2 pairs (shipped)"}
+if os.environ.get("KB_INDEXED_VARIANTS"):  # e.g. "0,2,8"
+    NAMES = {int(v): NAMES[int(v)] for v in os.environ["KB_INDEXED_VARIANTS"].split(",")}
+SEEDED = {0: "seeded shipped (packed pairs; ACA below 4 M: P1, 16 waves)", 1: "seeded P2, 4 waves/block",
           2: "seeded P1, 16 waves/block", 3: "seeded P2, 16 waves/block",
           4: "seeded P2, 8 waves/block, 64-bit remainder",
           5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw",
           7: "seeded P2, 8 waves/block, draws in place", 8: "seeded P2, 4 waves/block, draws in place",
-          9: "seeded P2, 8 waves/block (previous shipped)"}
+          9: "seeded P2, 8 waves/block (previous shipped)",
+          10: "seeded P2 paired f32x2, 8 waves/block, in place",
+          11: "seeded P2 paired f32x2, 16 waves/block, in place",
+          12: "seeded P2 paired f32x2, 4 waves/block, in place",
+          13: "seeded P1, 16 waves/block, draws in place (round-1 shipped)"}
 # KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
 SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
 OTHER_STREAM = (5, 6)  # one hash per draw: a different stream, not comparable bit for bit
+ALGO = int(os.environ.get("KB_ALGO", "0"))  # 0 ACA, 1 SKS (normalised)
+if os.environ.get("KB_SEEDED_VARIANTS"):  # e.g. "0,7,10,11,12"
+    SEEDED = {int(v): SEEDED[int(v)] for v in os.environ["KB_SEEDED_VARIANTS"].split(",")}
 
 
 def main():
@@ -58,10 +68,10 @@ def main():
         def run(v):
             if isinstance(v, tuple):
                 assert fs(v[1], ps.data_ptr(), pt.data_ptr(), npool, 11, 0, outs[v].data_ptr(), n,
-                          0, 1, st) == 0
+                          ALGO, 1, st) == 0
             else:
                 assert f(v, ps.data_ptr(), pt.data_ptr(), npool, idx.data_ptr(), outs[v].data_ptr(),
-                         n, 0, 1, st) == 0
+                         n, ALGO, 1, st) == 0
 
         for v in keys:
             for _ in range(3):
@@ -69,9 +79,12 @@ def main():
         torch.cuda.synchronize()
         exact = {v: bool(torch.equal(outs[v].view(torch.int32), outs[0].view(torch.int32)))
                  for v in keys}
+        # equal up to NaN payload and sign (the contract against the CPU reference)
+        nan_eq = {v: bool(((outs[v].view(torch.int32) == outs[0].view(torch.int32))
+                           | (outs[v].isnan() & outs[0].isnan())).all()) for v in keys}
         times = {v: [] for v in keys}
         reps = 20
-        for _ in range(7):
+        for _ in range(int(os.environ.get("KB_ROUNDS", "7"))):
             for v in keys:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
@@ -87,13 +100,14 @@ def main():
             nb = 36 if isinstance(v, tuple) else 52
             res[name] = {"us": round(us, 2), "G_hyp_per_s": round(n / us / 1e3, 2),
                          "algorithmic_gbps": round(n * nb / us / 1e3, 1),
-                         "bit_exact": None if isinstance(v, tuple) and v[1] in OTHER_STREAM else exact[v]}
+                         "bit_exact": None if isinstance(v, tuple) and v[1] in OTHER_STREAM else exact[v],
+                         "equal_nan_aware": None if isinstance(v, tuple) and v[1] in OTHER_STREAM else nan_eq[v]}
             print(n, name, res[name], flush=True)
         out[str(n)] = res
         del idx, outs
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
-    with open(os.path.join(ROOT, "gpurun_out", "kbench_sample.json"), "w") as fh:
-        json.dump(out, fh, indent=1)
+    with open(os.path.join(ROOT, "gpurun_out", f"kbench_sample{'_sks' if ALGO else ''}.json"), "w") as fh:
+        json.dump({"algo": ["aca", "sks"][ALGO], **out}, fh, indent=1)
 
 
 if __name__ == "__main__":
