@@ -776,6 +776,20 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     seeded_same = bool(torch.equal(pkg.sample_solve_seeded(ps, pt, hyps, SEED, 0).view(torch.int32),
                                    H.view(torch.int32)))
     del idx_b
+    # the seeded launch is a write-only stream (36 B of H per hypothesis, the pool stays in
+    # LDS): its own ceiling is a plain write-only stream of the same bytes on this box
+    # (tune library's 16-B store kernel, hg_tune_copy variant 5), interleaved with it
+    import ctypes
+    wr = pkg._lib.tune().hg_tune_copy
+    wr.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    wr.restype = ctypes.c_int
+    wbuf = torch.empty(big * 9, dtype=torch.float32, device=d.dev)
+    wstream = torch.cuda.current_stream(d.dev).cuda_stream
+    f_write = lambda: wr(5, None, wbuf.data_ptr(), big * 36, wstream)  # noqa: E731
+    for _ in range(30):
+        f_write()
+    ms_write = launch_stats(d, f_write, groups=20)["median_us"] * 1e-3
+    del wbuf
     return {
         "hypotheses": hyps, "pool": int(ps.shape[0]), "thresh_px": thresh,
         "sample_solve_us": round(ms_solve * 1e3, 2),
@@ -790,6 +804,8 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
             "G_hyp_per_s": round(big / (ms_seed * 1e-3) / 1e9, 2),
             "achieved_gbps": round(big * 36 / (ms_seed * 1e-3) / 1e9, 1),
             "frac": round(big * 36 / (ms_seed * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "write_only_stream_gbps": round(big * 36 / (ms_write * 1e-3) / 1e9, 1),
+            "frac_of_write_only_stream": round(ms_write / ms_seed, 4),
             "draws_then_indexed_us": round(ms_two * 1e3, 2),
             "speedup_vs_two_launch": round(ms_two / ms_seed, 2),
             "bit_identical_to_indexed": seeded_same},
