@@ -60,6 +60,7 @@ static __global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __re
 constexpr int kDrawsIndexed = 0;  // row p of the (n,4) index array
 constexpr int kDrawsPaired = 1;   // seeded: fill_bits' stream generated in place (shipped)
 constexpr int kDrawsSingle = 2;   // seeded, tune only: one hash per draw (the earlier stream)
+constexpr int kDrawsCheap = 3;    // tune ablation only: multiply-free scrambles of p (not a stream)
 
 // The 4 draws of hypothesis p: row p of the (n,4) index array, or -- seeded -- the same
 // four words generated in place: words offset + 4p ... + 3 of the stream, i.e. out[4p ..
@@ -77,6 +78,10 @@ __device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, bo
         const uint64_t z2 = mix64(b + 2);
         return u32x4{word_half(z0, true), word_half(z1, false), word_half(z1, true),
                      word_half(z2, false)};
+    } else if constexpr (DRAWS == kDrawsCheap) {
+        const uint32_t x = (uint32_t)p ^ (uint32_t)bits_base;
+        const uint32_t a = x ^ (x << 13), b = a ^ (a >> 17), c = b ^ (b << 5);
+        return u32x4{a, b, c, c ^ (c >> 11)};
     } else if constexpr (DRAWS == kDrawsSingle) {
         const uint64_t b = bits_base + 4 * (uint64_t)p;
         return u32x4{(uint32_t)(mix64(b) >> 32), (uint32_t)(mix64(b + 1) >> 32),
@@ -207,10 +212,41 @@ __device__ __forceinline__ uint32_t fastmod64_u32(uint32_t r, uint64_t M, uint32
 
 inline uint64_t fastmod64_magic(uint32_t d) { return ~0ull / d + 1; }
 
-template <bool MOD64>
+// A third exact form, all full-rate binary64 (tools/kbench_sample.py): with u = the
+// smallest double >= 1/d, q = trunc(RN(r u)) is floor(r/d) or one more (r u >= r/d, and
+// the two roundings add < 2^-19 for r < 2^32), r - q d is exact in one FMA (every value
+// an integer < 2^33), and a negative remainder takes d back.  Host side: the bits of u.
+// Valid for d < 2^31 (the remainder passes through int32): the LDS pools are < 10^4.
+__device__ __forceinline__ uint32_t fmod_f64_u32(uint32_t r, uint64_t inv_bits, uint32_t d) {
+    const double x = (double)r;
+    const double q = __builtin_trunc(x * __builtin_bit_cast(double, inv_bits));
+    const int32_t rem = (int32_t)__builtin_fma(-q, (double)d, x);
+    return (uint32_t)(rem < 0 ? rem + (int32_t)d : rem);
+}
+
+inline uint64_t fmod_f64_magic(uint32_t d) {
+    double u = 1.0 / (double)d;
+    if (__builtin_fma(u, (double)d, -1.0) < 0.0) u = __builtin_nextafter(u, 2.0);
+    uint64_t bits;
+    __builtin_memcpy(&bits, &u, sizeof bits);
+    return bits;
+}
+
+// Remainder forms: 0 fastmod_u32 (shipped), 1 fastmod64_u32, 2 fmod_f64_u32; 3 (tune
+// ablation only, wrong indices) r & 1023 clamped to the pool -- the loop without a remainder.
+template <int RED>
 __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uint32_t d) {
-    if constexpr (MOD64) return fastmod64_u32(r, magic, d);
+    if constexpr (RED == 1) return fastmod64_u32(r, magic, d);
+    else if constexpr (RED == 2) return fmod_f64_u32(r, magic, d);
+    else if constexpr (RED == 3) return (r & 1023u) < d ? (r & 1023u) : 0u;
     else return fastmod_u32(r, magic, d);
+}
+
+template <int RED>
+inline uint64_t reduce_magic(uint32_t d) {
+    if constexpr (RED == 1) return fastmod64_magic(d);
+    else if constexpr (RED == 2) return fmod_f64_magic(d);
+    else return fastmod_magic(d);
 }
 
 // The same sampler with the pool staged in LDS once per block: {x, y, u, v} 16-B
@@ -224,7 +260,7 @@ __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uin
 // packed f32x2 values, so each v_pk_mul_f32 / v_pk_add_f32 does the same IEEE operation
 // for both (the same bits as two scalar solves); the divisions stay scalar per half.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
-          int DRAWS = kDrawsIndexed, bool MOD64 = false, bool PAIR = false>
+          int DRAWS = kDrawsIndexed, int MOD64 = 0, bool PAIR = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -610,7 +646,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // tile's draws where they are used (nothing to hide when the draws are computed).  The
 // shipped shapes are launch_sample_seeded_shipped's; every parameter is open for the
 // variant sweep (hg_tune_sample_seeded).
-template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, bool MOD64 = false, int PF = 0,
+template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, int MOD64 = 0, int PF = 0,
           bool PAIR = false>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
@@ -638,7 +674,7 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = MOD64 ? fastmod64_magic(npool) : fastmod_magic(npool);
+    const uint64_t magic = reduce_magic<MOD64>(npool);
 #define HG_SD(A, N)                                                                         \
     do {                                                                                    \
         auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64, PAIR>;             \

@@ -629,6 +629,14 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
     switch (variant) {
         case 0: return launch_sample_seeded_shipped(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 13: return launch_sample_seeded<1, 16, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // the remainder and the draws of the 4-wave packed-pair shape: 14 the binary64
+        // remainder (exact); ablations, wrong bits, time only: 15 no remainder, 16 no hash,
+        // 17 neither; 18 the 8-wave shape with the binary64 remainder
+        case 14: return launch_sample_seeded<2, 4, kDrawsPaired, 2, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 15: return launch_sample_seeded<2, 4, kDrawsPaired, 3, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 16: return launch_sample_seeded<2, 4, kDrawsCheap, 0, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 17: return launch_sample_seeded<2, 4, kDrawsCheap, 3, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 18: return launch_sample_seeded<2, 8, kDrawsPaired, 2, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 1: return launch_sample_seeded<2, 4, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 2: return launch_sample_seeded<1, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 3: return launch_sample_seeded<2, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);

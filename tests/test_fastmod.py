@@ -3,7 +3,9 @@ one umulhi + one mullo, round-up division by an invariant integer) restated with
 integers at 32-bit width and checked against % for divisors across the whole uint32
 range -- every d up to 4096, powers of two and their neighbours, random large d -- and
 the numerators where such schemes break (0, d-1, d, multiples of d, 2^32-1, ...).  The
-GPU tests (test_gpu_ransac.py) check the device code itself against the oracle's %."""
+binary64 form (fmod_f64_u32 / fmod_f64_magic, d < 2^31) the same way, its one rounded
+product restated in numpy float64.  The GPU tests (test_gpu_ransac.py) check the device
+code itself against the oracle's %."""
 import numpy as np
 
 M32 = (1 << 32) - 1
@@ -45,3 +47,31 @@ def test_fastmod_matches_modulo_everywhere():
         m, sh = magic(d)
         for r in _numerators(d, rng):
             assert fastmod(r, m, sh, d) == r % d, (d, r)
+
+
+def fmod_f64_magic(d):
+    u = np.float64(1.0) / np.float64(d)
+    if int(u.as_integer_ratio()[0]) * d < u.as_integer_ratio()[1]:  # u < 1/d exactly
+        u = np.nextafter(u, np.float64(2.0))
+    return u
+
+
+def fmod_f64(r, u, d):
+    q = int(np.trunc(np.float64(r) * u))      # the one rounded product (RN), truncated
+    rem = r - q * d                           # one FMA: exact, every term an integer < 2^33
+    assert -(1 << 31) <= rem < (1 << 31)      # the int32 conversion is exact
+    return rem + d if rem < 0 else rem
+
+
+def test_fmod_f64_matches_modulo_below_2_31():
+    rng = np.random.default_rng(5)
+    ds = set(range(1, 4097))
+    for k in range(1, 31):
+        ds |= {(1 << k) - 1, 1 << k, (1 << k) + 1}
+    ds |= {(1 << 31) - 1, 2540, 9088, 20_000, 65_537}
+    ds |= set(int(x) for x in rng.integers(1, 1 << 31, 400, dtype=np.uint64))
+    for d in sorted(ds):
+        u = fmod_f64_magic(d)
+        assert u >= 0 and u.as_integer_ratio()[0] * d >= u.as_integer_ratio()[1]
+        for r in _numerators(d, rng):
+            assert fmod_f64(r, u, d) == r % d, (d, r)

@@ -96,6 +96,10 @@ for step in $STEPS; do
             KB_ROUNDS=11 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx 300 python tools/kbench_sample.py
             KB_ROUNDS=11 KB_ALGO=1 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx_sks 300 \
                 python tools/kbench_sample.py ;;
+        kbench_ablate)  # where the seeded sampler's time goes, and the binary64 remainder
+            KB_ROUNDS=11 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,13,14,15,16,17 run kbench_ablate 300 python tools/kbench_sample.py
+            KB_ROUNDS=11 KB_ALGO=1 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,18 run kbench_ablate_sks 300 \
+                python tools/kbench_sample.py ;;
         kbench_soa_small) run kbench_soa_small 300 python tools/kbench_soa_small.py ;;
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
         kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;

@@ -33,10 +33,15 @@ SEEDED = {0: "seeded shipped (packed pairs; ACA below 4 M: P1, 16 waves)", 1: "s
           10: "seeded P2 paired f32x2, 8 waves/block, in place",
           11: "seeded P2 paired f32x2, 16 waves/block, in place",
           12: "seeded P2 paired f32x2, 4 waves/block, in place",
-          13: "seeded P1, 16 waves/block, draws in place (round-1 shipped)"}
+          13: "seeded P1, 16 waves/block, draws in place (round-1 shipped)",
+          14: "seeded P2 pairs, 4 waves, binary64 remainder",
+          15: "ablation: P2 pairs, 4 waves, no remainder (wrong bits)",
+          16: "ablation: P2 pairs, 4 waves, no hash (wrong bits)",
+          17: "ablation: P2 pairs, 4 waves, no hash, no remainder (wrong bits)",
+          18: "seeded P2 pairs, 8 waves, binary64 remainder"}
 # KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
 SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
-OTHER_STREAM = (5, 6)  # one hash per draw: a different stream, not comparable bit for bit
+OTHER_STREAM = (5, 6, 15, 16, 17)  # other streams / ablations: not comparable bit for bit
 ALGO = int(os.environ.get("KB_ALGO", "0"))  # 0 ACA, 1 SKS (normalised)
 if os.environ.get("KB_SEEDED_VARIANTS"):  # e.g. "0,7,10,11,12"
     SEEDED = {int(v): SEEDED[int(v)] for v in os.environ["KB_SEEDED_VARIANTS"].split(",")}
