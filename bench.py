@@ -193,19 +193,27 @@ class Dist:
             self.pg.destroy_process_group()
 
 
+START_MARGIN_S = 0.003
+
+
 def timed_region(d: Dist, fn, steps: int):
     """barrier + sync, K steps, sync + barrier; returns (the job's wall seconds, mean
-    per-launch device time in ms from HIP events on the launch stream).  Each rank stamps
-    its start (after the opening barrier's release) and its end (after its final
-    synchronize) on CLOCK_MONOTONIC (time.perf_counter on Linux: one clock for every process
-    of the node), and the job's time is the latest end minus the earliest start over ranks --
-    release skew included, the closing barrier's own latency not (it is no work; at N = 1
-    there is none)."""
+    per-launch device time in ms from HIP events on the launch stream).  After the opening
+    barrier the ranks agree on a start instant a few ms ahead on CLOCK_MONOTONIC
+    (time.perf_counter on Linux: one clock for every process of the node) and each waits
+    for it, so the barrier's release skew between processes is not charged to the job; each
+    rank stamps its start when it begins and its end after its final synchronize, and the
+    job's time is the latest end minus the earliest start over ranks (a rank that missed
+    the common start is counted late; the closing barrier's own latency is not work; at
+    N = 1 it is the rank's own span)."""
     stream = torch.cuda.current_stream(d.dev)
     e0 = torch.cuda.Event(enable_timing=True)
     e1 = torch.cuda.Event(enable_timing=True)
     d.barrier()
     torch.cuda.synchronize(d.dev)
+    t_start = d.max(time.perf_counter()) + START_MARGIN_S
+    while time.perf_counter() < t_start:
+        pass
     t0 = time.perf_counter()
     e0.record(stream)
     for _ in range(steps):
