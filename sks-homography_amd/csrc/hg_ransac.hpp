@@ -258,9 +258,10 @@ inline uint64_t reduce_magic(uint32_t d) {
 // staging to fit the block's LDS (checked on the host).
 // PAIR (P even): hypotheses j and j+1 of a lane are solved together as the two halves of
 // packed f32x2 values, so each v_pk_mul_f32 / v_pk_add_f32 does the same IEEE operation
-// for both (the same bits as two scalar solves); the divisions stay scalar per half.
+// for both (the values of two scalar solves; only an SKS NaN's sign may differ, since a
+// packed subtraction is an add with a negate modifier); the divisions stay scalar per half.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
-          int DRAWS = kDrawsIndexed, int MOD64 = 0, bool PAIR = false>
+          int DRAWS = kDrawsIndexed, int RED = 0, bool PAIR = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -308,8 +309,8 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
                 f32x2 s[8], tt[8], hp[9];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
-                    const float4 a = pool[reduce_index<MOD64>(cur[j][k], magic, npool)];
-                    const float4 b = pool[reduce_index<MOD64>(cur[j + 1][k], magic, npool)];
+                    const float4 a = pool[reduce_index<RED>(cur[j][k], magic, npool)];
+                    const float4 b = pool[reduce_index<RED>(cur[j + 1][k], magic, npool)];
                     s[2 * k] = f32x2{a.x, b.x}; s[2 * k + 1] = f32x2{a.y, b.y};
                     tt[2 * k] = f32x2{a.z, b.z}; tt[2 * k + 1] = f32x2{a.w, b.w};
                 }
@@ -320,10 +321,10 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
         } else {
 #pragma unroll
             for (int j = 0; j < P; ++j) {
-                const uint32_t id[4] = {reduce_index<MOD64>(cur[j].x, magic, npool),
-                                        reduce_index<MOD64>(cur[j].y, magic, npool),
-                                        reduce_index<MOD64>(cur[j].z, magic, npool),
-                                        reduce_index<MOD64>(cur[j].w, magic, npool)};
+                const uint32_t id[4] = {reduce_index<RED>(cur[j].x, magic, npool),
+                                        reduce_index<RED>(cur[j].y, magic, npool),
+                                        reduce_index<RED>(cur[j].z, magic, npool),
+                                        reduce_index<RED>(cur[j].w, magic, npool)};
                 float s[8], tt[8];
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -646,7 +647,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // tile's draws where they are used (nothing to hide when the draws are computed).  The
 // shipped shapes are launch_sample_seeded_shipped's; every parameter is open for the
 // variant sweep (hg_tune_sample_seeded).
-template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, int MOD64 = 0, int PF = 0,
+template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, int RED = 0, int PF = 0,
           bool PAIR = false>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
@@ -674,10 +675,10 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     per_cu = per_cu < 1 ? 1 : (per_cu > 8 ? 8 : per_cu);
     const int64_t cap = per_cu * cu_count();
     const unsigned g = (unsigned)(want < cap ? want : cap);
-    const uint64_t magic = reduce_magic<MOD64>(npool);
+    const uint64_t magic = reduce_magic<RED>(npool);
 #define HG_SD(A, N)                                                                         \
     do {                                                                                    \
-        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, MOD64, PAIR>;             \
+        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, RED, PAIR>;               \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
         rc = launch(k, g, WPB * kWave, lds, s, ps, pt, npool, magic, nullptr, H, n, bits_base, \
                     odd);                                                                   \
