@@ -130,12 +130,13 @@ def test_score_special_values_vs_oracle(oracle, pkg, dev):
         np.testing.assert_array_equal(got, oracle.ransac_score(H, ps, pt, thresh))
 
 
-@pytest.mark.parametrize("npool", [1, 3, 2540, 20_000])
+@pytest.mark.parametrize("npool", [1, 3, 2540, 5000, 20_000])
 def test_sample_solve_seeded_vs_oracle(orc, oracle, pkg, dev, npool):
     """The seeded fused sampler (draws made in the kernel) equals fill_bits + the indexed
     sampler bit for bit, and both equal the oracle: LDS-pool and global-gather forms
-    (npool 20 000 exceeds the LDS pool), ragged batches, offsets past 2^32, both solvers,
-    normalised or not."""
+    (npool 20 000 exceeds the LDS pool; at 5000 the seeded launch keeps the pool in LDS,
+    past its 64 KiB opt-in, while the indexed one gathers from global memory), ragged
+    batches, offsets past 2^32, both solvers, normalised or not."""
     g = np.random.default_rng(npool + 1)
     ps = (g.random((npool, 2)) * 1000).astype(np.float32)
     pt = (g.random((npool, 2)) * 1000).astype(np.float32)
