@@ -44,6 +44,13 @@ def parse():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--problems-per-gpu", "--n", dest="n", type=int, default=10_000_000,
                     help="problems per GPU (--n is ambiguous under torchrun: use the long name)")
+    ap.add_argument("--algo", default="aca", choices=["aca", "sks", "ge", "gpt"],
+                    help="the headline solver (aca: BASELINE configs[1]; sks: configs[2])")
+    ap.add_argument("--layout", default="aos", choices=["aos", "soa"],
+                    help="aos: (n,8) -> (n,9), normalised as sks::runKernel_*; soa: (8,n) -> "
+                         "(9,n), unnormalised as cal_Homo_*")
+    ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
+    ap.add_argument("--seed", type=int, default=SEED, help="input stream seed")
     ap.add_argument("--rect-batch", type=int, default=65536)
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline")
     ap.add_argument("--no-extras", action="store_true", help="ACA headline only")
@@ -921,6 +928,8 @@ def main():
     except (AttributeError, RuntimeError, ValueError):
         numa["bdf_matches_device"] = None
     pkg = ge.load_package()
+    global SEED
+    SEED = args.seed
     n = args.n
     n_total = n * d.world
     src, tar = rank_block_inputs(pkg, d.dev, n, n_total, d.rank)
@@ -930,14 +939,48 @@ def main():
     def run(algo):
         return lambda: pkg.solve(algo, src, tar, normalize=True, out=H)
 
+    # the headline: BASELINE configs[1] by default (ACA, AoS f32, normalised); --algo /
+    # --layout / --dtype pick another solver or the reference GPU harness's layout over the
+    # same rank block (the sections after the headline keep the default buffers)
+    head_algo, head_layout, head_dtype = args.algo, args.layout, args.dtype
+    head_norm = head_layout == "aos"
+    default_head = (head_algo, head_layout, head_dtype) == ("aca", "aos", "f32")
+    if default_head:
+        run_head = run("aca")
+    else:
+        hs = src.double() if head_dtype == "f64" else src
+        ht = tar.double() if head_dtype == "f64" else tar
+        if head_layout == "soa":
+            hs, ht = hs.t().contiguous(), ht.t().contiguous()
+        hH = torch.empty((9, n) if head_layout == "soa" else (n, 9), dtype=hs.dtype, device=d.dev)
+
+        def run_head():
+            pkg.solve(head_algo, hs, ht, normalize=head_norm, layout=head_layout, out=hH)
+    bpp_head = pkg.BYTES_PER_PROBLEM[head_dtype]
+
     for _ in range(args.warmup):
-        run("aca")()
-    wall, ms_launch = timed_region(d, run("aca"), args.steps)
+        run_head()
+    wall, ms_launch = timed_region(d, run_head, args.steps)
     value = n_total * args.steps / wall / 1e6
-    per_launch = launch_stats(d, run("aca"))
-    achieved = n * bpp / (ms_launch * 1e-3) / 1e9
+    per_launch = launch_stats(d, run_head)
+    achieved = n * bpp_head / (ms_launch * 1e-3) / 1e9
     # the committed PMC figures are per launch at the bench's 10 M; another size has none
-    traffic = pmc_traffic("aca_f32_aos_norm") if n == 10_000_000 else None
+    traffic = (pmc_traffic(f"{head_algo}_{head_dtype}_{head_layout}_norm")
+               if n == 10_000_000 and head_norm else None)
+    if default_head:
+        workload = ("ACA general-quad 4-point homography, AoS f32, normalised (H[8]=1), "
+                    "batch=10M per GPU (BASELINE configs[1]; configs[4] at 8 GPUs)")
+        kernel = "hg::solve_aos<ACA,NORM,f32,P=2,nt|lds-dma> (hg_aos.hpp)"
+    else:
+        workload = (f"{head_algo.upper()} 4-point homography, {head_layout.upper()} {head_dtype}, "
+                    + ("normalised (H[8]=1)" if head_norm else "unnormalised (cal_Homo_* contract)")
+                    + f", batch={n / 1e6:g}M per GPU"
+                    + (" (BASELINE configs[2])" if (head_algo, head_layout, head_dtype, n) ==
+                       ("sks", "aos", "f32", 10_000_000) else ""))
+        kernel = (f"hg::solve_aos<{head_algo.upper()},NORM,{head_dtype},P={2 if head_dtype == 'f32' else 1},"
+                  "nt|lds-dma> (hg_aos.hpp)" if head_layout == "aos" else
+                  f"hg::solve_soa_narrow / solve_soa_vec <{head_algo.upper()},{head_dtype}> "
+                  "(hg_soa.hpp; the dispatcher picks by size and alignment)")
     line = {
         "metric": "M homographies/sec (ACA & SKS) at batch=10M; achieved HBM GB/s vs roofline",
         "value": round(value, 2),
@@ -949,20 +992,19 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
-        "data": "synthetic (on-device counter-based U[0,1024) coordinates, seed 11)",
+        "dtype": head_dtype,
+        "data": f"synthetic (on-device counter-based U[0,1024) coordinates, seed {SEED})",
         "config": {
-            "workload": "ACA general-quad 4-point homography, AoS f32, normalised (H[8]=1), "
-                        "batch=10M per GPU (BASELINE configs[1]; configs[4] at 8 GPUs)",
-            "algo": "aca", "batch_per_gpu": n, "global_batch": n_total, "layout": "aos",
+            "workload": workload,
+            "algo": head_algo, "batch_per_gpu": n, "global_batch": n_total, "layout": head_layout,
             "parallelism": f"dp{d.world} (contiguous shards, no data-path collective)",
         },
         "roofline": {
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "kernel": "hg::solve_aos<ACA,NORM,f32,P=2,nt|lds-dma> (hg_aos.hpp)",
-            "algorithmic_bytes_per_launch": n * bpp,
+            "kernel": kernel,
+            "algorithmic_bytes_per_launch": n * bpp_head,
             "launch_ms": round(ms_launch, 5),
         },
         "launch_stats": per_launch,
@@ -1013,7 +1055,9 @@ def main():
         try:
             if d.rank == args.inject_extras_failure:
                 raise RuntimeError("injected failure (--inject-extras-failure)")
-            line["reference_statistic"] = reference_statistic(d, run("aca"))
+            line["reference_statistic"] = reference_statistic(d, run_head)
+            # the ratios below are against ACA f32 AoS, the default headline
+            ms_aca = ms_launch if default_head else timed_region(d, run("aca"), args.steps)[1]
             for _ in range(args.warmup):
                 run("sks")()
             wall_s, ms_s = timed_region(d, run("sks"), args.steps)
@@ -1022,7 +1066,7 @@ def main():
                 "ms_per_step": round(wall_s / args.steps * 1e3, 5),
                 "achieved_gbps": round(n * bpp / (ms_s * 1e-3) / 1e9, 1),
                 "frac": round(n * bpp / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "sks_over_aca_time": round(ms_s / ms_launch, 3),
+                "sks_over_aca_time": round(ms_s / ms_aca, 3),
                 "traffic": pmc_traffic("sks_f32_aos_norm") if n == 10_000_000 else None,
             }
             # the reference's RHO-GE comparison baseline on the same inputs
@@ -1033,7 +1077,7 @@ def main():
                 "value": round(n_total * args.steps / wall_g / 1e6, 2), "unit": "M homographies/s",
                 "ms_per_step": round(wall_g / args.steps * 1e3, 5),
                 "achieved_gbps": round(n * bpp / (ms_g * 1e-3) / 1e9, 1),
-                "aca_speedup_over_ge": round(ms_g / ms_launch, 3),
+                "aca_speedup_over_ge": round(ms_g / ms_aca, 3),
                 "note": "all three closed forms are HBM-bound on MI355X: FLOP savings no longer "
                         "show at 10M; the CPU baseline shows them",
             }

@@ -43,3 +43,21 @@ def test_bench_line_contract():
         assert k in cb, k
     assert cb["kind"] == "reference" and cb["cores"] >= 1 and cb["all_core_output_bit_exact"]
     assert d["numa"]["per_rank"][0]["rank"] == 0
+
+
+@pytest.mark.parametrize("algo,layout,dtype,bpp", [("sks", "aos", "f32", 100), ("gpt", "soa", "f64", 200)])
+def test_bench_headline_selection(algo, layout, dtype, bpp):
+    """--algo / --layout / --dtype / --seed pick the headline (SURVEY 5's bench flags): the
+    line names the workload, its dtype, layout and algorithmic bytes, and the value still
+    follows from its own ms_per_step."""
+    n, steps = 100_000, 5
+    r = subprocess.run([sys.executable, "bench.py", "--problems-per-gpu", str(n), "--steps", str(steps),
+                        "--warmup", "2", "--no-extras", "--no-cpu", "--algo", algo, "--layout", layout,
+                        "--dtype", dtype, "--seed", "3"],
+                       cwd=ROOT, capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads([x for x in r.stdout.splitlines() if x.startswith("{")][-1])
+    assert d["dtype"] == dtype and d["config"]["algo"] == algo and d["config"]["layout"] == layout
+    assert algo.upper() in d["config"]["workload"] and "seed 3" in d["data"]
+    assert d["roofline"]["algorithmic_bytes_per_launch"] == n * bpp
+    assert abs(d["value"] - n / d["ms_per_step"] / 1e3) / d["value"] < 0.01
