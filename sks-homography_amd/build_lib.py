@@ -8,6 +8,7 @@ hipcc, gfx950 only.  Numerics flags are part of the contract, not tuning:
 """
 from __future__ import annotations
 
+import concurrent.futures
 import os
 import shutil
 import subprocess
@@ -52,7 +53,7 @@ def build(verbose: bool = False, force: bool = False) -> str:
     headers = [os.path.join(CSRC, f) for f in os.listdir(CSRC) if f.endswith((".hpp", ".h"))]
     headers += [os.path.join(ROOT, "include", f) for f in os.listdir(os.path.join(ROOT, "include"))]
     headers.append(os.path.abspath(__file__))  # a flag change here rebuilds every object
-    objs, tune_objs = [], []
+    objs, tune_objs, cmds = [], [], []
     for src in SOURCES + TUNE_SOURCES:
         path = os.path.join(CSRC, src)
         obj = os.path.join(BUILD, os.path.splitext(src)[0] + ".o")
@@ -69,7 +70,11 @@ def build(verbose: bool = False, force: bool = False) -> str:
             cmd[1:1] = ["-x", "c++", "-D__HIP_PLATFORM_AMD__", "-I/opt/rocm/include"]
         if verbose:
             print(" ".join(cmd))
-        subprocess.run(cmd, check=True)
+        cmds.append(cmd)
+    # the translation units are independent: compile them side by side (at most 4 at once)
+    with concurrent.futures.ThreadPoolExecutor(max_workers=min(4, max(1, len(cmds)))) as ex:
+        for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
+            f.result()
     if force or _stale(LIB, objs):
         cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
         if verbose:
