@@ -108,6 +108,8 @@ for step in $STEPS; do
         hbm_ceilings) run hbm_ceilings 300 python tools/hbm_ceilings.py ;;
         kbench_f64) run kbench_f64 300 python tools/kbench_f64.py ;;
         soa_streams) run soa_streams 300 python tools/soa_streams.py ;;
+        soa_streams_f64)  # the 25-row pattern at the binary64 10 M size, beside the shipped solvers
+            SOA_READ_TOTAL=1280000000 SOA_SHAPES=0 SOA_SOLVE=1 run soa_streams_f64 300 python tools/soa_streams.py ;;
         hbm_policy) run hbm_policy 300 python tools/hbm_policy.py ;;
         host_probe) run host_probe 300 python tools/host_probe.py ;;
         numa_probe) run numa_probe 300 python tools/numa_probe.py ;;
