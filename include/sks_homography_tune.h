@@ -67,9 +67,8 @@ int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void*
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
                     int64_t pitch_bytes, void* stream);
 
-/* Seeded fused sampler, (P, waves per block[, draws in place]): 0 shipped (packed pairs:
- * SKS (2, 8); ACA (2, 4) from 4 M hypotheses, (1, 16) below), 13 (1, 16, in place) -- the
- * round-1 shipped form,
+/* Seeded fused sampler, (P, waves per block[, draws in place]): 0 shipped (packed pairs,
+ * (2, 8); ACA from 4 M hypotheses (2, 4)), 13 (1, 16, in place) -- the round-1 shipped form,
  * 1 (2, 4), 2 (1, 16), 3 (2, 16), 4 (2, 8) with the 64-bit remainder, 5 / 6 one hash per draw
  * (a different stream) at (2, 4) / (2, 8), 7 (2, 8, in place), 8 (2, 4, in place), 9 (2, 8)
  * -- the previous shipped form; 10 / 11 / 12 (2, 8 / 16 / 4, in place) with the two

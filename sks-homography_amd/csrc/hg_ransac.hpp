@@ -690,25 +690,23 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     return rc;
 }
 
-// The shipped seeded shapes, all solving two hypotheses per lane as packed f32x2 pairs
-// (the indexed sampler's arithmetic, so a seeded launch equals fill_bits + an indexed one
-// to the NaN bit): SKS with 8 waves per block; ACA with 4 from kSeededPairMinN hypotheses
-// (fewer resident waves, fewer concurrent write streams: the launch is within ~7 % of the
-// write-only HBM ceiling there), below it the P = 1, 16-wave form, which keeps more waves
-// in flight for a short launch.  16 M: ACA 109-113 vs 118-126 us, SKS 131-133 vs 147-155
-// (tools/kbench_sample.py, profiles/r02/kbench_pair*.json).
+// The shipped seeded shapes, all solving two hypotheses per lane as packed f32x2 pairs --
+// the arithmetic of the indexed sampler and of both global-gather fallbacks, so a seeded
+// launch equals fill_bits + an indexed one to the last bit, NaN signs included (packed and
+// scalar solves agree on every value but not always on a NaN's sign).  8 waves per block;
+// ACA from kSeededPairMinN hypotheses 4 (fewer resident waves, fewer concurrent write
+// streams: the launch is within ~10 % of the write-only HBM ceiling there).  16 M: ACA
+// 109-114 vs 118-126 us for the round-1 P = 1 scalar form, SKS 131-133 vs 147-155; at 1 M
+// ACA pays ~5 % against that form (tools/kbench_sample.py, profiles/r02/kbench_pair*).
 constexpr int64_t kSeededPairMinN = int64_t(1) << 22;
 inline int launch_sample_seeded_shipped(const float2* ps, const float2* pt, uint32_t npool,
                                         uint64_t seed, uint64_t offset, float* H, int64_t n,
                                         int algo, bool norm, hipStream_t s) {
-    if (algo != 0)
-        return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset,
-                                                                         H, n, algo, norm, s);
-    if (n >= kSeededPairMinN)
-        return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset,
-                                                                         H, n, algo, norm, s);
-    return launch_sample_seeded<1, 16, kDrawsPaired, false, 0, false>(ps, pt, npool, seed, offset,
-                                                                       H, n, algo, norm, s);
+    if (algo == 0 && n >= kSeededPairMinN)
+        return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, true>(ps, pt, npool, seed, offset,
+                                                                     H, n, algo, norm, s);
+    return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, true>(ps, pt, npool, seed, offset, H,
+                                                                 n, algo, norm, s);
 }
 
 // Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice

@@ -193,3 +193,32 @@ def test_generators_validate_out(pkg, dev):
     assert pkg.fill_uniform(10, 1, out=o) is o
     with pytest.raises(ValueError, match="stream_copy"):
         pkg.stream_copy(torch.zeros(8, device=dev), torch.zeros(4, device=dev))
+
+
+from hypothesis import HealthCheck, given, settings  # noqa: E402
+from hypothesis import strategies as st  # noqa: E402
+from hypothesis.extra.numpy import arrays  # noqa: E402
+
+
+@settings(max_examples=25, deadline=None, suppress_health_check=list(HealthCheck))
+@given(pool=arrays(np.float32, st.tuples(st.integers(1, 48), st.just(4)),
+                   elements=st.floats(width=32, allow_nan=True, allow_infinity=True,
+                                      allow_subnormal=True)),
+       n=st.integers(1, 300), seed=st.integers(0, 2**32), off=st.integers(0, 2**34))
+def test_samplers_on_arbitrary_pools(orc, oracle, pkg, dev, pool, n, seed, off):
+    """Pools of arbitrary binary32 bit patterns (subnormals, +-Inf, NaN, huge and tiny values
+    drawn by hypothesis): the packed-pair samplers -- seeded and indexed -- agree with each
+    other bit for bit and with the scalar oracle NaN for NaN, both solvers, normalised or not
+    (the packed f32 instructions keep subnormals exactly as the scalar ones do)."""
+    ps = np.ascontiguousarray(pool[:, :2])
+    pt = np.ascontiguousarray(pool[:, 2:])
+    dps, dpt = torch.from_numpy(ps).to(dev), torch.from_numpy(pt).to(dev)
+    bits = pkg.fill_bits(n * 4, seed, off, dev).view(n, 4)
+    s, t = oracle.sample_problems(ps, pt, bits.cpu().numpy())
+    for algo in ("aca", "sks"):
+        for norm in (True, False):
+            H = pkg.sample_solve_seeded(dps, dpt, n, seed, off, algo=algo, normalize=norm)
+            ref = pkg.sample_solve(dps, dpt, bits, algo=algo, normalize=norm)
+            assert torch.equal(H.view(torch.int32), ref.view(torch.int32)), (algo, norm)
+            ok = orc.same_bits(H.cpu().numpy(), oracle.solve(algo, s, t, normalize=norm))
+            assert ok.all(), f"{algo} norm={norm}: {(~ok).sum()} differ"

@@ -24,7 +24,7 @@ NAMES = {0: "global gather P2 (scalar)", 1: "LDS pool P1", 2: "LDS pool P2 (roun
          8: "LDS pool P2, packed f32x2 pairs (shipped)"}
 if os.environ.get("KB_INDEXED_VARIANTS"):  # e.g. "0,2,8"
     NAMES = {int(v): NAMES[int(v)] for v in os.environ["KB_INDEXED_VARIANTS"].split(",")}
-SEEDED = {0: "seeded shipped (packed pairs; ACA below 4 M: P1, 16 waves)", 1: "seeded P2, 4 waves/block",
+SEEDED = {0: "seeded shipped (packed pairs; 8 waves, ACA from 4 M 4)", 1: "seeded P2, 4 waves/block",
           2: "seeded P1, 16 waves/block", 3: "seeded P2, 16 waves/block",
           4: "seeded P2, 8 waves/block, 64-bit remainder",
           5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw",
