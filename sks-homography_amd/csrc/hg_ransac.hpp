@@ -258,8 +258,8 @@ inline uint64_t reduce_magic(uint32_t d) {
 // staging to fit the block's LDS (checked on the host).
 // PAIR (P even): hypotheses j and j+1 of a lane are solved together as the two halves of
 // packed f32x2 values, so each v_pk_mul_f32 / v_pk_add_f32 does the same IEEE operation
-// for both (the values of two scalar solves; only an SKS NaN's sign may differ, since a
-// packed subtraction is an add with a negate modifier); the divisions stay scalar per half.
+// for both (the values of two scalar solves; only a NaN's sign may differ, since a packed
+// subtraction is an add with a negate modifier); the divisions stay scalar per half.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
           int DRAWS = kDrawsIndexed, int RED = 0, bool PAIR = false>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
