@@ -45,7 +45,7 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
 
 /* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2), 3 P = 2 with
  * two-tile prefetch, 4-6 wider blocks, 7 P = 2 with the 64-bit remainder, 8 P = 2 solved as
- * packed f32x2 pairs. */
+ * packed f32x2 pairs (shipped), 9 the same with the pairs' divisions split into scalar ones. */
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream);
 
@@ -72,8 +72,10 @@ int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
  * 1 (2, 4), 2 (1, 16), 3 (2, 16), 4 (2, 8) with the 64-bit remainder, 5 / 6 one hash per draw
  * (a different stream) at (2, 4) / (2, 8), 7 (2, 8, in place), 8 (2, 4, in place), 9 (2, 8)
  * -- the previous shipped form; 10 / 11 / 12 (2, 8 / 16 / 4, in place) with the two
- * hypotheses of a lane solved as packed f32x2 pairs.  "In place": each tile's draws made
- * where they are used rather than one tile ahead. */
+ * hypotheses of a lane solved as packed f32x2 pairs whose divisions split into scalar
+ * expansions (10 and 12: the round-2 shipped forms; 0 packs the divisions' FMA steps too);
+ * 14-18 the packed-division pairs with other remainders / ablations.  "In place": each
+ * tile's draws made where they are used rather than one tile ahead. */
 int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_tar,
                           uint32_t npool, uint64_t seed, uint64_t offset, float* H, int64_t n,
                           int algo, int flags, void* stream);

@@ -22,7 +22,6 @@ namespace hg {
 
 constexpr uint64_t kBitsMul = 0xA0761D6478BD642Full;
 
-typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef int i32x2 __attribute__((ext_vector_type(2)));
 
 // Word w of stream S = seed * kBitsMul is one half of the splitmix64 finaliser of counter
@@ -55,6 +54,13 @@ static __global__ __launch_bounds__(kBlock) void fill_bits_kernel(uint32_t* __re
         }
     }
 }
+
+// How a lane's two paired hypotheses divide (PAIR; 0 = one hypothesis at a time): both
+// solve as the halves of packed f32x2 values, and their divisions either split into two
+// scalar expansions (kPairScalarDiv, the round-2 form, tune only) or run as one expansion
+// whose FMA steps are packed too (kPairPacked, shipped; div_rn in hg_solvers.hpp).
+constexpr int kPairScalarDiv = 1;
+constexpr int kPairPacked = 2;
 
 // Where a hypothesis' four draws come from.
 constexpr int kDrawsIndexed = 0;  // row p of the (n,4) index array
@@ -96,7 +102,7 @@ __device__ __forceinline__ u32x4 draws4(const uint4* idx, uint64_t bits_base, bo
 // (npool x 8 B per side: L2/L1-resident), solves, and the H rows leave through the
 // LDS-staged 16-B stores.  Index r of a row selects pool[r % npool], as get_rand_list
 // does (.cu:56-59, modulo bias and duplicates included).
-template <int ALGO, bool NORM, int P, int DRAWS = kDrawsIndexed, bool PAIR = false>
+template <int ALGO, bool NORM, int P, int DRAWS = kDrawsIndexed, int PAIR = 0>
 __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     const uint4* __restrict__ idx, float* __restrict__ H, int64_t n, uint64_t bits_base = 0,
@@ -147,7 +153,7 @@ __global__ __launch_bounds__(kBlock) void sample_solve_kernel(
                 s[2 * k] = f32x2{as.x, bs.x}; s[2 * k + 1] = f32x2{as.y, bs.y};
                 t[2 * k] = f32x2{at.x, bt.x}; t[2 * k + 1] = f32x2{at.y, bt.y};
             }
-            solve<ALGO, NORM>(s, t, hp);
+            solve<ALGO, NORM, PAIR == kPairPacked>(s, t, hp);
 #pragma unroll
             for (int k = 0; k < 9; ++k) { h[j][k] = hp[k].x; h[j + 1][k] = hp[k].y; }
         }
@@ -261,7 +267,7 @@ inline uint64_t reduce_magic(uint32_t d) {
 // for both (the values of two scalar solves; only a NaN's sign may differ, since a packed
 // subtraction is an add with a negate modifier); the divisions stay scalar per half.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
-          int DRAWS = kDrawsIndexed, int RED = 0, bool PAIR = false>
+          int DRAWS = kDrawsIndexed, int RED = 0, int PAIR = 0>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -314,7 +320,7 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
                     s[2 * k] = f32x2{a.x, b.x}; s[2 * k + 1] = f32x2{a.y, b.y};
                     tt[2 * k] = f32x2{a.z, b.z}; tt[2 * k + 1] = f32x2{a.w, b.w};
                 }
-                solve<ALGO, NORM>(s, tt, hp);
+                solve<ALGO, NORM, PAIR == kPairPacked>(s, tt, hp);
 #pragma unroll
                 for (int k = 0; k < 9; ++k) { h[j][k] = hp[k].x; h[j + 1][k] = hp[k].y; }
             }
@@ -569,14 +575,16 @@ inline int cu_count() {
 // variant -1 = shipped choice; 0 = global-gather kernel (P = 2); 1 / 2 = LDS-pool kernel
 // P = 1 / 2; 3 = LDS-pool P = 2 with the index rows two tiles ahead; 4 = LDS-pool P = 2
 // with the 64-bit remainder (fastmod64_u32); 5 = LDS-pool P = 2, the two hypotheses of a
-// lane solved as packed f32x2 pairs.  The LDS forms fall back to 0 when the pool does not
-// fit.
+// lane solved as packed f32x2 pairs (shipped); 6 = 5 with the pairs' divisions split into
+// scalar expansions (the round-2 form, kPairScalarDiv).  The LDS forms fall back to 0 when
+// the pool does not fit.
 inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, uint32_t npool,
                         const uint4* ix, float* H, int64_t n, int algo, bool norm, hipStream_t s) {
     constexpr int kShippedP = 2;
     const bool pf2 = variant == 3;
     const bool mod64 = variant == 4;
-    const bool pair = variant == 5 || variant == -1;  // shipped: P = 2 packed pairs
+    const bool pair = variant == 5 || variant == 6 || variant == -1;  // shipped: P = 2 packed pairs
+    const bool split_div = variant == 6;
     int use_p = variant == -1 ? kShippedP : (pf2 || mod64 || pair ? 2 : variant);
     const size_t lds = use_p == 1 ? sample_lds_bytes<1>(npool) : sample_lds_bytes<2>(npool);
     if (use_p > 0 && lds > kSampleLdsMax) use_p = 0;
@@ -588,12 +596,16 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 #define HG_SS(A, N, PR)                                                                          \
     launch(sample_solve_kernel<A, N, P, kDrawsIndexed, PR>, g, kBlock, 0, s, ps, pt, npool, ix, H, n, \
            0, 0)
-        if (pair) {
-            if (algo == 0) return norm ? HG_SS(kACA, true, true) : HG_SS(kACA, false, true);
-            return norm ? HG_SS(kSKS, true, true) : HG_SS(kSKS, false, true);
+        if (pair && split_div) {
+            if (algo == 0) return norm ? HG_SS(kACA, true, kPairScalarDiv) : HG_SS(kACA, false, kPairScalarDiv);
+            return norm ? HG_SS(kSKS, true, kPairScalarDiv) : HG_SS(kSKS, false, kPairScalarDiv);
         }
-        if (algo == 0) return norm ? HG_SS(kACA, true, false) : HG_SS(kACA, false, false);
-        return norm ? HG_SS(kSKS, true, false) : HG_SS(kSKS, false, false);
+        if (pair) {
+            if (algo == 0) return norm ? HG_SS(kACA, true, kPairPacked) : HG_SS(kACA, false, kPairPacked);
+            return norm ? HG_SS(kSKS, true, kPairPacked) : HG_SS(kSKS, false, kPairPacked);
+        }
+        if (algo == 0) return norm ? HG_SS(kACA, true, 0) : HG_SS(kACA, false, 0);
+        return norm ? HG_SS(kSKS, true, 0) : HG_SS(kSKS, false, 0);
 #undef HG_SS
     }
     // persistent: as many blocks as fit at once (LDS-limited), never more than the tiles
@@ -620,11 +632,15 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 #undef HG_SL64
     }
     if (pair) {
-#define HG_SLP(A, N)                                                                             \
-    launch(sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, false, true>, g,     \
-           kBlock, lds, s, ps, pt, npool, magic, ix, H, n, 0, 0)
-        if (algo == 0) return norm ? HG_SLP(kACA, true) : HG_SLP(kACA, false);
-        return norm ? HG_SLP(kSKS, true) : HG_SLP(kSKS, false);
+#define HG_SLP(A, N, PR)                                                                         \
+    launch(sample_solve_lds_kernel<A, N, 2, 1, kWavesPerBlock, kDrawsIndexed, 0, PR>, g, kBlock, \
+           lds, s, ps, pt, npool, magic, ix, H, n, 0, 0)
+        if (split_div) {
+            if (algo == 0) return norm ? HG_SLP(kACA, true, kPairScalarDiv) : HG_SLP(kACA, false, kPairScalarDiv);
+            return norm ? HG_SLP(kSKS, true, kPairScalarDiv) : HG_SLP(kSKS, false, kPairScalarDiv);
+        }
+        if (algo == 0) return norm ? HG_SLP(kACA, true, kPairPacked) : HG_SLP(kACA, false, kPairPacked);
+        return norm ? HG_SLP(kSKS, true, kPairPacked) : HG_SLP(kSKS, false, kPairPacked);
 #undef HG_SLP
     }
     if (!pf2) {
@@ -648,7 +664,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // shipped shapes are launch_sample_seeded_shipped's; every parameter is open for the
 // variant sweep (hg_tune_sample_seeded).
 template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, int RED = 0, int PF = 0,
-          bool PAIR = false>
+          int PAIR = 0>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
                                 bool norm, hipStream_t s) {
@@ -703,10 +719,10 @@ inline int launch_sample_seeded_shipped(const float2* ps, const float2* pt, uint
                                         uint64_t seed, uint64_t offset, float* H, int64_t n,
                                         int algo, bool norm, hipStream_t s) {
     if (algo == 0 && n >= kSeededPairMinN)
-        return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, true>(ps, pt, npool, seed, offset,
-                                                                     H, n, algo, norm, s);
-    return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, true>(ps, pt, npool, seed, offset, H,
-                                                                 n, algo, norm, s);
+        return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, kPairPacked>(ps, pt, npool, seed,
+                                                                            offset, H, n, algo, norm, s);
+    return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked>(ps, pt, npool, seed, offset,
+                                                                        H, n, algo, norm, s);
 }
 
 // Four hypotheses per lane (two packed pairs): each scalar-loaded point feeds twice

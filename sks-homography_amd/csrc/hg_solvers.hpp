@@ -13,6 +13,46 @@
 
 namespace hg {
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// a / b, correctly rounded: the language's IEEE division.
+template <bool PK, typename T>
+__device__ __forceinline__ T div_rn(T a, T b) {
+    return a / b;
+}
+
+// Two binary32 divisions carried as the halves of packed f32x2 values (the RANSAC
+// samplers' paired hypotheses).  PK = false leaves them to the compiler, which splits
+// them into two scalar expansions.  PK = true issues that same expansion -- v_div_scale
+// of both operands, v_rcp, the three Newton-Raphson steps on the reciprocal and the
+// quotient, v_div_fmas, v_div_fixup -- once per half for the non-packed instructions, and
+// its six FMA / multiply steps once for both halves as v_pk_fma_f32 / v_pk_mul_f32 (22
+// VALU instructions per pair of divisions -> 16).  The same instructions on the same
+// operands, so the same bits as a / b, NaNs included.
+template <bool PK>
+__device__ __forceinline__ f32x2 div_rn(f32x2 a, f32x2 b) {
+    if constexpr (!PK) {
+        return a / b;
+    } else {
+        bool fx, fy, unused;
+        const f32x2 den = {__builtin_amdgcn_div_scalef(a.x, b.x, false, &unused),
+                           __builtin_amdgcn_div_scalef(a.y, b.y, false, &unused)};
+        const f32x2 num = {__builtin_amdgcn_div_scalef(a.x, b.x, true, &fx),
+                           __builtin_amdgcn_div_scalef(a.y, b.y, true, &fy)};
+        const f32x2 r0 = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+        const f32x2 nden = -den, one = {1.0f, 1.0f};
+        const f32x2 e0 = __builtin_elementwise_fma(nden, r0, one);
+        const f32x2 r1 = __builtin_elementwise_fma(e0, r0, r0);
+        const f32x2 q0 = num * r1;
+        const f32x2 e1 = __builtin_elementwise_fma(nden, q0, num);
+        const f32x2 q1 = __builtin_elementwise_fma(e1, r1, q0);
+        const f32x2 e2 = __builtin_elementwise_fma(nden, q1, num);
+        return f32x2{
+            __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e2.x, r1.x, q1.x, fx), b.x, a.x),
+            __builtin_amdgcn_div_fixupf(__builtin_amdgcn_div_fmasf(e2.y, r1.y, q1.y, fy), b.y, a.y)};
+    }
+}
+
 // ACA: H = H_A2^-1 * H_C * H_A1 (C++ Codes/modules/ACA_SKS.cpp:24-82, 85 FLOPs).
 // s, t = {Mx,My,Nx,Ny,Px,Py,Qx,Qy} of the source / target quad.
 template <typename T>
@@ -57,8 +97,8 @@ __device__ __forceinline__ void aca_solve(const T (&s)[8], const T (&t)[8], T (&
 
 // SKS: H = H_S2^-1 * H_K * H_S1 (ACA_SKS.cpp:189-293, 157 FLOPs, three IEEE
 // divisions).  The reference's double literals (`0.5 *`, `1.0 /`) round to the
-// same binary32 result as the binary32 operation used here.
-template <typename T>
+// same binary32 result as the binary32 operation used here.  PK: see div_rn.
+template <bool PK = true, typename T>
 __device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
     const T half = T(0.5), one = T(1);
     // similarities from the M-N anchor pair (:192-206)
@@ -72,7 +112,7 @@ __device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&
     const T d3x = s[4] - o1x, d3y = s[5] - o1y;
     const T g3x = e1x * d3x - e1y * d3y;
     const T g3y = e1y * d3x + e1x * d3y;
-    const T i3 = one / g3y;
+    const T i3 = div_rn<PK>(one, g3y);
     const T k5x = i3 * g3x;
     const T k5y = i3 * f1;
     const T d5x = s[6] - o1x, d5y = s[7] - o1y;
@@ -85,7 +125,7 @@ __device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&
     const T d4x = t[4] - o2x, d4y = t[5] - o2y;
     const T g4x = e2x * d4x - e2y * d4y;
     const T g4y = e2y * d4x + e2x * d4y;
-    const T i4 = one / g4y;
+    const T i4 = div_rn<PK>(one, g4y);
     const T k6x = i4 * g4x;
     const T k6y = i4 * f2;
     const T d6x = t[6] - o2x, d6y = t[7] - o2y;
@@ -98,7 +138,7 @@ __device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&
     const T n1 = z7x * z8x - z7y * z8y;
     const T n2 = z7x * z8y - z7y * z8x;
     const T dd = z7x * z7x - z7y * z7y;
-    const T sc = z7w / (dd * z8w);
+    const T sc = div_rn<PK>(z7w, dd * z8w);
     const T ka = n1 * sc;
     const T kb = n2 * sc;
     const T ku = k6x - ka * k5x - kb * k5y;
@@ -127,9 +167,9 @@ __device__ __forceinline__ void sks_solve(const T (&s)[8], const T (&t)[8], T (&
 
 // Last-element normalisation (ACA_SKS.cpp:94-98): one IEEE reciprocal-by-division,
 // eight multiplies, H[8] := 1.
-template <typename T>
+template <bool PK = true, typename T>
 __device__ __forceinline__ void normalize_h(T (&h)[9]) {
-    const T r = T(1) / h[8];
+    const T r = div_rn<PK>(T(1), h[8]);
 #pragma unroll
     for (int i = 0; i < 8; ++i) h[i] = h[i] * r;
     h[8] = T(1);
@@ -308,13 +348,14 @@ __device__ __forceinline__ void gpt_solve(const T (&s)[8], const T (&t)[8], T (&
 
 enum Algo : int { kACA = 0, kSKS = 1, kGE = 2, kGPT = 3 };
 
-template <int ALGO, bool NORM, typename T>
+// PK: how packed f32x2 pairs divide (div_rn); scalar T divides as the language does.
+template <int ALGO, bool NORM, bool PK = true, typename T>
 __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9]) {
     if constexpr (ALGO == kACA) aca_solve(s, t, h);
-    else if constexpr (ALGO == kSKS) sks_solve(s, t, h);
+    else if constexpr (ALGO == kSKS) sks_solve<PK>(s, t, h);
     else if constexpr (ALGO == kGE) ge_solve(s, t, h);
     else gpt_solve(s, t, h);
-    if constexpr (NORM) normalize_h(h);
+    if constexpr (NORM) normalize_h<PK>(h);
 }
 
 // TensorACA rectangle -> quad (PyTorch Codes/Modules_Runtime_Test.py:294-302),

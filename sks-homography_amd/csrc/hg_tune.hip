@@ -582,11 +582,12 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
     return rc ? -(double)rc : (double)ms * 1e3 / loops;
 }
 
-// Sampler variants for tools/kbench_sample.py (0 global gather, 1 / 2 LDS pool P1 / P2);
+// Sampler variants for tools/kbench_sample.py (0 global gather, 1 / 2 LDS pool P1 / P2;
+// 8 the shipped packed pairs, 9 the same with the pairs' divisions split into scalar ones);
 // same argument checks as hg_sample_solve_f32.
 int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, uint32_t npool,
                    const uint32_t* idx, float* H, int64_t n, int algo, int flags, void* stream) {
-    if (n <= 0 || npool == 0 || variant < 0 || variant > 8 || (algo != 0 && algo != 1))
+    if (n <= 0 || npool == 0 || variant < 0 || variant > 9 || (algo != 0 && algo != 1))
         return (int)hipErrorInvalidValue;
     if (!pool_src || !pool_tar || !idx || !H || (reinterpret_cast<uintptr_t>(idx) & 15u) ||
         (reinterpret_cast<uintptr_t>(H) & 15u) || (reinterpret_cast<uintptr_t>(pool_src) & 7u) ||
@@ -603,6 +604,7 @@ int hg_tune_sample(int variant, const float* pool_src, const float* pool_tar, ui
         case 6: return hg::launch_sample_wide<2, 16>(ps, pt, npool, ix, H, n, algo, norm, st, hg::cu_count());
         case 7: return hg::launch_sample_solve(4, ps, pt, npool, ix, H, n, algo, norm, st);
         case 8: return hg::launch_sample_solve(5, ps, pt, npool, ix, H, n, algo, norm, st);
+        case 9: return hg::launch_sample_solve(6, ps, pt, npool, ix, H, n, algo, norm, st);
         default: break;
     }
     return hg::launch_sample_solve(variant, reinterpret_cast<const float2*>(pool_src),
@@ -632,11 +634,11 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         // the remainder and the draws of the 4-wave packed-pair shape: 14 the binary64
         // remainder (exact); ablations, wrong bits, time only: 15 no remainder, 16 no hash,
         // 17 neither; 18 the 8-wave shape with the binary64 remainder
-        case 14: return launch_sample_seeded<2, 4, kDrawsPaired, 2, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 15: return launch_sample_seeded<2, 4, kDrawsPaired, 3, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 16: return launch_sample_seeded<2, 4, kDrawsCheap, 0, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 17: return launch_sample_seeded<2, 4, kDrawsCheap, 3, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 18: return launch_sample_seeded<2, 8, kDrawsPaired, 2, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 14: return launch_sample_seeded<2, 4, kDrawsPaired, 2, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 15: return launch_sample_seeded<2, 4, kDrawsPaired, 3, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 16: return launch_sample_seeded<2, 4, kDrawsCheap, 0, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 17: return launch_sample_seeded<2, 4, kDrawsCheap, 3, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 18: return launch_sample_seeded<2, 8, kDrawsPaired, 2, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 1: return launch_sample_seeded<2, 4, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 2: return launch_sample_seeded<1, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 3: return launch_sample_seeded<2, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
@@ -646,10 +648,11 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 7: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 8: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 9: return launch_sample_seeded<2, 8, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        // two hypotheses per lane solved as packed f32x2 pairs
-        case 10: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 11: return launch_sample_seeded<2, 16, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
-        case 12: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, true>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // two hypotheses per lane solved as packed f32x2 pairs, their divisions split into
+        // scalar expansions (the round-2 forms; 10 and, from 4 M ACA hypotheses, 12 shipped then)
+        case 10: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 11: return launch_sample_seeded<2, 16, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 12: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -98,6 +98,10 @@ for step in $STEPS; do
             KB_ROUNDS=11 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx 300 python tools/kbench_sample.py
             KB_ROUNDS=11 KB_ALGO=1 KB_INDEXED_VARIANTS=0,2,8 KB_SEEDED_VARIANTS=0,13 run kbench_pair_idx_sks 300 \
                 python tools/kbench_sample.py ;;
+        kbench_pkdiv)  # packed-pair divisions (shipped) vs the round-2 scalar-division pairs, ACA then SKS
+            KB_ROUNDS=11 KB_INDEXED_VARIANTS=0,8,9 KB_SEEDED_VARIANTS=0,10,12 run kbench_pkdiv 300 python tools/kbench_sample.py
+            KB_ROUNDS=11 KB_ALGO=1 KB_INDEXED_VARIANTS=0,8,9 KB_SEEDED_VARIANTS=0,10,12 run kbench_pkdiv_sks 300 \
+                python tools/kbench_sample.py ;;
         kbench_ablate)  # where the seeded sampler's time goes, and the binary64 remainder
             KB_ROUNDS=11 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,13,14,15,16,17 run kbench_ablate 300 python tools/kbench_sample.py
             KB_ROUNDS=11 KB_ALGO=1 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,18 run kbench_ablate_sks 300 \

@@ -1,5 +1,6 @@
 """Fused RANSAC sampler + solver (hg_tune_sample variants: 0 global gather, 1 / 2 pool in
-LDS with P = 1 / 2, 3 prefetch 2, 4-6 wider blocks, 7 the 64-bit remainder) across batch sizes over the reference's orig_pts_wall.txt pool
+LDS with P = 1 / 2, 3 prefetch 2, 4-6 wider blocks, 7 the 64-bit remainder, 8 / 9 packed
+pairs with packed / scalar divisions) across batch sizes over the reference's orig_pts_wall.txt pool
 (tests/golden), and the seeded form (draws made in the kernel, 36 B of H per hypothesis;
 hg_tune_sample_seeded) across tile shapes, either remainder, and the earlier one-hash-per-draw
 stream.  Device time per launch from event-bracketed back-to-back launches,
@@ -21,7 +22,8 @@ import __graft_entry__ as ge  # noqa: E402
 NAMES = {0: "global gather P2 (scalar)", 1: "LDS pool P1", 2: "LDS pool P2 (round-1 shipped)", 3: "LDS pool P2 prefetch 2",
          4: "LDS pool P1, 8 waves/block", 5: "LDS pool P1, 16 waves/block",
          6: "LDS pool P2, 16 waves/block", 7: "LDS pool P2, 64-bit remainder",
-         8: "LDS pool P2, packed f32x2 pairs (shipped)"}
+         8: "LDS pool P2, packed f32x2 pairs, packed divisions (shipped)",
+         9: "LDS pool P2, packed f32x2 pairs, scalar divisions (round-2 form)"}
 if os.environ.get("KB_INDEXED_VARIANTS"):  # e.g. "0,2,8"
     NAMES = {int(v): NAMES[int(v)] for v in os.environ["KB_INDEXED_VARIANTS"].split(",")}
 SEEDED = {0: "seeded shipped (packed pairs; 8 waves, ACA from 4 M 4)", 1: "seeded P2, 4 waves/block",
@@ -30,9 +32,9 @@ SEEDED = {0: "seeded shipped (packed pairs; 8 waves, ACA from 4 M 4)", 1: "seede
           5: "seeded P2, 4 waves/block, one hash per draw", 6: "seeded P2, 8 waves/block, one hash per draw",
           7: "seeded P2, 8 waves/block, draws in place", 8: "seeded P2, 4 waves/block, draws in place",
           9: "seeded P2, 8 waves/block (previous shipped)",
-          10: "seeded P2 paired f32x2, 8 waves/block, in place",
-          11: "seeded P2 paired f32x2, 16 waves/block, in place",
-          12: "seeded P2 paired f32x2, 4 waves/block, in place",
+          10: "seeded P2 paired f32x2, 8 waves/block, scalar divisions (round-2 shipped form)",
+          11: "seeded P2 paired f32x2, 16 waves/block, scalar divisions",
+          12: "seeded P2 paired f32x2, 4 waves/block, scalar divisions (round-2 ACA >= 4 M form)",
           13: "seeded P1, 16 waves/block, draws in place (round-1 shipped)",
           14: "seeded P2 pairs, 4 waves, binary64 remainder",
           15: "ablation: P2 pairs, 4 waves, no remainder (wrong bits)",
