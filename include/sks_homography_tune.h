@@ -43,6 +43,11 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
 int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
                  float b, void* stream);
 
+/* q = a / b elementwise (n even) in packed pairs as the RANSAC samplers divide: packed != 0
+ * the shipped expansion (div_rn, hg_solvers.hpp), 0 the compiler's scalar divisions. */
+int hg_tune_div_pairs(int packed, const float* a, const float* b, float* q, int64_t n,
+                      void* stream);
+
 /* Fused sampler variants: 0 global gather, 1 / 2 pool staged in LDS (P = 1 / 2), 3 P = 2 with
  * two-tile prefetch, 4-6 wider blocks, 7 P = 2 with the 64-bit remainder, 8 P = 2 solved as
  * packed f32x2 pairs (shipped), 9 the same with the pairs' divisions split into scalar ones. */

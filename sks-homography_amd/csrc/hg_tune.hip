@@ -326,9 +326,36 @@ __global__ __launch_bounds__(kBlock) void solve_generic_t(const T* __restrict__ 
     }
 }
 
+// q[i] = a[i] / b[i], two elements per lane as the halves of one f32x2 (div_rn): PK = true
+// the packed expansion the samplers ship, false the compiler's two scalar divisions.
+template <bool PK>
+__global__ __launch_bounds__(kBlock) void div_pairs_kernel(const float* __restrict__ a,
+                                                           const float* __restrict__ b,
+                                                           float* __restrict__ q, int64_t pairs) {
+    const int64_t i = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (i >= pairs) return;
+    const f32x2 x = {a[2 * i], a[2 * i + 1]}, y = {b[2 * i], b[2 * i + 1]};
+    const f32x2 r = div_rn<PK>(x, y);
+    q[2 * i] = r.x;
+    q[2 * i + 1] = r.y;
+}
+
 }  // namespace
 
 extern "C" {
+
+/* q = a / b elementwise, n even, in pairs as the RANSAC samplers divide (packed != 0: the
+ * shipped packed expansion; 0: the compiler's scalar divisions) -- the division's own test. */
+int hg_tune_div_pairs(int packed, const float* a, const float* b, float* q, int64_t n,
+                      void* stream) {
+    if (n <= 0 || (n & 1) || !a || !b || !q) return (int)hipErrorInvalidValue;
+    const int64_t pairs = n / 2;
+    const unsigned g = (unsigned)((pairs + kBlock - 1) / kBlock);
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    if (packed) div_pairs_kernel<true><<<g, kBlock, 0, st>>>(a, b, q, pairs);
+    else div_pairs_kernel<false><<<g, kBlock, 0, st>>>(a, b, q, pairs);
+    return (int)hipGetLastError();
+}
 
 int hg_tune_num_soa_variants(void) { return (int)(sizeof(kSoaVariants) / sizeof(kSoaVariants[0])); }
 

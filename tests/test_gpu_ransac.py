@@ -82,6 +82,63 @@ def _tune_sample(pkg):
     return f
 
 
+def _div_special_operands():
+    """Division operands where the expansion's scaling and fix-up steps matter: signed zeros,
+    subnormals (smallest, largest, in between), the normal range's ends, powers of two,
+    mantissas of all ones, +-Inf and NaNs -- every pairing of them, both orders."""
+    f = np.float32
+    tiny, big = np.finfo(f).tiny, np.finfo(f).max
+    vals = [0.0, -0.0, 1.0, -1.0, 3.0, 0.1, tiny, -tiny, big, -big, big / 2, tiny * 2,
+            np.nextafter(f(1), f(2)), np.nextafter(f(1), f(0)), np.nextafter(f(2), f(0)),
+            float(2.0 ** 64), float(2.0 ** -64), float(2.0 ** 126), float(2.0 ** -126),
+            np.inf, -np.inf, np.nan]
+    bits = [0x00000001, 0x80000001, 0x007FFFFF, 0x00400000, 0x00000100, 0x7FC00001, 0xFFC00000,
+            0x7F7FFFFF, 0x3FFFFFFF, 0x4B7FFFFF, 0x1FFFFFFF, 0x5F7FFFFF]
+    v = np.concatenate([np.array(vals, f), np.array(bits, np.uint32).view(f)])
+    a, b = np.meshgrid(v, v)
+    return a.ravel(), b.ravel()
+
+
+def test_packed_division_is_ieee(pkg, dev):
+    """div_rn's packed expansion (the samplers' divisions, hg_solvers.hpp) is binary32 IEEE
+    division: on 4 M random bit patterns plus every pairing of the special operands it equals
+    numpy's float32 a / b (correctly rounded) bit for bit -- NaN for NaN -- and equals the
+    compiler's own scalar divisions to the last bit, NaN payloads and signs included."""
+    import ctypes
+    f = pkg._lib.tune().hg_tune_div_pairs
+    f.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                  ctypes.c_void_p]
+    f.restype = ctypes.c_int
+    rng = np.random.default_rng(20261016)
+    sa, sb = _div_special_operands()
+    n_rand = 1 << 22
+    a = np.concatenate([rng.integers(0, 2 ** 32, n_rand, dtype=np.uint64).astype(np.uint32).view(np.float32), sa])
+    b = np.concatenate([rng.integers(0, 2 ** 32, n_rand, dtype=np.uint64).astype(np.uint32).view(np.float32), sb])
+    # quotients in every binade: b within a few binades of a, so few over/underflow to Inf/0
+    near = rng.integers(0, 2 ** 32, 1 << 20, dtype=np.uint64).astype(np.uint32)
+    shift = rng.integers(-(24 << 23), 24 << 23, 1 << 20).astype(np.int64)
+    b_near = np.clip(near.astype(np.int64) % (1 << 31) + shift, 0, 0x7F7FFFFF).astype(np.uint32)
+    b_near |= near & 0x80000000
+    a = np.concatenate([a, near.view(np.float32)])
+    b = np.concatenate([b, b_near.view(np.float32)])
+    if a.size % 2:
+        a, b = a[:-1], b[:-1]
+    da, db = torch.from_numpy(a).to(dev), torch.from_numpy(b).to(dev)
+    out = {}
+    for packed in (1, 0):
+        q = torch.empty_like(da)
+        assert f(packed, da.data_ptr(), db.data_ptr(), q.data_ptr(), a.size,
+                 torch.cuda.current_stream(dev).cuda_stream) == 0
+        out[packed] = q.cpu().numpy()
+    np.testing.assert_array_equal(out[1].view(np.uint32), out[0].view(np.uint32))
+    with np.errstate(all="ignore"):
+        want = a / b
+    nan = np.isnan(want)
+    assert (np.isnan(out[1]) == nan).all()
+    bad = np.flatnonzero(out[1][~nan].view(np.uint32) != want[~nan].view(np.uint32))
+    assert bad.size == 0, [(a[~nan][i], b[~nan][i]) for i in bad[:5]]
+
+
 @pytest.mark.parametrize("npool", [1, 2, 3, 4, 7, 8, 1024, 1025, 2540, 3900, 20_000])
 @pytest.mark.parametrize("variant", [0, 1, 2])
 def test_sample_solve_variants_vs_oracle(orc, oracle, pkg, dev, npool, variant):
