@@ -666,6 +666,11 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 16: return launch_sample_seeded<2, 4, kDrawsCheap, 0, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 17: return launch_sample_seeded<2, 4, kDrawsCheap, 3, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 18: return launch_sample_seeded<2, 8, kDrawsPaired, 2, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // the 8-wave shape (SKS's shipped one) ablated the same way: 19 no remainder, 20 no
+        // hash, 21 neither (wrong bits, time only)
+        case 19: return launch_sample_seeded<2, 8, kDrawsPaired, 3, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 20: return launch_sample_seeded<2, 8, kDrawsCheap, 0, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 21: return launch_sample_seeded<2, 8, kDrawsCheap, 3, 0, kPairPacked>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 1: return launch_sample_seeded<2, 4, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 2: return launch_sample_seeded<1, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 3: return launch_sample_seeded<2, 16, kDrawsPaired, false, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);

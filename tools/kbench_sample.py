@@ -40,10 +40,13 @@ SEEDED = {0: "seeded shipped (packed pairs; 8 waves, ACA from 4 M 4)", 1: "seede
           15: "ablation: P2 pairs, 4 waves, no remainder (wrong bits)",
           16: "ablation: P2 pairs, 4 waves, no hash (wrong bits)",
           17: "ablation: P2 pairs, 4 waves, no hash, no remainder (wrong bits)",
-          18: "seeded P2 pairs, 8 waves, binary64 remainder"}
+          18: "seeded P2 pairs, 8 waves, binary64 remainder",
+          19: "ablation: P2 pairs, 8 waves, no remainder (wrong bits)",
+          20: "ablation: P2 pairs, 8 waves, no hash (wrong bits)",
+          21: "ablation: P2 pairs, 8 waves, no hash, no remainder (wrong bits)"}
 # KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
 SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
-OTHER_STREAM = (5, 6, 15, 16, 17)  # other streams / ablations: not comparable bit for bit
+OTHER_STREAM = (5, 6, 15, 16, 17, 19, 20, 21)  # other streams / ablations: not comparable bit for bit
 ALGO = int(os.environ.get("KB_ALGO", "0"))  # 0 ACA, 1 SKS (normalised)
 if os.environ.get("KB_SEEDED_VARIANTS"):  # e.g. "0,7,10,11,12"
     SEEDED = {int(v): SEEDED[int(v)] for v in os.environ["KB_SEEDED_VARIANTS"].split(",")}
