@@ -266,8 +266,10 @@ inline uint64_t reduce_magic(uint32_t d) {
 // packed f32x2 values, so each v_pk_mul_f32 / v_pk_add_f32 does the same IEEE operation
 // for both (the values of two scalar solves; only a NaN's sign may differ, since a packed
 // subtraction is an add with a negate modifier); the divisions stay scalar per half.
+// STP (tune only): the H stores' cache policy -- 0 non-temporal (shipped), 1 default,
+// 2 sc1 buffer stores, 3 sc1|nt buffer stores.
 template <int ALGO, bool NORM, int P, int PF = 1, int WPB = kWavesPerBlock,
-          int DRAWS = kDrawsIndexed, int RED = 0, int PAIR = 0>
+          int DRAWS = kDrawsIndexed, int RED = 0, int PAIR = 0, int STP = 0>
 __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
     const float2* __restrict__ pool_src, const float2* __restrict__ pool_tar, uint32_t npool,
     uint64_t magic, const uint4* __restrict__ idx, float* __restrict__ H, int64_t n,
@@ -343,7 +345,8 @@ __global__ __launch_bounds__(WPB * kWave) void sample_solve_lds_kernel(
         }
         const int64_t base = t * kTile;
         if (base + kTile <= n) {
-            store_rows9_staged<float, P, true>(reinterpret_cast<char*>(H + base * 9), h, stage, lane);
+            store_rows9_staged<float, P, STP == 0 || STP == 3, STP >= 2>(
+                reinterpret_cast<char*>(H + base * 9), h, stage, lane);
         } else {
 #pragma unroll
             for (int j = 0; j < P; ++j) {
@@ -664,7 +667,7 @@ inline int launch_sample_solve(int variant, const float2* ps, const float2* pt, 
 // shipped shapes are launch_sample_seeded_shipped's; every parameter is open for the
 // variant sweep (hg_tune_sample_seeded).
 template <int P = 1, int WPB = 16, int DRAWS = kDrawsPaired, int RED = 0, int PF = 0,
-          int PAIR = 0>
+          int PAIR = 0, int STP = 0>
 inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npool,
                                 uint64_t seed, uint64_t offset, float* H, int64_t n, int algo,
                                 bool norm, hipStream_t s) {
@@ -694,7 +697,7 @@ inline int launch_sample_seeded(const float2* ps, const float2* pt, uint32_t npo
     const uint64_t magic = reduce_magic<RED>(npool);
 #define HG_SD(A, N)                                                                         \
     do {                                                                                    \
-        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, RED, PAIR>;               \
+        auto k = sample_solve_lds_kernel<A, N, P, PF, WPB, DRAWS, RED, PAIR, STP>;          \
         if (lds > kSampleLdsMax && !lds_opt_in(k)) return (int)hipErrorInvalidValue;        \
         rc = launch(k, g, WPB * kWave, lds, s, ps, pt, npool, magic, nullptr, H, n, bits_base, \
                     odd);                                                                   \

@@ -685,6 +685,14 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 10: return launch_sample_seeded<2, 8, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 11: return launch_sample_seeded<2, 16, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 12: return launch_sample_seeded<2, 4, kDrawsPaired, false, 0, kPairScalarDiv>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // the shipped shapes with other H store policies (STP): 22-24 the 4-wave shape with
+        // default, sc1, sc1|nt stores; 25-27 the 8-wave shape the same way
+        case 22: return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, kPairPacked, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 23: return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, kPairPacked, 2>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 24: return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 25: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 26: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 2>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 27: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }
