@@ -632,6 +632,47 @@ def reference_layout(d: Dist, pkg):
     return out
 
 
+def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
+    """The reference harness's sampling flow in its own formats (GPU_Runtime Test.cu:
+    1441-1451) on its own point file, N = 1M: MRG32K3A words (rocRAND, seed 11), then
+    get_rand_list + cal_Homo_ACA/SKS -- unfused (gather to (8,N) rows, then the SoA solver)
+    and fused (hg_gather_solve_f64: 16 B of words in, 72 B of H out per hypothesis).
+    Table 8 times cal_Homo_* alone (245 / 436 us at 1M)."""
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"]).to(d.dev).double()  # Point2f -> Point2d (.cu:1414-1416)
+    pt = torch.from_numpy(g["pool_tar"]).to(d.dev).double()
+    f_draw = lambda: pkg.rand_mrg32k3a(4 * n, SEED, d.dev)  # noqa: E731
+    rl = f_draw().view(4, n)
+    for _ in range(3):
+        f_draw()
+    _, ms_draw = timed_region(d, f_draw, 20)
+    out = {"n": n, "pool": int(ps.shape[0]), "draws_us": round(ms_draw * 1e3, 2)}
+    for algo in ("aca", "sks"):
+        H = torch.empty((9, n), dtype=torch.float64, device=d.dev)
+        f_fused = lambda: pkg.gather_solve(ps, pt, rl, algo)  # noqa: E731
+
+        def f_split():
+            s_, t_ = pkg.get_rand_list(rl, ps, pt)
+            pkg.solve(algo, s_, t_, normalize=False, layout="soa", out=H)
+
+        for _ in range(10):
+            f_fused()
+            f_split()
+        _, ms_fused = timed_region(d, f_fused, 200)
+        _, ms_split = timed_region(d, f_split, 200)
+        f_split()
+        same = bool(torch.equal(f_fused().view(torch.int64), H.view(torch.int64)))
+        out[algo] = {"fused_us": round(ms_fused * 1e3, 2),
+                     "fused_gbps": round(n * 88 / (ms_fused * 1e-3) / 1e9, 1),
+                     "fused_frac": round(n * 88 / (ms_fused * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                     "gather_then_solve_us": round(ms_split * 1e3, 2),
+                     "table8_solver_us": TABLE8_US[algo],
+                     "fused_speedup_vs_table8_solver": round(TABLE8_US[algo] / (ms_fused * 1e3), 2),
+                     "fused_bit_identical_to_unfused": same}
+        del H
+    return out
+
+
 def host_boundary_section(d: Dist, pkg, n: int):
     """What the host-buffer side of the boundary costs (reported, never `value`):
     (1) the reference's single-problem C++ call sks::runKernel_ACA on host pointers
@@ -1179,6 +1220,7 @@ def main():
             del bs_h, bt_h, Hb
             line["reference_layout"] = reference_layout(d, pkg)
             line["table8_sweep"] = table8_sweep(d, pkg)
+            line["table8_pipeline"] = table8_pipeline_section(d, pkg)
             line["grouped_small"] = grouped_section(d, pkg)
             line["ransac"] = ransac_section(d, pkg)
             line["host_boundary"] = host_boundary_section(d, pkg, n)

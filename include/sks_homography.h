@@ -161,6 +161,33 @@ int hg_sample_solve_seeded_f32(const float* pool_src, const float* pool_tar, uin
 int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const float* pool_tar,
                         uint32_t npool, float thresh, uint32_t* counts, void* stream);
 
+/* ---- The reference's Table-8 sampling pipeline in its own formats (hg_table8.hip) ----
+ * GPU_Runtime Test.cu:1441-1451: 4*n MRG32K3A words, get_rand_list, cal_ACA/cal_SKS.
+ * rand_list is (4,n) uint32 -- word k of hypothesis id at rand_list[id + k*n], as
+ * get_rand_list reads it (.cu:56-59) -- and each word selects pool[word % size] (modulo
+ * bias and duplicates kept).  Pools are (size,2) binary64 {x, y} pairs (Point2d),
+ * 16-B aligned. */
+
+/* curandCreateGenerator(CURAND_RNG_PSEUDO_MRG32K3A) + curandSetPseudoRandomGeneratorSeed
+ * + curandGenerate (.cu:1441-1444) through rocRAND's MRG32K3A (default ordering): `count`
+ * 32-bit words into `out`.  The one entry point that allocates (rocRAND's generator
+ * state, created and destroyed per call) and so is not graph-capturable.  Equality with
+ * cuRAND's stream is not checked here (no cuRAND in this image). */
+int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream);
+
+/* get_rand_list (.cu:52-78) itself: d_src / d_tar (8,n) binary64 rows, row 2k / 2k+1 =
+ * x / y of the k-th selected point. */
+int hg_get_rand_list_f64(const uint32_t* rand_list, uint32_t size, const double* pool_src,
+                         const double* pool_tar, double* d_src, double* d_tar, int64_t n,
+                         void* stream);
+
+/* get_rand_list fused with cal_Homo_{ACA,SKS,GE,GPT} (.cu:52-78 + :81-507): H (9,n)
+ * binary64 SoA, the bits of hg_get_rand_list_f64 followed by hg_<algo>_f64(...,
+ * HG_LAYOUT_SOA, flags) without the (8,n) rows ever reaching memory.  algo: HG_ALGO_*;
+ * flags 0 (the reference kernels' unnormalised H) or HG_FLAG_NORMALIZE. */
+int hg_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar, uint32_t size,
+                        const uint32_t* rand_list, double* H, int64_t n, int flags, void* stream);
+
 /* ONE problem, latency path: src[8] and tar[8] are read on the HOST and passed in the
  * kernel launch itself (no copy); H[9] is written by the device -- pass device memory,
  * or host memory mapped into the device address space (hipHostMalloc(...,

@@ -24,7 +24,7 @@ TORCH_LIB = os.path.join(LIB_DIR, "libsks_homography_torch.so")
 TUNE_LIB = os.path.join(LIB_DIR, "libsks_homography_tune.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
-SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_sks_api.cpp", "hg_host.cpp"]
+SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_table8.hip", "hg_sks_api.cpp", "hg_host.cpp"]
 # kernel-variant sweeps and timing loops (tools/, tests): a separate library so the product
 # library carries only the shipped kernels
 TUNE_SOURCES = ["hg_tune.hip"]
@@ -76,7 +76,9 @@ def build(verbose: bool = False, force: bool = False) -> str:
         for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
             f.result()
     if force or _stale(LIB, objs):
-        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
+        # rocRAND: the reference's MRG32K3A draws (hg_rand_mrg32k3a_u32, hg_table8.hip)
+        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
+               "-L/opt/rocm/lib", "-lrocrand", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -1,0 +1,81 @@
+// hg_gather.hpp -- the reference's own sampling pipeline in its own data formats
+// (GPU_Runtime Test.cu:1441-1451): 4*N cuRAND MRG32K3A words laid out as FOUR ROWS of N
+// (word k of hypothesis id at randList[id + k*N]), get_rand_list (:52-78) gathering
+// Point2d (two binary64) source / target points into (8,N) SoA binary64 rows, then
+// cal_Homo_* (:81-507) over them, unnormalised.  Round 1's sampler (hg_ransac.hpp) is the
+// binary32 AoS form of the same pipeline; these kernels keep the reference's formats so
+// Table 8's flow runs unchanged, with the gather and the solve fused into one pass.
+#pragma once
+#include "hg_ransac.hpp"
+
+namespace hg {
+
+// One lane per hypothesis.  rand_list (4,n) uint32, pool_src / pool_tar (size,2) binary64
+// (Point2d), d_src / d_tar (8,n): get_rand_list's own statement order (x, y of r1..r4).
+// Exact r % size through fastmod_u32.
+__global__ __launch_bounds__(kBlock) void get_rand_list_kernel(
+    const uint32_t* __restrict__ rand_list, uint32_t size, uint64_t magic,
+    const double2* __restrict__ pool_src, const double2* __restrict__ pool_tar,
+    double* __restrict__ d_src, double* __restrict__ d_tar, int64_t n) {
+    const int64_t id = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    if (id >= n) return;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t r = fastmod_u32(rand_list[id + k * n], magic, size);
+        const double2 s = pool_src[r], t = pool_tar[r];
+        __builtin_nontemporal_store(s.x, d_src + id + (2 * k) * n);
+        __builtin_nontemporal_store(s.y, d_src + id + (2 * k + 1) * n);
+        __builtin_nontemporal_store(t.x, d_tar + id + (2 * k) * n);
+        __builtin_nontemporal_store(t.y, d_tar + id + (2 * k + 1) * n);
+    }
+}
+
+// Fused get_rand_list + cal_Homo_*: each lane reads its 4 words (4 coalesced rows),
+// gathers its 4 correspondences and solves in registers; the (8,n) intermediate rows
+// never reach HBM, so a hypothesis moves 16 B in and 72 B out instead of 16 + 2*128 + 2*128
+// + 72.  POOL_LDS: the block first copies the pool into LDS as 32-B {sx, sy, tx, ty}
+// records and gathers from there (persistent grid, one pool copy per block); otherwise
+// the gathers go to the pool in global memory (L2-resident for the reference's sizes).
+// 1024-lane blocks (16 waves share one pool copy); GPT-LU's binary64 elimination needs more
+// than the 128 VGPRs that allows, so it runs 512-lane blocks.
+template <int ALGO>
+constexpr int gather_block() { return ALGO == kGPT ? 512 : 1024; }
+
+template <int ALGO, bool NORM, bool POOL_LDS>
+__global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
+    const uint32_t* __restrict__ rand_list, uint32_t size, uint64_t magic,
+    const double2* __restrict__ pool_src, const double2* __restrict__ pool_tar,
+    double* __restrict__ H, int64_t n) {
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    double2* pool = reinterpret_cast<double2*>(dyn);  // [2 i] = src i, [2 i + 1] = tar i
+    if constexpr (POOL_LDS) {
+        for (uint32_t i = threadIdx.x; i < size; i += blockDim.x) {
+            pool[2 * i] = pool_src[i];
+            pool[2 * i + 1] = pool_tar[i];
+        }
+        __syncthreads();
+    }
+    const int64_t stride = POOL_LDS ? (int64_t)gridDim.x * blockDim.x : n;
+    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < n; id += stride) {
+        double s[8], t[8], h[9];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const uint32_t r = fastmod_u32(__builtin_nontemporal_load(rand_list + id + k * n), magic, size);
+            double2 a, b;
+            if constexpr (POOL_LDS) {
+                a = pool[2 * r];
+                b = pool[2 * r + 1];
+            } else {
+                a = pool_src[r];
+                b = pool_tar[r];
+            }
+            s[2 * k] = a.x; s[2 * k + 1] = a.y;
+            t[2 * k] = b.x; t[2 * k + 1] = b.y;
+        }
+        solve<ALGO, NORM>(s, t, h);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) __builtin_nontemporal_store(h[k], H + id + k * n);
+    }
+}
+
+}  // namespace hg

@@ -1,0 +1,106 @@
+// hg_table8.hip -- the reference's Table-8 sampling pipeline in its own formats
+// (GPU_Runtime Test.cu:1441-1451): MRG32K3A draws, get_rand_list (:52-78) and
+// cal_Homo_* (:81-507), the last two also fused into one pass.  Kernels: hg_gather.hpp.
+//
+//   hg_rand_mrg32k3a_u32   curandCreateGenerator(MRG32K3A) + SetPseudoRandomGeneratorSeed
+//                          + curandGenerate (.cu:1441-1444), through rocRAND
+//   hg_get_rand_list_f64   get_rand_list itself: (4,n) words -> (8,n) src / tar rows
+//   hg_gather_solve_f64    get_rand_list fused with cal_Homo_{ACA,SKS,GE,GPT}: (9,n) H
+#include <rocrand/rocrand.h>
+
+#include "hg_gather.hpp"
+
+namespace {
+
+constexpr int kInvalid = (int)hipErrorInvalidValue;
+constexpr size_t kPoolLdsMax = 160 * 1024;  // gfx950: the whole LDS of a CU for one block
+
+bool misaligned(const void* p, uintptr_t a) { return (reinterpret_cast<uintptr_t>(p) & (a - 1)) != 0; }
+
+template <int ALGO, bool NORM>
+int launch_gather_solve(const uint32_t* rl, uint32_t size, const double2* ps, const double2* pt,
+                        double* H, int64_t n, hipStream_t s) {
+    constexpr int kGatherBlock = hg::gather_block<ALGO>();
+    const uint64_t magic = hg::fastmod_magic(size);
+    const size_t lds = (size_t)size * 32;
+    const int64_t blocks = (n + kGatherBlock - 1) / kGatherBlock;
+    if (lds <= kPoolLdsMax) {
+        // persistent: as many blocks as are resident at once, each with one pool copy
+        auto k = hg::gather_solve_f64_kernel<ALGO, NORM, true>;
+        if (lds > hg::kSampleLdsMax && !hg::lds_opt_in(k)) return kInvalid;
+        int64_t per_cu = (int64_t)kPoolLdsMax / (int64_t)(lds ? lds : 1);
+        const int64_t max_per_cu = 2048 / kGatherBlock;  // 32 waves per CU
+        per_cu = per_cu < 1 ? 1 : (per_cu > max_per_cu ? max_per_cu : per_cu);
+        const int64_t cap = per_cu * hg::cu_count();
+        const unsigned g = (unsigned)(blocks < cap ? blocks : cap);
+        return hg::launch(k, g, kGatherBlock, lds, s, rl, size, magic, ps, pt, H, n);
+    }
+    if (blocks > 0x7fffffffLL) return kInvalid;
+    return hg::launch(hg::gather_solve_f64_kernel<ALGO, NORM, false>, (unsigned)blocks,
+                      kGatherBlock, 0, s, rl, size, magic, ps, pt, H, n);
+}
+
+}  // namespace
+
+extern "C" {
+
+int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream) {
+    if (count < 0) return kInvalid;
+    if (count == 0) return 0;
+    if (!out || misaligned(out, 4)) return kInvalid;
+    rocrand_generator g = nullptr;
+    if (rocrand_create_generator(&g, ROCRAND_RNG_PSEUDO_MRG32K3A) != ROCRAND_STATUS_SUCCESS)
+        return (int)hipErrorNotInitialized;
+    rocrand_status st = rocrand_set_stream(g, reinterpret_cast<hipStream_t>(stream));
+    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_seed(g, seed);
+    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_generate(g, out, (size_t)count);
+    const rocrand_status dst = rocrand_destroy_generator(g);
+    if (st != ROCRAND_STATUS_SUCCESS || dst != ROCRAND_STATUS_SUCCESS)
+        return (int)hipErrorLaunchFailure;
+    return 0;
+}
+
+int hg_get_rand_list_f64(const uint32_t* rand_list, uint32_t size, const double* pool_src,
+                         const double* pool_tar, double* d_src, double* d_tar, int64_t n,
+                         void* stream) {
+    if (n < 0 || size == 0) return kInvalid;
+    if (n == 0) return 0;
+    if (!rand_list || !pool_src || !pool_tar || !d_src || !d_tar) return kInvalid;
+    if (misaligned(rand_list, 4) || misaligned(pool_src, 16) || misaligned(pool_tar, 16) ||
+        misaligned(d_src, 8) || misaligned(d_tar, 8))
+        return kInvalid;
+    const int64_t blocks = (n + hg::kBlock - 1) / hg::kBlock;
+    if (blocks > 0x7fffffffLL) return kInvalid;
+    return hg::launch(hg::get_rand_list_kernel, (unsigned)blocks, hg::kBlock, 0,
+                      reinterpret_cast<hipStream_t>(stream), rand_list, size,
+                      hg::fastmod_magic(size), reinterpret_cast<const double2*>(pool_src),
+                      reinterpret_cast<const double2*>(pool_tar), d_src, d_tar, n);
+}
+
+int hg_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar, uint32_t size,
+                        const uint32_t* rand_list, double* H, int64_t n, int flags, void* stream) {
+    if (n < 0 || size == 0 || algo < HG_ALGO_ACA || algo > HG_ALGO_GPT ||
+        (flags & ~HG_FLAG_NORMALIZE))
+        return kInvalid;
+    if (n == 0) return 0;
+    if (!rand_list || !pool_src || !pool_tar || !H) return kInvalid;
+    if (misaligned(rand_list, 4) || misaligned(pool_src, 16) || misaligned(pool_tar, 16) ||
+        misaligned(H, 8))
+        return kInvalid;
+    const auto* ps = reinterpret_cast<const double2*>(pool_src);
+    const auto* pt = reinterpret_cast<const double2*>(pool_tar);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
+#define HG_GS(A)                                                                         \
+    return norm ? launch_gather_solve<A, true>(rand_list, size, ps, pt, H, n, s)         \
+                : launch_gather_solve<A, false>(rand_list, size, ps, pt, H, n, s)
+    switch (algo) {
+        case HG_ALGO_ACA: HG_GS(hg::kACA);
+        case HG_ALGO_SKS: HG_GS(hg::kSKS);
+        case HG_ALGO_GE: HG_GS(hg::kGE);
+        default: HG_GS(hg::kGPT);
+    }
+#undef HG_GS
+}
+
+}  // extern "C"

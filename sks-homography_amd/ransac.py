@@ -109,6 +109,71 @@ def score(H: torch.Tensor, pool_src: torch.Tensor, pool_tar: torch.Tensor,
     return counts
 
 
+# ---- the reference's Table-8 pipeline in its own formats (GPU_Runtime Test.cu:1441-1451) ----
+_ALGO_IDS = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
+
+
+def rand_mrg32k3a(count: int, seed: int = 11, device="cuda") -> torch.Tensor:
+    """``count`` MRG32K3A words (rocRAND), as curandGenerate fills the reference's index list
+    (.cu:1441-1444, seed 11); uint32 values in an int32 tensor."""
+    if count < 0:
+        raise ValueError(f"count must be >= 0, got {count}")
+    dev = _gpu_device(device)
+    out = torch.empty(count, dtype=torch.int32, device=dev)
+    with _guard(dev):
+        _lib.call("hg_rand_mrg32k3a_u32", out.data_ptr(), count, seed, _stream(dev))
+    return out
+
+
+def _point_pool(pool: torch.Tensor) -> torch.Tensor:
+    if pool.dim() != 2 or pool.shape[1] != 2 or pool.dtype != torch.float64:
+        raise ValueError(f"pool must be an (npool,2) float64 tensor (Point2d), got "
+                         f"{tuple(pool.shape)} {pool.dtype}")
+    return pool.contiguous()
+
+
+def _rand_list(rl: torch.Tensor) -> torch.Tensor:
+    if rl.dim() != 2 or rl.shape[0] != 4 or rl.dtype not in (torch.int32, torch.uint32):
+        raise ValueError("rand_list must be a (4,n) int32/uint32 tensor (word k of hypothesis "
+                         "id at [k, id], as get_rand_list reads it)")
+    return rl.contiguous()
+
+
+def get_rand_list(rand_list: torch.Tensor, pool_src: torch.Tensor, pool_tar: torch.Tensor):
+    """The reference's get_rand_list (.cu:52-78): (4,n) words and two (npool,2) float64
+    point pools -> (d_src, d_tar), each (8,n) float64 SoA, ready for solve(..., layout="soa")."""
+    dev = _require_device(rand_list, pool_src, pool_tar)
+    rl, ps, pt = _rand_list(rand_list), _point_pool(pool_src), _point_pool(pool_tar)
+    if ps.shape[0] != pt.shape[0] or ps.shape[0] == 0:
+        raise ValueError("pool_src and pool_tar must hold the same, non-zero number of points")
+    n = rl.shape[1]
+    d_src = torch.empty((8, n), dtype=torch.float64, device=dev)
+    d_tar = torch.empty((8, n), dtype=torch.float64, device=dev)
+    with _guard(dev):
+        _lib.call("hg_get_rand_list_f64", rl.data_ptr(), ps.shape[0], ps.data_ptr(), pt.data_ptr(),
+                  d_src.data_ptr(), d_tar.data_ptr(), n, _stream(dev))
+    return d_src, d_tar
+
+
+def gather_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, rand_list: torch.Tensor,
+                 algo: str = "aca", normalize: bool = False) -> torch.Tensor:
+    """get_rand_list fused with cal_Homo_{ACA,SKS,GE,GPT} (.cu:52-78 + :81-507): (9,n)
+    float64 SoA H, bit for bit ``solve(algo, *get_rand_list(...), normalize, layout="soa")``
+    without the (8,n) rows in memory.  Unnormalised by default, like the reference kernels."""
+    dev = _require_device(rand_list, pool_src, pool_tar)
+    if algo not in _ALGO_IDS:
+        raise ValueError(f"algo must be one of {sorted(_ALGO_IDS)}, got {algo!r}")
+    rl, ps, pt = _rand_list(rand_list), _point_pool(pool_src), _point_pool(pool_tar)
+    if ps.shape[0] != pt.shape[0] or ps.shape[0] == 0:
+        raise ValueError("pool_src and pool_tar must hold the same, non-zero number of points")
+    n = rl.shape[1]
+    H = torch.empty((9, n), dtype=torch.float64, device=dev)
+    with _guard(dev):
+        _lib.call("hg_gather_solve_f64", _ALGO_IDS[algo], ps.data_ptr(), pt.data_ptr(), ps.shape[0],
+                  rl.data_ptr(), H.data_ptr(), n, 1 if normalize else 0, _stream(dev))
+    return H
+
+
 class RansacResult(NamedTuple):
     H: torch.Tensor          # (9,) best hypothesis (normalised)
     inliers: int             # its inlier count

@@ -111,6 +111,21 @@ def test_other_entry_validation(pkg):
     assert lib.hg_tensor_aca_offsets_f32(None, None, None, 0, 1.0, 1.0, None) == 0
     assert lib.hg_tensor_aca_offsets_backward_f32(None, None, None, 3, 1.0, 1.0, None, None,
                                                   None) == 1
+    # the Table-8 pipeline entry points (hg_table8.hip)
+    assert lib.hg_rand_mrg32k3a_u32(None, -1, 11, None) == 1
+    assert lib.hg_rand_mrg32k3a_u32(None, 0, 11, None) == 0
+    assert lib.hg_rand_mrg32k3a_u32(None, 4, 11, None) == 1                       # NULL
+    assert lib.hg_rand_mrg32k3a_u32(2, 4, 11, None) == 1                          # unaligned
+    assert lib.hg_get_rand_list_f64(None, 0, None, None, None, None, 4, None) == 1  # size 0
+    assert lib.hg_get_rand_list_f64(None, 5, None, None, None, None, -1, None) == 1
+    assert lib.hg_get_rand_list_f64(None, 5, None, None, None, None, 0, None) == 0
+    assert lib.hg_get_rand_list_f64(None, 5, None, None, None, None, 4, None) == 1
+    assert lib.hg_get_rand_list_f64(16, 5, 8, 16, 16, 16, 4, None) == 1            # pool not 16-B
+    for algo, flags, n, want in ((4, 0, 4, 1), (-1, 0, 4, 1), (0, 2, 4, 1), (0, 0, -1, 1),
+                                 (3, 1, 0, 0), (0, 0, 4, 1)):
+        assert lib.hg_gather_solve_f64(algo, None, None, 5, None, None, n, flags, None) == want
+    assert lib.hg_gather_solve_f64(0, None, None, 0, None, None, 4, 0, None) == 1  # size 0
+    assert lib.hg_gather_solve_f64(0, 16, 16, 5, 16, 4, 4, 0, None) == 1           # H unaligned
     assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
                                                None) == 1
     assert lib.hg_solve_one_f32(0, None, None, None, 1, None) == 1               # NULL points
