@@ -670,6 +670,17 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
                      "fused_speedup_vs_table8_solver": round(TABLE8_US[algo] / (ms_fused * 1e3), 2),
                      "fused_bit_identical_to_unfused": same}
         del H
+    # the fused kernel's HBM figure at the headline's batch size (88 B per hypothesis)
+    big = 10 * n
+    rl_b = pkg.rand_mrg32k3a(4 * big, SEED, d.dev).view(4, big)
+    f_big = lambda: pkg.gather_solve(ps, pt, rl_b, "aca")  # noqa: E731
+    for _ in range(5):
+        f_big()
+    _, ms_big = timed_region(d, f_big, 50)
+    out["aca_large"] = {"n": big, "fused_us": round(ms_big * 1e3, 2),
+                        "fused_gbps": round(big * 88 / (ms_big * 1e-3) / 1e9, 1),
+                        "fused_frac": round(big * 88 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
+    del rl_b
     return out
 
 

@@ -94,6 +94,13 @@ int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
                   const float* pool_tar, uint32_t npool, float thresh, uint32_t* counts,
                   void* stream);
 
+/* The fused get_rand_list + cal_Homo_ACA/SKS kernel (hg_gather.hpp) in other shapes: 0 pool
+ * in LDS, 1024-lane persistent blocks (shipped up to 5120 pairs); 1 global gather; 2 / 3 pool
+ * in LDS with 512 / 256-lane blocks.  algo 0 ACA, 1 SKS; unnormalised (9,n) H. */
+int hg_tune_gather_solve_f64(int variant, int algo, const double* pool_src, const double* pool_tar,
+                             uint32_t size, const uint32_t* rand_list, double* H, int64_t n,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -41,11 +41,14 @@ __global__ __launch_bounds__(kBlock) void get_rand_list_kernel(
 template <int ALGO>
 constexpr int gather_block() { return ALGO == kGPT ? 512 : 1024; }
 
-template <int ALGO, bool NORM, bool POOL_LDS>
+// V = 2 (tune): a lane owns two consecutive hypotheses, so its word reads are 8 B and its H
+// stores 16 B per row (needs n even and 16-B aligned H).
+template <int ALGO, bool NORM, bool POOL_LDS, int V = 1>
 __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
     const uint32_t* __restrict__ rand_list, uint32_t size, uint64_t magic,
     const double2* __restrict__ pool_src, const double2* __restrict__ pool_tar,
     double* __restrict__ H, int64_t n) {
+    static_assert(V == 1 || V == 2, "one or two hypotheses per lane");
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     double2* pool = reinterpret_cast<double2*>(dyn);  // [2 i] = src i, [2 i + 1] = tar i
     if constexpr (POOL_LDS) {
@@ -55,26 +58,53 @@ __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
         }
         __syncthreads();
     }
-    const int64_t stride = POOL_LDS ? (int64_t)gridDim.x * blockDim.x : n;
-    for (int64_t id = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; id < n; id += stride) {
-        double s[8], t[8], h[9];
+    auto gather = [&](uint32_t word, double2& a, double2& b) {
+        const uint32_t r = fastmod_u32(word, magic, size);
+        if constexpr (POOL_LDS) {
+            a = pool[2 * r];
+            b = pool[2 * r + 1];
+        } else {
+            a = pool_src[r];
+            b = pool_tar[r];
+        }
+    };
+    const int64_t m = n / V;  // lanes' units
+    const int64_t stride = POOL_LDS ? (int64_t)gridDim.x * blockDim.x : m;
+    for (int64_t u = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; u < m; u += stride) {
+        const int64_t id = u * V;
+        double s[V][8], t[V][8], h[V][9];
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const uint32_t r = fastmod_u32(__builtin_nontemporal_load(rand_list + id + k * n), magic, size);
-            double2 a, b;
-            if constexpr (POOL_LDS) {
-                a = pool[2 * r];
-                b = pool[2 * r + 1];
+            uint32_t w[V];
+            if constexpr (V == 1) {
+                w[0] = __builtin_nontemporal_load(rand_list + id + k * n);
             } else {
-                a = pool_src[r];
-                b = pool_tar[r];
+                typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+                const u32x2 x = __builtin_nontemporal_load(
+                    reinterpret_cast<const u32x2*>(rand_list + id + k * n));
+                w[0] = x[0];
+                w[1] = x[1];
             }
-            s[2 * k] = a.x; s[2 * k + 1] = a.y;
-            t[2 * k] = b.x; t[2 * k + 1] = b.y;
-        }
-        solve<ALGO, NORM>(s, t, h);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) __builtin_nontemporal_store(h[k], H + id + k * n);
+            for (int v = 0; v < V; ++v) {
+                double2 a, b;
+                gather(w[v], a, b);
+                s[v][2 * k] = a.x; s[v][2 * k + 1] = a.y;
+                t[v][2 * k] = b.x; t[v][2 * k + 1] = b.y;
+            }
+        }
+#pragma unroll
+        for (int v = 0; v < V; ++v) solve<ALGO, NORM>(s[v], t[v], h[v]);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) {
+            if constexpr (V == 1) {
+                __builtin_nontemporal_store(h[0][k], H + id + k * n);
+            } else {
+                typedef double f64x2 __attribute__((ext_vector_type(2)));
+                const f64x2 o = {h[0][k], h[1][k]};
+                __builtin_nontemporal_store(o, reinterpret_cast<f64x2*>(H + id + k * n));
+            }
+        }
     }
 }
 

@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 
 #include "hg_aos.hpp"
+#include "hg_gather.hpp"
 #include "hg_ransac.hpp"
 #include "hg_rect.hpp"
 #include "hg_soa.hpp"
@@ -695,6 +696,47 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 27: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
+}
+
+// Fused get_rand_list + cal_Homo_ACA/SKS (binary64, hg_gather.hpp) for tools/kbench_gather.py:
+// 0 = pool in LDS (the shipped form for pools up to 5120 pairs; 1024-lane persistent blocks),
+// 1 = the global-gather form, 2 = pool in LDS with 512-lane blocks (two blocks per CU when
+// the pool fits 80 KiB), 3 = pool in LDS, 256-lane blocks, 4 / 5 / 6 = 0 / 2 / 3 with two
+// hypotheses per lane (8-B word reads, 16-B H stores; n even).  Unnormalised.
+int hg_tune_gather_solve_f64(int variant, int algo, const double* pool_src, const double* pool_tar,
+                             uint32_t size, const uint32_t* rand_list, double* H, int64_t n,
+                             void* stream) {
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 6)
+        return (int)hipErrorInvalidValue;
+    const bool pair = variant >= 4;
+    if (pair && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15u) ||
+                 (reinterpret_cast<uintptr_t>(rand_list) & 7u)))
+        return (int)hipErrorInvalidValue;
+    if (pair) variant = variant == 4 ? 0 : variant - 3;
+    const auto* ps = reinterpret_cast<const double2*>(pool_src);
+    const auto* pt = reinterpret_cast<const double2*>(pool_tar);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const uint64_t magic = hg::fastmod_magic(size);
+    const size_t lds = (size_t)size * 32;
+    const int block = variant == 2 ? 512 : (variant == 3 ? 256 : 1024);
+    const int64_t blocks = (n / (pair ? 2 : 1) + block - 1) / block;
+    if (variant == 1) {
+        auto k = algo == 0 ? hg::gather_solve_f64_kernel<hg::kACA, false, false>
+                           : hg::gather_solve_f64_kernel<hg::kSKS, false, false>;
+        return hg::launch(k, (unsigned)blocks, block, 0, s, rand_list, size, magic, ps, pt, H, n);
+    }
+    if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
+    auto k = algo == 0 ? (pair ? hg::gather_solve_f64_kernel<hg::kACA, false, true, 2>
+                               : hg::gather_solve_f64_kernel<hg::kACA, false, true>)
+                       : (pair ? hg::gather_solve_f64_kernel<hg::kSKS, false, true, 2>
+                               : hg::gather_solve_f64_kernel<hg::kSKS, false, true>);
+    if (lds > hg::kSampleLdsMax && !hg::lds_opt_in(k)) return (int)hipErrorInvalidValue;
+    int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
+    const int64_t max_per_cu = 2048 / block;
+    per_cu = per_cu < 1 ? 1 : (per_cu > max_per_cu ? max_per_cu : per_cu);
+    const int64_t cap = per_cu * hg::cu_count();
+    return hg::launch(k, (unsigned)(blocks < cap ? blocks : cap), block, lds, s, rand_list, size,
+                      magic, ps, pt, H, n);
 }
 
 // Scorer variants for tools/kbench_score.py: 0 = one hypothesis per lane (unroll 4),
