@@ -1,10 +1,12 @@
 // runtime_test.cpp -- the reference GPU harness's flow ("C++ Codes/Runtime Test/GPU_Runtime
-// Test/GPU_Runtime Test.cu": read_points, random 4-point draws from the correspondence
-// file, cal_ACA / cal_SKS / cal_GPT / cal_GE timing loops) as a native C++ caller of the
-// MI355X C ABI.  For each batch size N it gathers N random 4-subsets of the file's
-// correspondences into the harness's SoA binary64 layout ((8,N) src / tar, (9,N) H), then
-// times back-to-back launches the way cal_ACA does (one calibration launch, loops sized
-// from it, event-timed mean) and checks ACA against the GE baseline.
+// Test/GPU_Runtime Test.cu": read_points, MRG32K3A draws, get_rand_list, cal_ACA / cal_SKS /
+// cal_GPT / cal_GE timing loops) as a native C++ caller of the MI355X C ABI.  For each batch
+// size N it draws 4*N MRG32K3A words with seed 11 and gathers N random 4-subsets of the
+// file's correspondences on the device into the harness's SoA binary64 layout ((8,N) src /
+// tar, (9,N) H) exactly as .cu:1441-1451 does (hg_rand_mrg32k3a_u32, hg_get_rand_list_f64),
+// then times back-to-back launches the way cal_ACA does (one calibration launch, loops sized
+// from it, event-timed mean), checks ACA against the GE baseline, and checks that the fused
+// gather + solve (hg_gather_solve_f64) returns the same bits as gather-then-cal_Homo_ACA.
 //
 //   runtime_test <points.txt> [max_N] [seconds_per_case]
 //
@@ -19,7 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
-#include <random>
+#include <cstring>
 #include <string>
 #include <vector>
 
@@ -98,26 +100,24 @@ int main(int argc, char** argv) {
     const int64_t npool = (int64_t)p1.size() / 2;
     std::printf("%lld correspondences from %s (%s)\n", (long long)npool, argv[1], hg_version());
 
-    std::mt19937 rng(11);  // the harness draws 4 random indices per hypothesis (.cu:52-78)
-    std::uniform_int_distribution<int64_t> pick(0, npool - 1);
+    // the correspondence pools on the device as Point2d (.cu:1414-1440)
+    double *d_src_in, *d_tar_in;
+    CHECK(hipMalloc(&d_src_in, p1.size() * sizeof(double)));
+    CHECK(hipMalloc(&d_tar_in, p2.size() * sizeof(double)));
+    CHECK(hipMemcpy(d_src_in, p1.data(), p1.size() * sizeof(double), hipMemcpyHostToDevice));
+    CHECK(hipMemcpy(d_tar_in, p2.data(), p2.size() * sizeof(double), hipMemcpyHostToDevice));
     int failures = 0;
     for (int64_t n = 1; n <= max_n; n *= 10) {
-        std::vector<double> hs(8 * n), ht(8 * n);
-        for (int64_t i = 0; i < n; ++i)
-            for (int k = 0; k < 4; ++k) {
-                const int64_t j = pick(rng);
-                hs[(2 * k) * n + i] = p1[2 * j];
-                hs[(2 * k + 1) * n + i] = p1[2 * j + 1];
-                ht[(2 * k) * n + i] = p2[2 * j];
-                ht[(2 * k + 1) * n + i] = p2[2 * j + 1];
-            }
+        // 4*N MRG32K3A words, seed 11, then get_rand_list (.cu:1441-1451)
+        uint32_t* p_d;
         double *ds, *dt, *dh, *dg;
+        CHECK(hipMalloc(&p_d, 4 * n * sizeof(uint32_t)));
         CHECK(hipMalloc(&ds, 8 * n * sizeof(double)));
         CHECK(hipMalloc(&dt, 8 * n * sizeof(double)));
         CHECK(hipMalloc(&dh, 9 * n * sizeof(double)));
         CHECK(hipMalloc(&dg, 9 * n * sizeof(double)));
-        CHECK(hipMemcpy(ds, hs.data(), 8 * n * sizeof(double), hipMemcpyHostToDevice));
-        CHECK(hipMemcpy(dt, ht.data(), 8 * n * sizeof(double), hipMemcpyHostToDevice));
+        CHECK(hg_rand_mrg32k3a_u32(p_d, 4 * n, 11ULL, nullptr));
+        CHECK(hg_get_rand_list_f64(p_d, (uint32_t)npool, d_src_in, d_tar_in, ds, dt, n, nullptr));
         const struct { const char* name; SolveF64 fn; double* out; } cases[] = {
             {"cal_Homo_ACA", hg_aca_f64, dh}, {"cal_Homo_SKS", hg_sks_f64, dg},
             {"cal_Homo_GPT", hg_gpt_f64, dg}, {"cal_Homo_GE ", hg_ge_f64, dg}};
@@ -130,6 +130,18 @@ int main(int argc, char** argv) {
         std::vector<double> ha(9 * n), hg(9 * n);
         CHECK(hipMemcpy(ha.data(), dh, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(hg.data(), dg, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
+        // the fused gather + cal_Homo_ACA: the same bits as gather-then-solve
+        CHECK(hg_gather_solve_f64(HG_ALGO_ACA, d_src_in, d_tar_in, (uint32_t)npool, p_d, dg, n, 0,
+                                  nullptr));
+        std::vector<double> hf(9 * n);
+        CHECK(hipMemcpy(hf.data(), dg, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
+        int64_t differ = 0;
+        for (int64_t i = 0; i < 9 * n; ++i)
+            differ += std::memcmp(&hf[i], &ha[i], sizeof(double)) != 0 &&
+                      !(std::isnan(hf[i]) && std::isnan(ha[i]));
+        std::printf("  fused gather + cal_Homo_ACA: %lld of %lld words differ from gather-then-solve\n",
+                    (long long)differ, (long long)(9 * n));
+        if (differ) ++failures;
         int64_t agree = 0, finite = 0;
         for (int64_t i = 0; i < n; ++i) {
             const double w = ha[8 * n + i];
@@ -147,8 +159,11 @@ int main(int argc, char** argv) {
         std::printf("  ACA vs GE: %lld of %lld finite solutions agree to 1e-6 relative\n",
                     (long long)agree, (long long)finite);
         if (finite > 0 && agree < finite * 99 / 100) ++failures;
-        CHECK(hipFree(ds)); CHECK(hipFree(dt)); CHECK(hipFree(dh)); CHECK(hipFree(dg));
+        CHECK(hipFree(p_d)); CHECK(hipFree(ds)); CHECK(hipFree(dt)); CHECK(hipFree(dh));
+        CHECK(hipFree(dg));
         std::printf("----------------------------------------------------------\n");
     }
+    CHECK(hipFree(d_src_in));
+    CHECK(hipFree(d_tar_in));
     return failures ? 1 : 0;
 }

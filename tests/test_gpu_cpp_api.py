@@ -56,8 +56,9 @@ def test_cpp_dropin_program(pkg, dev, tmp_path):
 def test_cpp_runtime_harness(pkg, dev, tmp_path):
     """examples/runtime_test.cpp -- the reference GPU harness's flow in native C++ over the
     C ABI: reads the reference's point-file format (written here from the committed
-    orig_pts_wall.txt fixture), draws random 4-subsets, times ACA/SKS/GPT/GE per N and
-    checks ACA against GE."""
+    orig_pts_wall.txt fixture), draws 4*N MRG32K3A words, gathers the 4-subsets on the device
+    (get_rand_list), times ACA/SKS/GPT/GE per N, checks ACA against GE and the fused gather +
+    solve against gather-then-solve bit for bit."""
     import numpy as np
     from conftest import load_golden
     g = load_golden("cpp_wall.npz")
@@ -78,3 +79,4 @@ def test_cpp_runtime_harness(pkg, dev, tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "cal_Homo_ACA N=100000" in r.stdout and "cal_Homo_GE  N=100000" in r.stdout
+    assert "0 of 900000 words differ" in r.stdout, r.stdout
