@@ -2,7 +2,8 @@
  * sks_homography.h -- C ABI of the MI355X (gfx950) batched 4-point homography
  * solver.  Library: sks-homography_amd/lib/libsks_homography_amd.so
  *
- * Every entry point except hg_solve_host_* (host-resident batches, synchronous, below):
+ * Every entry point except hg_solve_host_* (host-resident batches, synchronous, below) and
+ * hg_rand_mrg32k3a_u32 (rocRAND's generator: allocates and synchronises, below):
  *   - takes DEVICE pointers the caller owns (the library allocates nothing),
  *   - enqueues its work on `stream` (a hipStream_t; NULL = the legacy default
  *     stream) and returns without synchronising,
@@ -171,7 +172,8 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
 /* curandCreateGenerator(CURAND_RNG_PSEUDO_MRG32K3A) + curandSetPseudoRandomGeneratorSeed
  * + curandGenerate (.cu:1441-1444) through rocRAND's MRG32K3A (default ordering): `count`
  * 32-bit words into `out`.  The one entry point that allocates (rocRAND's generator
- * state, created and destroyed per call) and so is not graph-capturable.  Equality with
+ * state, created and destroyed per call): it returns once the words are written (it
+ * synchronises `stream`) and is not graph-capturable.  Equality with
  * cuRAND's stream is not checked here (no cuRAND in this image). */
 int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream);
 

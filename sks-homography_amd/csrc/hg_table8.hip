@@ -54,10 +54,14 @@ int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stre
     rocrand_status st = rocrand_set_stream(g, reinterpret_cast<hipStream_t>(stream));
     if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_seed(g, seed);
     if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_generate(g, out, (size_t)count);
+    // the generator's device state must outlive the kernels that use it: wait for them
+    // before it is released (this call is synchronous, like curandGenerate's caller at
+    // .cu:1444-1448, which launches get_rand_list on the default stream right after)
+    const hipError_t sync = hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream));
     const rocrand_status dst = rocrand_destroy_generator(g);
     if (st != ROCRAND_STATUS_SUCCESS || dst != ROCRAND_STATUS_SUCCESS)
         return (int)hipErrorLaunchFailure;
-    return 0;
+    return (int)sync;
 }
 
 int hg_get_rand_list_f64(const uint32_t* rand_list, uint32_t size, const double* pool_src,
