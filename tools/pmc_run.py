@@ -55,6 +55,13 @@ def main():
     idx = pkg.fill_bits(big * 4, 11, 0, dev).view(big, 4)
     for _ in range(REPS):
         pkg.sample_solve(ps, pt, idx)
+    del idx
+    # the fused binary64 gather + cal_Homo_ACA in the reference's formats (hg_gather.hpp),
+    # 10 M hypotheses on the wall file: 16 B of words in, 72 B of H out per hypothesis
+    rl = pkg.rand_mrg32k3a(4 * n, 11, dev).view(4, n)
+    ps64, pt64 = ps.double(), pt.double()
+    for _ in range(REPS):
+        pkg.gather_solve(ps64, pt64, rl, "aca")
     torch.cuda.synchronize()
     print("pmc workload done")
 

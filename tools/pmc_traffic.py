@@ -31,6 +31,7 @@ KEYS = {
     "tensor_aca_offsets": ("void hg::tensor_aca_offsets_kernel", None),
     "sample_solve_lds": ("void hg::sample_solve_lds_kernel", None),
     "solve_soa": ("void hg::solve_soa_vec", None),
+    "gather_solve_f64_aca": ("void hg::gather_solve_f64_kernel<0", 10_000_000 * 88),
 }
 
 
