@@ -3,7 +3,7 @@
  * solver.  Library: sks-homography_amd/lib/libsks_homography_amd.so
  *
  * Every entry point except hg_solve_host_* (host-resident batches, synchronous, below) and
- * hg_rand_mrg32k3a_u32 (rocRAND's generator: allocates and synchronises, below):
+ * hg_rand_mrg32k3a_u32 (rocRAND's generator: allocates once, synchronises, below):
  *   - takes DEVICE pointers the caller owns (the library allocates nothing),
  *   - enqueues its work on `stream` (a hipStream_t; NULL = the legacy default
  *     stream) and returns without synchronising,
@@ -171,9 +171,10 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
 
 /* curandCreateGenerator(CURAND_RNG_PSEUDO_MRG32K3A) + curandSetPseudoRandomGeneratorSeed
  * + curandGenerate (.cu:1441-1444) through rocRAND's MRG32K3A (default ordering): `count`
- * 32-bit words into `out`.  The one entry point that allocates (rocRAND's generator
- * state, created and destroyed per call): it returns once the words are written (it
- * synchronises `stream`) and is not graph-capturable.  Equality with
+ * 32-bit words into `out`; every call restarts the stream at `seed`, offset 0.  The one
+ * entry point that allocates (rocRAND's generator state, one per device, created on first
+ * use and kept); calls are serialised, each returns once its words are written (it
+ * synchronises `stream`), and it is not graph-capturable.  Equality with
  * cuRAND's stream is not checked here (no cuRAND in this image). */
 int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream);
 

@@ -8,6 +8,8 @@
 //   hg_gather_solve_f64    get_rand_list fused with cal_Homo_{ACA,SKS,GE,GPT}: (9,n) H
 #include <rocrand/rocrand.h>
 
+#include <mutex>
+
 #include "hg_gather.hpp"
 
 namespace {
@@ -48,19 +50,30 @@ int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stre
     if (count < 0) return kInvalid;
     if (count == 0) return 0;
     if (!out || misaligned(out, 4)) return kInvalid;
-    rocrand_generator g = nullptr;
-    if (rocrand_create_generator(&g, ROCRAND_RNG_PSEUDO_MRG32K3A) != ROCRAND_STATUS_SUCCESS)
+    // One generator per device, created on first use and kept (its state allocation is most
+    // of a fresh generator's cost); calls are serialised on it.  Re-seeding every call
+    // restarts the stream at offset 0, so each call's words are those of a fresh
+    // curandCreateGenerator + SetPseudoRandomGeneratorSeed + Generate (.cu:1441-1444).
+    constexpr int kMaxDevices = 64;
+    static std::mutex mu;
+    static rocrand_generator gens[kMaxDevices] = {};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return kInvalid;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!gens[dev] &&
+        rocrand_create_generator(&gens[dev], ROCRAND_RNG_PSEUDO_MRG32K3A) != ROCRAND_STATUS_SUCCESS) {
+        gens[dev] = nullptr;
         return (int)hipErrorNotInitialized;
+    }
+    rocrand_generator g = gens[dev];
     rocrand_status st = rocrand_set_stream(g, reinterpret_cast<hipStream_t>(stream));
     if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_seed(g, seed);
     if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_generate(g, out, (size_t)count);
-    // the generator's device state must outlive the kernels that use it: wait for them
-    // before it is released (this call is synchronous, like curandGenerate's caller at
-    // .cu:1444-1448, which launches get_rand_list on the default stream right after)
+    // the shared generator's device state is rewritten by the next call (perhaps on another
+    // stream): wait for this call's kernels before releasing it (the call is synchronous,
+    // like curandGenerate's caller at .cu:1444-1448)
     const hipError_t sync = hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream));
-    const rocrand_status dst = rocrand_destroy_generator(g);
-    if (st != ROCRAND_STATUS_SUCCESS || dst != ROCRAND_STATUS_SUCCESS)
-        return (int)hipErrorLaunchFailure;
+    if (st != ROCRAND_STATUS_SUCCESS) return (int)hipErrorLaunchFailure;
     return (int)sync;
 }
 

@@ -125,6 +125,14 @@ def test_mrg32k3a_stream(pkg, dev):
     c = pkg.rand_mrg32k3a(1 << 22, 12, dev)
     assert torch.equal(a, b)
     assert not torch.equal(a, c)
+    # every call restarts its seed's stream (one cached generator per device): a request of
+    # another size and seed in between, or on another stream, leaves the next call's words alone
+    pkg.rand_mrg32k3a(12345, 99, dev)
+    s2 = torch.cuda.Stream(dev)
+    with torch.cuda.stream(s2):
+        d = pkg.rand_mrg32k3a(1 << 22, 11, dev)
+    s2.synchronize()
+    assert torch.equal(a, d)
     u = a.cpu().numpy().view(np.uint32).astype(np.float64)
     assert u.min() >= 1 and u.max() <= MRG_M1
     x = u / 2.0**32
