@@ -200,7 +200,8 @@ DEFINE_BATCH(oracle_sks_f64, double, sks_one_f64, normalize_f64)
  * ATen CPU evaluation (pinned by tests/golden/tensor_aca_rect.npz):
  *   d[r][j]  = tar[r][j+1] - tar[r][0]
  *   c        = cross(d[1], d[0]), component i = fma(a_j, b_k, -(a_k * b_j))
- *   S        = (c0 + c1) + c2
+ *   S        = ((+0 + c0) + c1) + c2  (torch.sum's accumulator starts at +0: three -0
+ *              terms give +0; written ((c0 + c1) + c2) + 0, the same value for every input)
  *   b[r]     = S * tar[r][0]
  *   H[r][0]  = tar[r][1] * c0 - b[r]
  *   H[r][1]  = div * (tar[r][2] * c1 - b[r])
@@ -216,7 +217,7 @@ int oracle_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int
         float c0 = fmaf(ay, bz, -(az * by));
         float c1 = fmaf(az, bx, -(ax * bz));
         float c2 = fmaf(ax, by, -(ay * bx));
-        float S = (c0 + c1) + c2;
+        float S = ((c0 + c1) + c2) + 0.f;
         float mx = s[0], my = s[4];
         for (int r = 0; r < 3; ++r) {
             float br = S * t[4 * r + 0];
@@ -322,7 +323,7 @@ int oracle_tensor_aca_rect_backward_f32(const float* src, const float* tar, cons
         float c0 = fmaf(ay, bz, -(az * by));
         float c1 = fmaf(az, bx, -(ax * bz));
         float c2 = fmaf(ax, by, -(ay * bx));
-        float S = (c0 + c1) + c2;
+        float S = ((c0 + c1) + c2) + 0.f;
         float gc0 = 0.f, gc1 = 0.f, gS = 0.f, gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
         for (int r = 0; r < 3; ++r) {
             float br = S * t[4 * r];

@@ -360,8 +360,9 @@ __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9
 
 // TensorACA rectangle -> quad (PyTorch Codes/Modules_Runtime_Test.py:294-302),
 // evaluated as ATen evaluates it: the cross product contracts one product per
-// component into an FMA, the 3-term sum runs left to right, every other op rounds
-// on its own.  tr = (3,4) target tensor rows {x, y, w} x cols {M, N, P, Q}.
+// component into an FMA, the 3-term sum runs left to right from ATen's +0 accumulator
+// (so three -0 terms sum to +0: the trailing "+ 0.f", exact for every other value),
+// every other op rounds on its own.  tr = (3,4) target tensor rows {x, y, w} x cols {M, N, P, Q}.
 // SQUARE: the square specialisation of ACA_rect.m:28 (ratio 1, 44 FLOPs) -- drops the
 // multiply by div, which is exact when div == 1, so the bits are those of the general form.
 template <bool SQUARE = false>
@@ -372,7 +373,7 @@ __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], flo
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
     const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
     const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
-    const float sum = (c0 + c1) + c2;
+    const float sum = ((c0 + c1) + c2) + 0.f;  // torch.sum starts from +0
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const float b = sum * tr[4 * r];
@@ -418,7 +419,7 @@ __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], floa
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
     const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
     const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
-    const float sum = (c0 + c1) + c2;
+    const float sum = ((c0 + c1) + c2) + 0.f;  // torch.sum starts from +0
     float gc0 = 0.f, gc1 = 0.f, gs = 0.f;
     gmx = 0.f; gmy = 0.f; gscale = 0.f; gdiv = 0.f;
 #pragma unroll

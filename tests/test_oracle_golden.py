@@ -227,3 +227,33 @@ def test_oracle_ge_f64_tracks_reference_f32(orc, oracle):
     h32 = g["ge_f32"].astype(np.float64)
     rel = np.abs(h64 - h32) / np.maximum(np.abs(h64), 1e-12)
     assert np.median(rel) < 1e-5
+
+
+def test_tensor_aca_restatement_equals_aten_on_special_values(orc, oracle):
+    """The TensorACA restatement against the reference's ATen composition on CPU torch
+    (bench.torch_tensor_aca_rect, Modules_Runtime_Test.py:294-302) beyond the fixtures:
+    special values, signed zeros (three -0 cross terms: torch.sum starts from +0) and random
+    bit patterns, bit for bit.  AVX-512 hosts only (ATen's cross contracts to FMA there)."""
+    import pytest
+    import torch
+
+    import bench
+    if not orc.cpu_has_avx512():
+        pytest.skip("ATen's CPU cross takes its FMA path only on an AVX-512 host")
+    rng = np.random.default_rng(48259)
+    vals = np.array([0.0, -0.0, 1.0, -1.0, 2.0, 0.5, 1024.0, np.inf, -np.inf, np.nan, 1e-45,
+                     -1.2e-40, 3e38], np.float32)
+    B = 50_000
+    cases = [tuple(rng.choice(vals, size=(B, 3, 4)).astype(np.float32) for _ in range(2)),
+             tuple(rng.integers(0, 2**32 - 1, size=(B, 3, 4), dtype=np.uint32, endpoint=True)
+                   .view(np.float32) for _ in range(2))]
+    # the case that showed it: every cross term -0 (underflowing products of tiny differences)
+    one = np.array([[[1.4e-45, -0.0, 0.0, 0.0], [-1.2e-40, 0.0, -0.0, 0.0], [-0.0, 1024.0, -0.0, 0.0]]],
+                   np.float32)
+    cases.append((np.full((1, 3, 4), 2.0, np.float32), one))
+    for src, tar in cases:
+        for scale, div in ((128.0, 1.0), (50.0, 1.25), (float("inf"), 0.5)):
+            want = bench.torch_tensor_aca_rect(torch.from_numpy(src), torch.from_numpy(tar),
+                                               torch.tensor([scale]), torch.tensor([div])).numpy()
+            got = oracle.tensor_aca_rect(src, tar, scale, div)
+            assert orc.same_bits(got, want).all(), (scale, div, int((~orc.same_bits(got, want)).sum()))
