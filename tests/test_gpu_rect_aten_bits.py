@@ -58,3 +58,24 @@ def test_rect_equals_aten_cpu_composition(orc, pkg, dev, kind, scale, div):
                 f"problem {i}, element {bad[0] % 9}: got {got[i].ravel().tolist()} want "
                 f"{want[i].ravel().tolist()} src {src[i].ravel().view(np.uint32).tolist()} "
                 f"tar {tar[i].ravel().view(np.uint32).tolist()}")
+
+
+@pytest.mark.parametrize("tag,scale,div", [("128_1", 128.0, 1.0), ("50_125", 50.0, 1.25),
+                                           ("inf_05", float("inf"), 0.5)])
+def test_rect_and_vanilla_equal_reference_special_fixture(orc, pkg, dev, tag, scale, div):
+    """tests/golden/torch_special.npz -- the reference's own TensorACA_rect and ACA_vanilla
+    statements executed on CPU torch here (tools/make_golden.py --torch-special) over special
+    values, problem 0 an all-(-0) cross product -- through both scalar forms and ACA_vanilla."""
+    from conftest import load_golden
+    g = load_golden("torch_special.npz")
+    B = g["rect_src"].shape[0]
+    ds, dt = torch.from_numpy(g["rect_src"]).to(dev), torch.from_numpy(g["rect_tar"]).to(dev)
+    sc = torch.tensor([scale], dtype=torch.float32, device=dev)
+    dv = torch.tensor([div], dtype=torch.float32, device=dev)
+    for what, got in (("device scalars", pkg.TensorACA_rect(B, ds, dt, sc, dv)),
+                      ("host scalars", pkg.TensorACA_rect(B, ds, dt, scale, div))):
+        ok = orc.same_bits(got.cpu().numpy(), g[f"rect_{tag}"])
+        assert ok.all(), f"{tag} {what}: {int((~ok).sum())} differ"
+    H = pkg.ACA_vanilla(B, torch.from_numpy(g["van_src"]).to(dev), torch.from_numpy(g["van_tar"]).to(dev))
+    ok = orc.same_bits(H.cpu().numpy(), g["vanilla"])
+    assert ok.all(), f"ACA_vanilla: {int((~ok).sum())} differ"

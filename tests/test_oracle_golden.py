@@ -257,3 +257,23 @@ def test_tensor_aca_restatement_equals_aten_on_special_values(orc, oracle):
                                                torch.tensor([scale]), torch.tensor([div])).numpy()
             got = oracle.tensor_aca_rect(src, tar, scale, div)
             assert orc.same_bits(got, want).all(), (scale, div, int((~orc.same_bits(got, want)).sum()))
+
+
+@pytest.mark.parametrize("tag,scale,div", [("128_1", 128.0, 1.0), ("50_125", 50.0, 1.25),
+                                           ("inf_05", float("inf"), 0.5)])
+def test_tensor_aca_restatement_equals_reference_special_fixture(orc, oracle, tag, scale, div):
+    """torch_special.npz: the reference's own TensorACA_rect statements on special values
+    (tools/make_golden.py --torch-special), problem 0 an all-(-0) cross product."""
+    g = load_golden("torch_special.npz")
+    got = oracle.tensor_aca_rect(g["rect_src"], g["rect_tar"], scale, div)
+    ok = orc.same_bits(got, g[f"rect_{tag}"])
+    assert ok.all(), int((~ok).sum())
+
+
+def test_aca_vanilla_restatement_equals_reference_special_fixture(orc, oracle):
+    g = load_golden("torch_special.npz")
+    B = g["van_src"].shape[0]
+    got = oracle.solve("aca", g["van_src"].reshape(B, 8), g["van_tar"].reshape(B, 8),
+                       normalize=False).reshape(B, 3, 3)
+    ok = orc.same_bits(got, g["vanilla"])
+    assert ok.all(), int((~ok).sum())

@@ -267,6 +267,8 @@ def main():
                     "scale 50/div 1.25)" % (torch.__version__,
                                             torch.backends.cpu.get_cpu_capability()))
 
+    manifest.append(torch_special())
+
     # 6. the reference input generator itself (seed 0, B=8)
     torch.manual_seed(0)
     out = gen["adjust"]("cpu", 8)
@@ -283,5 +285,47 @@ def main():
     print("\n".join(manifest))
 
 
+def torch_special() -> str:
+    """TensorACA_rect / ACA_vanilla statements of the reference on special values, CPU torch:
+    signed zeros, +-Inf, NaN, subnormals, near-overflow and ties (4096 problems each), the
+    all-(-0) cross-product case (torch.sum's +0 accumulator decides its sign), and quads over
+    24 decades of scale.  Writes tests/golden/torch_special.npz; returns its manifest line."""
+    rng = np.random.default_rng(20261016)
+    vals = np.array([0.0, -0.0, 1.0, -1.0, 2.0, 0.5, 3.0, 1024.0, np.inf, -np.inf, np.nan,
+                     1e-45, -1.2e-40, 3e38, -3e38], np.float32)
+    w = np.array([8, 6, 8, 6, 6, 4, 4, 4, 1, 1, 1, 1, 1, 1, 1], np.float64)
+    B = 4096
+    rect_src = rng.choice(vals, size=(B, 3, 4), p=w / w.sum()).astype(np.float32)
+    rect_tar = rng.choice(vals, size=(B, 3, 4), p=w / w.sum()).astype(np.float32)
+    # problem 0: every cross term -0 (underflowing products of tiny differences)
+    rect_src[0] = 2.0
+    rect_tar[0] = [[1.4e-45, -0.0, 0.0, 0.0], [-1.2e-40, 0.0, -0.0, 0.0], [-0.0, 1024.0, -0.0, 0.0]]
+    scaled = lambda: (rng.uniform(-1, 1, (B, 4, 2)) *  # noqa: E731
+                      10.0 ** rng.integers(-12, 13, (B, 1, 1))).astype(np.float32)
+    van_src, van_tar = scaled(), scaled()
+    k = B // 4  # a quarter of the quads with special coordinates mixed in
+    van_src[:k] = rng.choice(vals, size=(k, 4, 2), p=w / w.sum())
+    out = {"rect_src": rect_src, "rect_tar": rect_tar, "van_src": van_src, "van_tar": van_tar}
+    for tag, sc, dv in (("128_1", 128.0, 1.0), ("50_125", 50.0, 1.25), ("inf_05", np.inf, 0.5)):
+        out[f"rect_{tag}"] = run_ref_statements(
+            "TensorACA_rect", bs=B, src=torch.from_numpy(rect_src), tar=torch.from_numpy(rect_tar),
+            scale=torch.tensor([sc], dtype=torch.float32),
+            div=torch.tensor([dv], dtype=torch.float32))["H"].numpy().copy()
+    out["vanilla"] = run_ref_statements("ACA_vanilla", bs=B, src=torch.from_numpy(van_src),
+                                        tar=torch.from_numpy(van_tar))["H"].numpy().copy()
+    np.savez_compressed(os.path.join(OUT, "torch_special.npz"), **out)
+    return ("torch_special.npz: TensorACA_rect (scale/div 128/1, 50/1.25, inf/0.5) and ACA_vanilla "
+            "statements of the reference on CPU torch %s (ATen CPU capability %s) over 4096 "
+            "special-value problems each (signed zeros, +-Inf, NaN, subnormals, near-overflow; "
+            "problem 0 of rect: all three cross terms -0) and 24 decades of scale" %
+            (torch.__version__, torch.backends.cpu.get_cpu_capability()))
+
+
 if __name__ == "__main__":
-    main()
+    if sys.argv[1:] == ["--torch-special"]:  # this fixture alone, appended to the manifest
+        line = torch_special()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    else:
+        main()
