@@ -150,3 +150,33 @@ def test_sampler_pairs_equal_reference_cpp(orc, oracle, ref, pkg, dev, npool):
         _check(orc, pkg.sample_solve(ps, pt, idx, algo=algo), want, f"indexed {algo} npool={npool}")
         seeded = pkg.sample_solve_seeded(ps, pt, n, 21, 5, algo=algo)
         _check(orc, seeded, want, f"seeded {algo} npool={npool}")
+
+
+def test_single_call_and_host_batch_equal_reference_cpp(orc, ref, pkg, dev):
+    """The two other kernel forms behind the reference's own signatures: the single-problem
+    sks::runKernel_* calls on host pointers (points in the launch arguments, hg_solve_one_*)
+    and host-resident batches (hg_solve_host_*, the kernel reading the caller's pageable
+    memory over PCIe), on random binary32 / binary64 bit patterns and special mixtures."""
+    import ctypes
+
+    from test_gpu_parity import _sks_api
+    fns = _sks_api(pkg)
+    s32, t32 = _random_bits(256, np.float32, 107)
+    m32, n32 = _special_mixture(256, 108)
+    s64, t64 = _random_bits(256, np.float64, 109)
+    for key, algo, (s, t) in (("aca", "aca", (s32, t32)), ("sks", "sks", (s32, t32)),
+                              ("aca", "aca", (m32, n32)), ("sks", "sks", (m32, n32)),
+                              ("aca64", "aca", (s64, t64)), ("sks64", "sks", (s64, t64))):
+        f, ct = fns[key]
+        P = ctypes.POINTER(ct)
+        want = ref.solve(algo, s, t)
+        got = np.zeros_like(want)
+        for i in range(s.shape[0]):
+            si, ti, hi = (np.ascontiguousarray(a[i]) for a in (s, t, got))
+            assert f(si.ctypes.data_as(P), ti.ctypes.data_as(P), hi.ctypes.data_as(P)) == 0
+            got[i] = hi
+        _check(orc, got, want, f"sks::{key} single calls")
+    for s, t in ((_random_bits(100_003, np.float32, 110)), (_random_bits(100_003, np.float64, 111))):
+        for algo in ("aca", "sks"):
+            H = pkg.solve_host(algo, torch.from_numpy(s), torch.from_numpy(t), normalize=True)
+            _check(orc, H, ref.solve(algo, s, t), f"solve_host {algo} {s.dtype}")
