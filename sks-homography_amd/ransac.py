@@ -16,10 +16,33 @@ from . import _lib
 from .ops import _gpu_device, _guard, _require_device, _stream
 
 
+_strtof_fn = None
+
+
+def _strtof(tokens):
+    """Decimal strings -> binary32 the way the reference's sscanf("%f") converts them (C
+    strtof: one correct rounding).  numpy's str -> float32 goes through binary64 first, and
+    that double rounding gives the other neighbour for a decimal just above a binary32
+    midpoint (e.g. 1.00000005960464477539062500000001 -> 1.0 instead of 1 + 2^-23)."""
+    global _strtof_fn
+    import ctypes
+    import ctypes.util
+
+    import numpy as np
+
+    if _strtof_fn is None:
+        fn = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6").strtof
+        fn.restype = ctypes.c_float
+        fn.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+        _strtof_fn = fn
+    return np.array([_strtof_fn(t.encode(), None) for t in tokens], dtype=np.float32)
+
+
 def read_points(filename: str):
-    """The reference's correspondence-file reader (CPU_Runtime Test/utils.cpp:6-21): the
-    first line holds the count N, then N lines "x1 y1 x2 y2" (source point, target
-    point).  Returns (pool_src, pool_tar), each an (N,2) float32 numpy array, ready for
+    """The reference's correspondence-file reader (CPU_Runtime Test/utils.cpp:6-21; the GPU
+    harness's copy at GPU_Runtime Test.cu:31-46): the first line holds the count N, then N
+    lines "x1 y1 x2 y2" (source point, target point), each value parsed as sscanf's "%f"
+    does.  Returns (pool_src, pool_tar), each an (N,2) float32 numpy array, ready for
     sample_solve / score / ransac (orig_pts_wall.txt is the reference's own file)."""
     import numpy as np
 
@@ -28,13 +51,13 @@ def read_points(filename: str):
         if not head:
             raise ValueError(f"{filename}: empty file (expected the point count first)")
         count = int(head[0])
-        rows = []
+        tokens = []
         for i in range(count):
             vals = f.readline().split()[:4]
             if len(vals) < 4:
                 raise ValueError(f"{filename}: line {i + 2} has fewer than 4 values")
-            rows.append(vals)
-    a = np.asarray(rows, dtype=np.float32).reshape(count, 4)
+            tokens += vals
+    a = _strtof(tokens).reshape(count, 4)
     return np.ascontiguousarray(a[:, 0:2]), np.ascontiguousarray(a[:, 2:4])
 
 

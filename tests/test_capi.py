@@ -280,3 +280,30 @@ def test_read_points_matches_reference_format(pkg, tmp_path):
     bad.write_text("3\n1 2 3 4\n")
     with pytest.raises(ValueError):
         pkg.read_points(str(bad))
+
+
+def test_read_points_rounds_once_like_sscanf(pkg, tmp_path):
+    """Values are converted the way the reference's sscanf("%f", &float) converts them (one
+    correct rounding to binary32), not through binary64 first: a decimal just above the
+    midpoint between 1 and 1 + 2^-23 must give 1 + 2^-23 (binary64 first lands on the
+    midpoint, and ties-to-even then gives 1).  Checked against the C library's strtof and
+    exact rational rounding."""
+    import ctypes
+    import ctypes.util
+    from fractions import Fraction
+
+    import numpy as np
+    tricky = ["1.00000005960464477539062500000001", "0.99999997019767761230468749999999",
+              "16777217.0000000000000001", "3.4028235677973366e38", "1e-46", "-0.0", "356.39"]
+    path = tmp_path / "tricky.txt"
+    path.write_text("2\n" + " ".join(tricky[:4]) + "\n" + " ".join(tricky[3:7]) + "\n")
+    rs, rt = pkg.read_points(str(path))
+    got = np.concatenate([rs, rt], axis=1).ravel()
+    strtof = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6").strtof
+    strtof.restype, strtof.argtypes = ctypes.c_float, [ctypes.c_char_p, ctypes.c_void_p]
+    want = np.array([strtof(t.encode(), None) for t in tricky[:4] + tricky[3:7]], np.float32)
+    assert np.array_equal(got.view(np.uint32), want.view(np.uint32))
+    assert got[0].view(np.uint32) == np.float32(1.0).view(np.uint32) + 1
+    # the first value by exact rounding of the rational: above the midpoint -> the upper neighbour
+    lo, hi = Fraction(1), Fraction(1) + Fraction(1, 2**23)
+    assert Fraction(tricky[0]) > (lo + hi) / 2 and Fraction(float(got[0])) == hi

@@ -79,9 +79,15 @@ def ref_generators():
 
 # ----------------------------------------------------------------- data helpers
 def read_wall():
+    """orig_pts_wall.txt parsed as the reference parses it: sscanf("%f") = C strtof, one
+    rounding to binary32 (not float() then float32, which rounds twice)."""
+    import ctypes
+    import ctypes.util
+    strtof = ctypes.CDLL(ctypes.util.find_library("c") or "libc.so.6").strtof
+    strtof.restype, strtof.argtypes = ctypes.c_float, [ctypes.c_char_p, ctypes.c_void_p]
     with open(WALL) as f:
         count = int(f.readline().split()[0])
-        rows = [list(map(float, f.readline().split()[:4])) for _ in range(count)]
+        rows = [[strtof(v.encode(), None) for v in f.readline().split()[:4]] for _ in range(count)]
     a = np.asarray(rows, dtype=np.float32)
     return a[:, 0:2], a[:, 2:4]
 
