@@ -43,7 +43,8 @@ constexpr int gather_block() { return ALGO == kGPT ? 512 : 1024; }
 
 // V = 2 (tune): a lane owns two consecutive hypotheses, so its word reads are 8 B and its H
 // stores 16 B per row (needs n even and 16-B aligned H).
-template <int ALGO, bool NORM, bool POOL_LDS, int V = 1>
+// NTS (tune): non-temporal H stores (shipped) or default-policy ones.
+template <int ALGO, bool NORM, bool POOL_LDS, int V = 1, bool NTS = true>
 __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
     const uint32_t* __restrict__ rand_list, uint32_t size, uint64_t magic,
     const double2* __restrict__ pool_src, const double2* __restrict__ pool_tar,
@@ -98,7 +99,8 @@ __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
 #pragma unroll
         for (int k = 0; k < 9; ++k) {
             if constexpr (V == 1) {
-                __builtin_nontemporal_store(h[0][k], H + id + k * n);
+                if constexpr (NTS) __builtin_nontemporal_store(h[0][k], H + id + k * n);
+                else H[id + k * n] = h[0][k];
             } else {
                 typedef double f64x2 __attribute__((ext_vector_type(2)));
                 const f64x2 o = {h[0][k], h[1][k]};

@@ -702,12 +702,15 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
 // 0 = pool in LDS (the shipped form for pools up to 5120 pairs; 1024-lane persistent blocks),
 // 1 = the global-gather form, 2 = pool in LDS with 512-lane blocks (two blocks per CU when
 // the pool fits 80 KiB), 3 = pool in LDS, 256-lane blocks, 4 / 5 / 6 = 0 / 2 / 3 with two
-// hypotheses per lane (8-B word reads, 16-B H stores; n even).  Unnormalised.
+// hypotheses per lane (8-B word reads, 16-B H stores; n even), 7 = 0 with default-policy
+// (not non-temporal) H stores.  Unnormalised.
 int hg_tune_gather_solve_f64(int variant, int algo, const double* pool_src, const double* pool_tar,
                              uint32_t size, const uint32_t* rand_list, double* H, int64_t n,
                              void* stream) {
-    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 6)
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 7)
         return (int)hipErrorInvalidValue;
+    const bool plain_st = variant == 7;
+    if (plain_st) variant = 0;
     const bool pair = variant >= 4;
     if (pair && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15u) ||
                  (reinterpret_cast<uintptr_t>(rand_list) & 7u)))
@@ -727,9 +730,11 @@ int hg_tune_gather_solve_f64(int variant, int algo, const double* pool_src, cons
     }
     if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
     auto k = algo == 0 ? (pair ? hg::gather_solve_f64_kernel<hg::kACA, false, true, 2>
-                               : hg::gather_solve_f64_kernel<hg::kACA, false, true>)
+                               : (plain_st ? hg::gather_solve_f64_kernel<hg::kACA, false, true, 1, false>
+                                           : hg::gather_solve_f64_kernel<hg::kACA, false, true>))
                        : (pair ? hg::gather_solve_f64_kernel<hg::kSKS, false, true, 2>
-                               : hg::gather_solve_f64_kernel<hg::kSKS, false, true>);
+                               : (plain_st ? hg::gather_solve_f64_kernel<hg::kSKS, false, true, 1, false>
+                                           : hg::gather_solve_f64_kernel<hg::kSKS, false, true>));
     if (lds > hg::kSampleLdsMax && !hg::lds_opt_in(k)) return (int)hipErrorInvalidValue;
     int64_t per_cu = (int64_t)(160 * 1024) / (int64_t)lds;
     const int64_t max_per_cu = 2048 / block;

@@ -21,7 +21,10 @@ import __graft_entry__ as ge  # noqa: E402
 NAMES = {0: "pool in LDS, 1024-lane persistent blocks (shipped)", 1: "global gather",
          2: "pool in LDS, 512-lane blocks", 3: "pool in LDS, 256-lane blocks",
          4: "pool in LDS, 1024-lane blocks, 2 per lane", 5: "pool in LDS, 512-lane blocks, 2 per lane",
-         6: "pool in LDS, 256-lane blocks, 2 per lane"}
+         6: "pool in LDS, 256-lane blocks, 2 per lane",
+         7: "pool in LDS, 1024-lane blocks, default-policy H stores"}
+if os.environ.get("KB_GATHER_VARIANTS"):  # e.g. "0,7"
+    NAMES = {int(v): NAMES[int(v)] for v in os.environ["KB_GATHER_VARIANTS"].split(",")}
 ROUNDS = int(os.environ.get("KB_ROUNDS", "7"))
 
 
