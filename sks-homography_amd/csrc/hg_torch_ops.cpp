@@ -61,7 +61,11 @@ at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::T
     on_gpu(scale_, "scale", dev);
     on_gpu(div_, "div", dev);
     check_rect(src_, tar_);
-    TORCH_CHECK(scale_.numel() >= 1 && div_.numel() >= 1, "sks_amd: scale/div must be non-empty");
+    // batch-uniform, one element each (the reference derives them from sample 0 into (1,)
+    // tensors, .py:33-35); a per-sample tensor would not mean what it does in the reference's
+    // broadcasting composition, so it is refused rather than read at element 0
+    TORCH_CHECK(scale_.numel() == 1 && div_.numel() == 1,
+                "sks_amd: scale and div must hold one element each (batch-uniform, .py:33-35)");
     const int64_t B = tar_.size(0);
     check_out(out, {B, 3, 3}, dev);
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
@@ -115,6 +119,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
     on_gpu(scale_, "scale", dev);
     on_gpu(div_, "div", dev);
     check_rect(src_, tar_);
+    TORCH_CHECK(scale_.numel() == 1 && div_.numel() == 1,
+                "sks_amd: scale and div must hold one element each (batch-uniform, .py:33-35)");
     const int64_t B = tar_.size(0);
     TORCH_CHECK(grad_.dim() == 3 && grad_.size(0) == B && grad_.size(1) == 3 && grad_.size(2) == 3,
                 "sks_amd::tensor_aca_rect_backward: grad must be (B,3,3)");

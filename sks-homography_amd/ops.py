@@ -212,8 +212,12 @@ def _dev_scalar(x, dev: torch.device) -> torch.Tensor:
     the reference keeps scale/div in (1,)-shaped tensors, .py:33-35; the op checks that
     it sits on the batch's device)."""
     if type(x) is torch.Tensor and x.dtype is torch.float32 and x.is_cuda:
-        return x
-    return torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)[:1]
+        return x  # the native op refuses more than one element
+    t = torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)
+    if t.numel() != 1:
+        raise ValueError(f"scale/div must be one batch-uniform value (.py:33-35), got "
+                         f"{t.numel()} elements")
+    return t
 
 
 def _gpu_device(device) -> torch.device:

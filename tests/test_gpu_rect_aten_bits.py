@@ -79,3 +79,17 @@ def test_rect_and_vanilla_equal_reference_special_fixture(orc, pkg, dev, tag, sc
     H = pkg.ACA_vanilla(B, torch.from_numpy(g["van_src"]).to(dev), torch.from_numpy(g["van_tar"]).to(dev))
     ok = orc.same_bits(H.cpu().numpy(), g["vanilla"])
     assert ok.all(), f"ACA_vanilla: {int((~ok).sum())} differ"
+
+
+def test_scale_and_div_must_be_batch_uniform(pkg, dev):
+    """scale / div hold one value for the whole batch (the reference derives them from sample
+    0 into (1,) tensors, .py:33-35): a multi-element one is refused, never read at element 0."""
+    torch.manual_seed(0)
+    _, _, sh, th, sc, dv = pkg.adjust(dev, 16)
+    assert pkg.TensorACA_rect(16, sh, th, sc, dv).shape == (16, 3, 3)
+    two = torch.tensor([128.0, 64.0], device=dev)
+    for bad_scale, bad_div in ((two, dv), (sc, two), (torch.tensor([128.0, 64.0]), 1.0)):
+        with pytest.raises((RuntimeError, ValueError)):
+            pkg.TensorACA_rect(16, sh, th, bad_scale, bad_div)
+    with pytest.raises((RuntimeError, ValueError)):
+        pkg.tensor_aca_rect_backward(sh, th, torch.ones((16, 3, 3), device=dev), two, dv)
