@@ -634,7 +634,7 @@ def reference_layout(d: Dist, pkg):
 
 def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
     """The reference harness's sampling flow in its own formats (GPU_Runtime Test.cu:
-    1441-1451) on its own point file, N = 1M: MRG32K3A words (rocRAND, seed 11), then
+    1443-1451) on its own point file, N = 1M: MRG32K3A words (rocRAND, seed 11), then
     get_rand_list + cal_Homo_ACA/SKS -- unfused (gather to (8,N) rows, then the SoA solver)
     and fused (hg_gather_solve_f64: 16 B of words in, 72 B of H out per hypothesis).
     Table 8 times cal_Homo_* alone (245 / 436 us at 1M)."""

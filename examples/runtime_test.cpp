@@ -3,7 +3,7 @@
 // cal_GPT / cal_GE timing loops) as a native C++ caller of the MI355X C ABI.  For each batch
 // size N it draws 4*N MRG32K3A words with seed 11 and gathers N random 4-subsets of the
 // file's correspondences on the device into the harness's SoA binary64 layout ((8,N) src /
-// tar, (9,N) H) exactly as .cu:1441-1451 does (hg_rand_mrg32k3a_u32, hg_get_rand_list_f64),
+// tar, (9,N) H) exactly as .cu:1443-1451 does (hg_rand_mrg32k3a_u32, hg_get_rand_list_f64),
 // then times back-to-back launches the way cal_ACA does (one calibration launch, loops sized
 // from it, event-timed mean), checks ACA against the GE baseline, and checks that the fused
 // gather + solve (hg_gather_solve_f64) returns the same bits as gather-then-cal_Homo_ACA.
@@ -108,7 +108,7 @@ int main(int argc, char** argv) {
     CHECK(hipMemcpy(d_tar_in, p2.data(), p2.size() * sizeof(double), hipMemcpyHostToDevice));
     int failures = 0;
     for (int64_t n = 1; n <= max_n; n *= 10) {
-        // 4*N MRG32K3A words, seed 11, then get_rand_list (.cu:1441-1451)
+        // 4*N MRG32K3A words, seed 11, then get_rand_list (.cu:1443-1451)
         uint32_t* p_d;
         double *ds, *dt, *dh, *dg;
         CHECK(hipMalloc(&p_d, 4 * n * sizeof(uint32_t)));

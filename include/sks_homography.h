@@ -163,20 +163,29 @@ int hg_ransac_score_f32(const float* H, int64_t n, const float* pool_src, const 
                         uint32_t npool, float thresh, uint32_t* counts, void* stream);
 
 /* ---- The reference's Table-8 sampling pipeline in its own formats (hg_table8.hip) ----
- * GPU_Runtime Test.cu:1441-1451: 4*n MRG32K3A words, get_rand_list, cal_ACA/cal_SKS.
+ * GPU_Runtime Test.cu:1443-1451: 4*n MRG32K3A words, get_rand_list, cal_ACA/cal_SKS.
  * rand_list is (4,n) uint32 -- word k of hypothesis id at rand_list[id + k*n], as
  * get_rand_list reads it (.cu:56-59) -- and each word selects pool[word % size] (modulo
  * bias and duplicates kept).  Pools are (size,2) binary64 {x, y} pairs (Point2d),
  * 16-B aligned. */
 
 /* curandCreateGenerator(CURAND_RNG_PSEUDO_MRG32K3A) + curandSetPseudoRandomGeneratorSeed
- * + curandGenerate (.cu:1441-1444) through rocRAND's MRG32K3A (default ordering): `count`
- * 32-bit words into `out`; every call restarts the stream at `seed`, offset 0.  The one
- * entry point that allocates (rocRAND's generator state, one per device, created on first
- * use and kept); calls are serialised, each returns once its words are written (it
- * synchronises `stream`), and it is not graph-capturable.  Equality with
- * cuRAND's stream is not checked here (no cuRAND in this image). */
+ * + curandGenerate (.cu:1443-1446): `count` 32-bit MRG32K3A words into `out`, every call
+ * starting the stream at `seed`, offset 0.  A hand-written generator (csrc/hg_mrg32k3a.hpp,
+ * hg_gather.hpp::mrg_words_kernel): L'Ecuyer's recurrence with rocRAND's seeding, output
+ * conversion and host-API word order (word i = position i / 2^17 of subsequence
+ * i % 2^17), equal to rocrand_generate's words (tested); cuRAND's own seeding, conversion
+ * and ordering are not available in this image, so equality with cuRAND is unpinned.
+ * Asynchronous on `stream`, allocates nothing, graph-capturable (the host computes the
+ * start states' jumps into the launch arguments). */
 int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream);
+
+/* HOST function: the MRG32K3A engine state after seeding with `seed`, skipping
+ * `subsequence` subsequences of 2^76 words and then `offset` words -- what
+ * curand_init(seed, subsequence, offset, &state) / rocrand_init set up -- as
+ * state[6] = {x1[n-3], x1[n-2], x1[n-1], x2[n-3], x2[n-2], x2[n-1]}.  The next word is then
+ * made from these.  Returns 0, or hipErrorInvalidValue for a NULL state. */
+int hg_mrg32k3a_state(uint64_t seed, uint64_t subsequence, uint64_t offset, uint32_t* state);
 
 /* get_rand_list (.cu:52-78) itself: d_src / d_tar (8,n) binary64 rows, row 2k / 2k+1 =
  * x / y of the k-th selected point. */
@@ -190,6 +199,13 @@ int hg_get_rand_list_f64(const uint32_t* rand_list, uint32_t size, const double*
  * flags 0 (the reference kernels' unnormalised H) or HG_FLAG_NORMALIZE. */
 int hg_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar, uint32_t size,
                         const uint32_t* rand_list, double* H, int64_t n, int flags, void* stream);
+
+/* The whole Table-8 draw step fused too (.cu:1443-1451 + :52-78 + :81-507): the bits of
+ * hg_rand_mrg32k3a_u32(words, 4*n, seed) followed by hg_gather_solve_f64(..., words, ...),
+ * with the (4,n) words made in registers and never written to memory.  n <= 2^61. */
+int hg_rand_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar,
+                             uint32_t size, uint64_t seed, double* H, int64_t n, int flags,
+                             void* stream);
 
 /* ONE problem, latency path: src[8] and tar[8] are read on the HOST and passed in the
  * kernel launch itself (no copy); H[9] is written by the device -- pass device memory,

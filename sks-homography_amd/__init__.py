@@ -20,8 +20,9 @@ from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib
 from .ops import (aca, fill_uniform, sks, solve, solve_grouped, solve_host, stream_copy, tensor_aca_rect,
                   tensor_aca_rect_autograd, tensor_aca_rect_backward,
                   tensor_aca_offsets, tensor_aca_offsets_backward)
-from .ransac import (RansacResult, fill_bits, gather_solve, get_rand_list, rand_mrg32k3a, ransac,
-                     read_points, sample_solve, sample_solve_seeded)
+from .ransac import (RansacResult, fill_bits, gather_solve, get_rand_list, mrg32k3a_state,
+                     rand_gather_solve, rand_mrg32k3a, ransac, read_points, sample_solve,
+                     sample_solve_seeded)
 from .ransac import score as ransac_score
 from .reference_api import ACA_vanilla, TensorACA_rect, adjust, getInput, getTar
 from .shard import gather_blocks, scatter_blocks, shard_range
@@ -33,7 +34,8 @@ __all__ = [
     "aca", "sks", "solve", "solve_grouped", "solve_host", "tensor_aca_rect", "tensor_aca_rect_autograd",
     "tensor_aca_rect_backward", "tensor_aca_offsets", "tensor_aca_offsets_backward",
     "fill_uniform", "sample_solve", "sample_solve_seeded", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
-    "read_points", "rand_mrg32k3a", "get_rand_list", "gather_solve",
+    "read_points", "rand_mrg32k3a", "get_rand_list", "gather_solve", "rand_gather_solve",
+    "mrg32k3a_state",
     "TensorACA_rect", "ACA_vanilla", "getInput", "getTar", "adjust", "shard_range",
     "gather_blocks", "scatter_blocks", "lib", "version", "HipError", "HG_LAYOUT_AOS", "HG_LAYOUT_SOA",
     "HG_FLAG_NORMALIZE", "BYTES_PER_PROBLEM", "RECT_BYTES_PER_PROBLEM",

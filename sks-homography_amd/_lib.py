@@ -48,6 +48,9 @@ SIGNATURES = {
     "hg_ransac_score_f32": ([_vp, _i64, _vp, _vp, ctypes.c_uint32, ctypes.c_float, _vp, _vp],
                             _int),
     "hg_rand_mrg32k3a_u32": ([_vp, _i64, ctypes.c_uint64, _vp], _int),
+    "hg_mrg32k3a_state": ([ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _vp], _int),
+    "hg_rand_gather_solve_f64": ([_int, _vp, _vp, ctypes.c_uint32, ctypes.c_uint64, _vp, _i64, _int,
+                                  _vp], _int),
     "hg_get_rand_list_f64": ([_vp, ctypes.c_uint32, _vp, _vp, _vp, _vp, _i64, _vp], _int),
     "hg_gather_solve_f64": ([_int, _vp, _vp, ctypes.c_uint32, _vp, _vp, _i64, _int, _vp], _int),
     "hg_solve_one_f32": ([_int, _vp, _vp, _vp, _int, _vp], _int),

@@ -76,15 +76,15 @@ def build(verbose: bool = False, force: bool = False) -> str:
         for f in [ex.submit(subprocess.run, c, check=True) for c in cmds]:
             f.result()
     if force or _stale(LIB, objs):
-        # rocRAND: the reference's MRG32K3A draws (hg_rand_mrg32k3a_u32, hg_table8.hip)
-        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs,
-               "-L/opt/rocm/lib", "-lrocrand", "-Wl,-rpath,/opt/rocm/lib"]
+        cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", LIB, *objs]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
     if force or _stale(TUNE_LIB, tune_objs + [LIB]):
+        # rocRAND: the checker of the hand-written MRG32K3A generator (hg_tune.hip)
         cmd = [cc, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", TUNE_LIB, *tune_objs,
-               f"-L{LIB_DIR}", "-lsks_homography_amd", "-Wl,-rpath,$ORIGIN"]
+               f"-L{LIB_DIR}", "-lsks_homography_amd", "-Wl,-rpath,$ORIGIN",
+               "-L/opt/rocm/lib", "-lrocrand", "-Wl,-rpath,/opt/rocm/lib"]
         if verbose:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)

@@ -1,14 +1,76 @@
 // hg_gather.hpp -- the reference's own sampling pipeline in its own data formats
-// (GPU_Runtime Test.cu:1441-1451): 4*N cuRAND MRG32K3A words laid out as FOUR ROWS of N
+// (GPU_Runtime Test.cu:1443-1451): 4*N cuRAND MRG32K3A words laid out as FOUR ROWS of N
 // (word k of hypothesis id at randList[id + k*N]), get_rand_list (:52-78) gathering
 // Point2d (two binary64) source / target points into (8,N) SoA binary64 rows, then
 // cal_Homo_* (:81-507) over them, unnormalised.  Round 1's sampler (hg_ransac.hpp) is the
 // binary32 AoS form of the same pipeline; these kernels keep the reference's formats so
 // Table 8's flow runs unchanged, with the gather and the solve fused into one pass.
 #pragma once
+#include "hg_mrg32k3a.hpp"
 #include "hg_ransac.hpp"
 
+#include <type_traits>
+
 namespace hg {
+
+// J^l and J^(512 h) for the subsequence jumps, evaluated by the compiler (internal linkage:
+// each translation unit holds its own copy of the 61 KiB)
+static __constant__ mrg::JumpTable kMrgJump = mrg::make_jump_table();
+static constexpr mrg::PowTable kMrgPow = mrg::make_pow_table();
+
+// J^l v for l < 256 (one table row per lane), as the binary64 engine state.  v: x1[3], x2[3].
+__device__ __forceinline__ mrg::State mrg_apply_lo(uint32_t l, const uint32_t (&v)[6]) {
+    const uint32_t* e = kMrgJump.lo[l];
+    mrg::State st;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        st.x1[r] = (double)mrg::row_dot<1>(e + 3 * r, v[0], v[1], v[2]);
+        st.x2[r] = (double)mrg::row_dot<2>(e + 9 + 3 * r, v[3], v[4], v[5]);
+    }
+    return st;
+}
+
+// Element t < 6 of (M v): row t % 3 of component t / 3 of the jump matrix entry e.
+__device__ __forceinline__ uint32_t mrg_entry_dot(const uint32_t* e, int t, const uint32_t* v) {
+    return t < 3 ? mrg::row_dot<1>(e + 3 * t, v[0], v[1], v[2])
+                 : mrg::row_dot<2>(e + 9 + 3 * (t - 3), v[3], v[4], v[5]);
+}
+
+// The host API's `count` words: word i = position i >> 17 of subsequence i & (2^17 - 1).
+// Block (x, j) owns subsequences 256 x .. 256 x + 255 and positions [j Q, j Q + Q): six lanes
+// make the block's base J^(256 x) y[j] (y[j] = A^(j Q) x0), every lane then applies J^l for
+// its own l < 256 and writes its positions -- lane-consecutive subsequences, so every store
+// instruction covers 256 contiguous bytes.  Default-policy stores: the words are read again
+// by the gather that follows, from the MALL when they fit.
+__global__ __launch_bounds__(kBlock) void mrg_words_kernel(uint32_t* __restrict__ out,
+                                                           mrg::WordsArgs a) {
+    static_assert(kBlock == mrg::kLo, "one table row per lane");
+    __shared__ uint32_t base[6];
+    const int j = blockIdx.y;
+    if (threadIdx.x < 6) base[threadIdx.x] = mrg_entry_dot(kMrgJump.hi[blockIdx.x], threadIdx.x, a.y[j].w);
+    __syncthreads();
+    const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
+    const int64_t cols = a.count < mrg::kOrder ? a.count : mrg::kOrder;
+    if (s >= cols) return;
+    const int64_t q_end_s = (a.count - s + mrg::kOrder - 1) >> mrg::kOrderLog2;
+    const int64_t q = (int64_t)j * a.chunk;
+    const int64_t q_end = q + a.chunk < q_end_s ? q + a.chunk : q_end_s;
+    if (q >= q_end) return;
+    const uint32_t v[6] = {base[0], base[1], base[2], base[3], base[4], base[5]};
+    mrg::State st = mrg_apply_lo(threadIdx.x, v);
+    // block-uniform base pointer (positions advance it), the lane's subsequence as offset
+    uint32_t* o = out + (q << mrg::kOrderLog2) + (int64_t)blockIdx.x * kBlock;
+    const uint32_t lane = threadIdx.x;
+    const int64_t left = q_end - q;
+    int64_t i = 0;
+    for (; i + 3 <= left; i += 3, o += 3 * mrg::kOrder) {  // three steps: the state stays put
+        o[lane] = mrg::step<0>(st);
+        o[mrg::kOrder + lane] = mrg::step<1>(st);
+        o[2 * mrg::kOrder + lane] = mrg::step<2>(st);
+    }
+    if (i < left) o[lane] = mrg::step<0>(st);
+    if (i + 1 < left) o[mrg::kOrder + lane] = mrg::step<1>(st);
+}
 
 // One lane per hypothesis.  rand_list (4,n) uint32, pool_src / pool_tar (size,2) binary64
 // (Point2d), d_src / d_tar (8,n): get_rand_list's own statement order (x, y of r1..r4).
@@ -108,6 +170,212 @@ __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
             }
         }
     }
+}
+
+// The draws fused in too: the bits of mrg_words_kernel(4 n words) followed by
+// gather_solve_f64_kernel, with no (4,n) word rows in memory.
+//
+// Word h + k n (row k of hypothesis h) is position (h + k n) >> 17 of subsequence
+// (h + k n) & (2^17 - 1).  For the hypotheses h = h0 + q 2^17 of one residue class h0, row k
+// therefore walks ONE subsequence, s_k = (h0 + b_k) mod 2^17, at consecutive positions
+// q + a_k + carry_k (k n = a_k 2^17 + b_k, carry_k = h0 + b_k >= 2^17): one engine per
+// (class, row), stepped once per hypothesis.  A block owns C = B/4 consecutive classes at a
+// time (a group); lane (k, c) runs the engine of row k of class c (k is wave-uniform) and
+// writes 4 words per chunk into LDS, then lane (qq, c) solves hypothesis h0_c + (q0 + qq)
+// 2^17 from the 4 words of its class and position -- one hypothesis per lane per chunk, the
+// next chunk's words made in the same pass (double buffer, one barrier per chunk).  H
+// stores stay lane-consecutive in h.  Engine starts: with y[k][c] = A^(a_k + c) x0 from the
+// host and base_k = (g C + b_k) mod 2^17, class c of row k starts at J^c (J^base_k y[k][0]),
+// or at J^(c - w) y[k][1] past the wrap (c >= w = 2^17 - base_k), or at J^c (J^base_k y[k][1])
+// when g C + b_k itself wrapped.  J^base_k y[k][.] is made
+// once per group by 24 lanes (two table levels, through LDS, for a batch of the block's
+// groups at once); each lane then applies one table row J^c per component.
+// Block size: 1024 lanes (16 waves share one pool copy); RHO-GE and GPT-LU hold more than the
+// 128 VGPRs that allows beside the engine's binary64 state, so they run 512-lane blocks.
+template <int ALGO>
+constexpr int mrg_gather_block() { return ALGO == kGPT || ALGO == kGE ? 512 : 1024; }
+
+template <int ALGO>
+constexpr size_t mrg_words_lds() { return (size_t)2 * 4 * 4 * (mrg_gather_block<ALGO>() / 4) * 4; }
+
+constexpr int kMrgGroupBatch = 8;  // groups whose engine bases one pass makes
+constexpr size_t kMrgStaticLds = 2 * kMrgGroupBatch * 24 * 4;
+
+template <int ALGO, bool NORM, bool POOL_LDS>
+__global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64_kernel(
+    uint32_t size, uint64_t magic, const double2* __restrict__ pool_src,
+    const double2* __restrict__ pool_tar, double* __restrict__ H, int64_t n,
+    mrg::GatherArgs a) {
+    constexpr int kB = mrg_gather_block<ALGO>();
+    constexpr int kC = kB / 4;  // classes per group
+    constexpr int kQ = 4;       // positions per chunk
+    extern __shared__ __attribute__((aligned(16))) char dyn[];
+    uint32_t* words = reinterpret_cast<uint32_t*>(dyn);  // [2][4][kQ][kC]
+    double2* pool = reinterpret_cast<double2*>(dyn + mrg_words_lds<ALGO>());
+    if constexpr (POOL_LDS) {
+        for (uint32_t i = threadIdx.x; i < size; i += kB) {
+            pool[2 * i] = pool_src[i];
+            pool[2 * i + 1] = pool_tar[i];
+        }
+    }
+    __shared__ uint32_t base_u[kMrgGroupBatch][24], base_v[kMrgGroupBatch][24];
+    const int k = threadIdx.x / kC;  // engine row; also the solve's position in the chunk
+    const int c = threadIdx.x % kC;
+    const int64_t cols = n < mrg::kOrder ? n : mrg::kOrder;
+    const int64_t groups = (cols + kC - 1) / kC;
+    const int64_t stride = gridDim.x;
+    for (int64_t g0 = blockIdx.x; g0 < groups; g0 += stride * kMrgGroupBatch) {
+        // J^base_k y[k][0] of up to kMrgGroupBatch groups: lane (i, kk, t) makes element t
+        // of group i, row kk -- first through the table's low level, then the high one
+        const int bi = threadIdx.x / 24, br = threadIdx.x % 24, bk = br / 6, bt = br % 6;
+        const int64_t bg = g0 + bi * stride;
+        const bool bl = threadIdx.x < 24 * kMrgGroupBatch && bg < groups;
+        const int64_t braw = bg * kC + a.b[bl ? bk : 0];  // < 2^18
+        const int bcarry = braw >= mrg::kOrder;
+        const uint32_t bbase = (uint32_t)(braw & (mrg::kOrder - 1));
+        if (bl)
+            base_u[bi][br] = mrg_entry_dot(kMrgJump.lo[bbase & (mrg::kLo - 1)], bt, a.y[bk][bcarry].w);
+        __syncthreads();
+        if (bl)
+            base_v[bi][br] = mrg_entry_dot(kMrgJump.hi[bbase >> mrg::kLoBits], bt, &base_u[bi][bk * 6]);
+        __syncthreads();
+    for (int gi = 0; gi < kMrgGroupBatch; ++gi) {
+        const int64_t g = g0 + gi * stride;
+        if (g >= groups) break;
+        const int64_t h0 = g * kC + c;
+        mrg::State st;
+        {
+            // the group's first class already wrapped (g C + b_k >= 2^17): every class of the
+            // row is at position a_k + 1, and its base was made from y[k][1]
+            const int64_t raw = g * kC + a.b[k];
+            const uint32_t base = (uint32_t)(raw & (mrg::kOrder - 1));
+            const uint32_t w = (uint32_t)mrg::kOrder - base;  // classes from w on wrapped
+            if (raw >= mrg::kOrder || (uint32_t)c < w) {
+                const uint32_t* bv = base_v[gi] + k * 6;
+                const uint32_t v[6] = {bv[0], bv[1], bv[2], bv[3], bv[4], bv[5]};
+                st = mrg_apply_lo((uint32_t)c, v);
+            } else {
+                st = mrg_apply_lo((uint32_t)c - w, a.y[k][1].w);
+            }
+        }
+        // chunk m holds steps 4m .. 4m+3, in state slots (m + i) mod 3: one copy of the four
+        // steps per phase m mod 3 (a block-uniform branch), so no step moves the state
+        auto gen = [&](int buf, int phase) {
+            uint32_t* w = words + (buf * 4 + k) * kQ * kC + c;
+            auto four = [&](auto p) {
+                constexpr int P = decltype(p)::value;
+                w[0] = mrg::step<P % 3>(st);
+                w[kC] = mrg::step<(P + 1) % 3>(st);
+                w[2 * kC] = mrg::step<(P + 2) % 3>(st);
+                w[3 * kC] = mrg::step<P % 3>(st);
+            };
+            if (phase == 0) four(std::integral_constant<int, 0>());
+            else if (phase == 1) four(std::integral_constant<int, 1>());
+            else four(std::integral_constant<int, 2>());
+        };
+        // positions of the group's first class (the others have as many or one fewer)
+        const int64_t qn = (n - g * kC + mrg::kOrder - 1) >> mrg::kOrderLog2;
+        gen(0, 0);
+        __syncthreads();
+        int buf = 0, phase = 0;
+        for (int64_t q0 = 0; q0 < qn; q0 += kQ, buf ^= 1) {
+            phase = phase == 2 ? 0 : phase + 1;  // the phase of chunk q0 / 4 + 1
+            if (q0 + kQ < qn) gen(buf ^ 1, phase);
+            const int64_t h = h0 + ((q0 + k) << mrg::kOrderLog2);
+            if (h < n) {
+                double s[8], t[8], hh[9];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const uint32_t w = words[((buf * 4 + r) * kQ + k) * kC + c];
+                    const uint32_t ix = fastmod_u32(w, magic, size);
+                    double2 ps, pt;
+                    if constexpr (POOL_LDS) {
+                        ps = pool[2 * ix];
+                        pt = pool[2 * ix + 1];
+                    } else {
+                        ps = pool_src[ix];
+                        pt = pool_tar[ix];
+                    }
+                    s[2 * r] = ps.x; s[2 * r + 1] = ps.y;
+                    t[2 * r] = pt.x; t[2 * r + 1] = pt.y;
+                }
+                solve<ALGO, NORM>(s, t, hh);
+#pragma unroll
+                for (int r = 0; r < 9; ++r) __builtin_nontemporal_store(hh[r], H + h + r * n);
+            }
+            __syncthreads();
+        }
+    }
+    }
+}
+
+// ---- host launchers ----
+
+inline mrg::Packed mrg_seed_jump(uint64_t seed, uint64_t e) {  // A^e x0(seed)
+    mrg::Vec x1, x2;
+    mrg::seed_state(seed, x1, x2);
+    return mrg::pack(mrg::host_jump(kMrgPow.p1, 1, e, x1), mrg::host_jump(kMrgPow.p2, 2, e, x2));
+}
+
+// Positions per thread below which the standalone generator stops splitting subsequences
+// over more threads (each thread's start costs four 3x3 products mod m).
+constexpr int64_t kMrgMinChunk = 16;
+
+inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
+                            hipStream_t s) {
+    mrg::WordsArgs a{};
+    a.count = count;
+    const int64_t positions = (count + mrg::kOrder - 1) >> mrg::kOrderLog2;
+    int64_t chunks = positions / (min_chunk < 1 ? 1 : min_chunk);
+    chunks = chunks < 1 ? 1 : (chunks > mrg::kWordsMaxChunks ? mrg::kWordsMaxChunks : chunks);
+    a.chunk = (positions + chunks - 1) / chunks;
+    chunks = (positions + a.chunk - 1) / a.chunk;
+    mrg::Vec x1, x2;
+    mrg::seed_state(seed, x1, x2);
+    for (int64_t j = 0; j < chunks; ++j)
+        a.y[j] = mrg::pack(mrg::host_jump(kMrgPow.p1, 1, (uint64_t)(j * a.chunk), x1),
+                           mrg::host_jump(kMrgPow.p2, 2, (uint64_t)(j * a.chunk), x2));
+    const int64_t cols = count < mrg::kOrder ? count : mrg::kOrder;
+    const dim3 grid((unsigned)((cols + kBlock - 1) / kBlock), (unsigned)chunks);
+    return launch(mrg_words_kernel, grid, dim3(kBlock), 0, s, out, a);
+}
+
+// variant: -1 shipped (pool in LDS when it fits beside the draws buffer), 0 pool in global
+// memory
+template <int ALGO, bool NORM>
+inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32_t size,
+                                    uint64_t seed, double* H, int64_t n, hipStream_t s,
+                                    int variant = -1) {
+    constexpr int kB = mrg_gather_block<ALGO>();
+    constexpr size_t kLdsMax = 160 * 1024;
+    mrg::GatherArgs a{};
+    mrg::Vec x1, x2;
+    mrg::seed_state(seed, x1, x2);
+    for (int k = 0; k < 4; ++k) {
+        const uint64_t kn = (uint64_t)k * (uint64_t)n;
+        a.b[k] = (uint32_t)(kn & (uint64_t)(mrg::kOrder - 1));
+        const mrg::Vec y1 = mrg::host_jump(kMrgPow.p1, 1, kn >> mrg::kOrderLog2, x1);
+        const mrg::Vec y2 = mrg::host_jump(kMrgPow.p2, 2, kn >> mrg::kOrderLog2, x2);
+        a.y[k][0] = mrg::pack(y1, y2);
+        a.y[k][1] = mrg::pack(mrg::host_jump(kMrgPow.p1, 1, 1, y1),
+                              mrg::host_jump(kMrgPow.p2, 2, 1, y2));
+    }
+    const int64_t cols = n < mrg::kOrder ? n : mrg::kOrder;
+    const int64_t groups = (cols + kB / 4 - 1) / (kB / 4);
+    const uint64_t magic = fastmod_magic(size);
+    const size_t words = mrg_words_lds<ALGO>();
+    const bool pool_lds = variant != 0 && kMrgStaticLds + words + (size_t)size * 32 <= kLdsMax;
+    const size_t lds = pool_lds ? words + (size_t)size * 32 : words;
+    auto k = pool_lds ? mrg_gather_solve_f64_kernel<ALGO, NORM, true>
+                      : mrg_gather_solve_f64_kernel<ALGO, NORM, false>;
+    if (lds + kMrgStaticLds > kSampleLdsMax && !lds_opt_in(k, kMrgStaticLds))
+        return (int)hipErrorInvalidValue;
+    int64_t per_cu = (int64_t)(kLdsMax / (lds + kMrgStaticLds));
+    const int64_t max_per_cu = 2048 / kB;  // 32 waves per CU
+    per_cu = per_cu < 1 ? 1 : (per_cu > max_per_cu ? max_per_cu : per_cu);
+    const int64_t cap = per_cu * cu_count();
+    const unsigned grid = (unsigned)(groups < cap ? groups : cap);
+    return launch(k, dim3(grid), dim3(kB), lds, s, size, magic, ps, pt, H, n, a);
 }
 
 }  // namespace hg

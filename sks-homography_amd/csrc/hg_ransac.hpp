@@ -380,7 +380,8 @@ constexpr size_t kSampleLdsOptIn = 160 * 1024;   // gfx950: a workgroup may take
 // Allows `kernel` more than 64 KiB of dynamic LDS on the current device.  Remembered per
 // (device, kernel): the kernels of one signature share a function type, so a static per
 // template instantiation would opt in only the first of them.
-inline bool lds_opt_in(const void* kernel) {
+// static_lds: the kernel's own __shared__ bytes, which count against the same 160 KiB.
+inline bool lds_opt_in(const void* kernel, size_t static_lds = 0) {
     static std::mutex mu;
     static std::vector<std::pair<int, const void*>> done;
     int dev = 0;
@@ -389,14 +390,14 @@ inline bool lds_opt_in(const void* kernel) {
     for (const auto& e : done)
         if (e.first == dev && e.second == kernel) return true;
     if (hipFuncSetAttribute(kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)kSampleLdsOptIn) != hipSuccess)
+                            (int)(kSampleLdsOptIn - static_lds)) != hipSuccess)
         return false;
     done.emplace_back(dev, kernel);
     return true;
 }
 template <typename K>
-inline bool lds_opt_in(K kernel) {
-    return lds_opt_in(reinterpret_cast<const void*>(kernel));
+inline bool lds_opt_in(K kernel, size_t static_lds = 0) {
+    return lds_opt_in(reinterpret_cast<const void*>(kernel), static_lds);
 }
 
 // Variant sweep helper: the LDS-pool sampler with WPB waves per block (tools/kbench_sample.py).

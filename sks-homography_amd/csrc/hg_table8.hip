@@ -1,15 +1,13 @@
 // hg_table8.hip -- the reference's Table-8 sampling pipeline in its own formats
-// (GPU_Runtime Test.cu:1441-1451): MRG32K3A draws, get_rand_list (:52-78) and
+// (GPU_Runtime Test.cu:1443-1451): MRG32K3A draws, get_rand_list (:52-78) and
 // cal_Homo_* (:81-507), the last two also fused into one pass.  Kernels: hg_gather.hpp.
 //
 //   hg_rand_mrg32k3a_u32   curandCreateGenerator(MRG32K3A) + SetPseudoRandomGeneratorSeed
-//                          + curandGenerate (.cu:1441-1444), through rocRAND
+//                          + curandGenerate (.cu:1443-1446): hand-written (hg_mrg32k3a.hpp)
+//   hg_rand_gather_solve_f64  all three fused: words made in registers, H (9,n)
+//   hg_mrg32k3a_state      (host) the engine state of curand_init / rocrand_init
 //   hg_get_rand_list_f64   get_rand_list itself: (4,n) words -> (8,n) src / tar rows
 //   hg_gather_solve_f64    get_rand_list fused with cal_Homo_{ACA,SKS,GE,GPT}: (9,n) H
-#include <rocrand/rocrand.h>
-
-#include <mutex>
-
 #include "hg_gather.hpp"
 
 namespace {
@@ -50,31 +48,8 @@ int hg_rand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stre
     if (count < 0) return kInvalid;
     if (count == 0) return 0;
     if (!out || misaligned(out, 4)) return kInvalid;
-    // One generator per device, created on first use and kept (its state allocation is most
-    // of a fresh generator's cost); calls are serialised on it.  Re-seeding every call
-    // restarts the stream at offset 0, so each call's words are those of a fresh
-    // curandCreateGenerator + SetPseudoRandomGeneratorSeed + Generate (.cu:1441-1444).
-    constexpr int kMaxDevices = 64;
-    static std::mutex mu;
-    static rocrand_generator gens[kMaxDevices] = {};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return kInvalid;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!gens[dev] &&
-        rocrand_create_generator(&gens[dev], ROCRAND_RNG_PSEUDO_MRG32K3A) != ROCRAND_STATUS_SUCCESS) {
-        gens[dev] = nullptr;
-        return (int)hipErrorNotInitialized;
-    }
-    rocrand_generator g = gens[dev];
-    rocrand_status st = rocrand_set_stream(g, reinterpret_cast<hipStream_t>(stream));
-    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_seed(g, seed);
-    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_generate(g, out, (size_t)count);
-    // the shared generator's device state is rewritten by the next call (perhaps on another
-    // stream): wait for this call's kernels before releasing it (the call is synchronous,
-    // like curandGenerate's caller at .cu:1444-1448)
-    const hipError_t sync = hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream));
-    if (st != ROCRAND_STATUS_SUCCESS) return (int)hipErrorLaunchFailure;
-    return (int)sync;
+    return hg::launch_mrg_words(out, count, seed, hg::kMrgMinChunk,
+                                reinterpret_cast<hipStream_t>(stream));
 }
 
 int hg_get_rand_list_f64(const uint32_t* rand_list, uint32_t size, const double* pool_src,
@@ -118,6 +93,63 @@ int hg_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar
         default: HG_GS(hg::kGPT);
     }
 #undef HG_GS
+}
+
+int hg_mrg32k3a_state(uint64_t seed, uint64_t subsequence, uint64_t offset, uint32_t* state) {
+    if (!state) return kInvalid;
+    namespace m = hg::mrg;
+    m::Vec x1, x2;
+    m::seed_state(seed, x1, x2);
+    // (A^(2^76))^subsequence, then A^offset, by squaring
+    m::Mat j1 = m::pow2<1>(m::kStep1, 76), j2 = m::pow2<2>(m::kStep2, 76);
+    for (uint64_t e = subsequence; e; e >>= 1) {
+        if (e & 1) {
+            x1 = m::mat_vec<1>(j1, x1);
+            x2 = m::mat_vec<2>(j2, x2);
+        }
+        j1 = m::mat_mul<1>(j1, j1);
+        j2 = m::mat_mul<2>(j2, j2);
+    }
+    j1 = m::kStep1;
+    j2 = m::kStep2;
+    for (uint64_t e = offset; e; e >>= 1) {
+        if (e & 1) {
+            x1 = m::mat_vec<1>(j1, x1);
+            x2 = m::mat_vec<2>(j2, x2);
+        }
+        j1 = m::mat_mul<1>(j1, j1);
+        j2 = m::mat_mul<2>(j2, j2);
+    }
+    for (int k = 0; k < 3; ++k) {
+        state[k] = x1.v[k];
+        state[3 + k] = x2.v[k];
+    }
+    return 0;
+}
+
+int hg_rand_gather_solve_f64(int algo, const double* pool_src, const double* pool_tar,
+                             uint32_t size, uint64_t seed, double* H, int64_t n, int flags,
+                             void* stream) {
+    if (n < 0 || size == 0 || algo < HG_ALGO_ACA || algo > HG_ALGO_GPT ||
+        (flags & ~HG_FLAG_NORMALIZE) || n > (INT64_C(1) << 61))
+        return kInvalid;
+    if (n == 0) return 0;
+    if (!pool_src || !pool_tar || !H) return kInvalid;
+    if (misaligned(pool_src, 16) || misaligned(pool_tar, 16) || misaligned(H, 8)) return kInvalid;
+    const auto* ps = reinterpret_cast<const double2*>(pool_src);
+    const auto* pt = reinterpret_cast<const double2*>(pool_tar);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
+#define HG_RGS(A)                                                                          \
+    return norm ? hg::launch_rand_gather_solve<A, true>(ps, pt, size, seed, H, n, s)       \
+                : hg::launch_rand_gather_solve<A, false>(ps, pt, size, seed, H, n, s)
+    switch (algo) {
+        case HG_ALGO_ACA: HG_RGS(hg::kACA);
+        case HG_ALGO_SKS: HG_RGS(hg::kSKS);
+        case HG_ALGO_GE: HG_RGS(hg::kGE);
+        default: HG_RGS(hg::kGPT);
+    }
+#undef HG_RGS
 }
 
 }  // extern "C"

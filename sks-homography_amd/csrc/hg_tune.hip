@@ -2,6 +2,7 @@
 // declared in include/sks_homography_tune.h).  Every variant computes the same bits
 // as the shipped kernel; only the memory schedule differs.
 #include <hip/hip_runtime.h>
+#include <rocrand/rocrand.h>
 
 #include "hg_aos.hpp"
 #include "hg_gather.hpp"
@@ -770,4 +771,48 @@ int hg_tune_score(int variant, const float* H, int64_t n, const float* pool_src,
     return (int)hipGetLastError();
 }
 
+// ---- MRG32K3A (round 3) ----
+// rocRAND's own host API, the checker the hand-written generator is pinned against
+// (tests/test_gpu_mrg32k3a.py) and the timing it replaced (tools/kbench_mrg.py): a fresh
+// generator per call, as the reference harness creates one (GPU_Runtime Test.cu:1443-1446).
+// Synchronous.  Statuses: ROCRAND_STATUS_ALLOCATION_FAILED -> hipErrorOutOfMemory, any
+// other failure -> hipErrorLaunchFailure.
+int hg_tune_rocrand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream) {
+    if (count < 0 || (count > 0 && !out)) return (int)hipErrorInvalidValue;
+    if (count == 0) return 0;
+    rocrand_generator g = nullptr;
+    rocrand_status st = rocrand_create_generator(&g, ROCRAND_RNG_PSEUDO_MRG32K3A);
+    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_stream(g, reinterpret_cast<hipStream_t>(stream));
+    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_set_seed(g, seed);
+    if (st == ROCRAND_STATUS_SUCCESS) st = rocrand_generate(g, out, (size_t)count);
+    const hipError_t sync = hipStreamSynchronize(reinterpret_cast<hipStream_t>(stream));
+    if (g) rocrand_destroy_generator(g);
+    if (st == ROCRAND_STATUS_ALLOCATION_FAILED) return (int)hipErrorOutOfMemory;
+    if (st != ROCRAND_STATUS_SUCCESS) return (int)hipErrorLaunchFailure;
+    return (int)sync;
+}
+
+// The standalone generator with another split threshold (positions per thread).
+int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
+                      void* stream) {
+    if (count <= 0 || !out || min_chunk < 1) return (int)hipErrorInvalidValue;
+    return hg::launch_mrg_words(out, count, seed, min_chunk, reinterpret_cast<hipStream_t>(stream));
+}
+
+// Fused draws + gather + solve (unnormalised ACA / SKS): 0 = pool in global memory,
+// 1 = pool in LDS beside the draws buffer (shipped when it fits).
+int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
+                                  const double* pool_tar, uint32_t size, uint64_t seed, double* H,
+                                  int64_t n, void* stream) {
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 1)
+        return (int)hipErrorInvalidValue;
+    const auto* ps = reinterpret_cast<const double2*>(pool_src);
+    const auto* pt = reinterpret_cast<const double2*>(pool_tar);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int v = variant == 0 ? 0 : -1;
+    return algo == 0 ? hg::launch_rand_gather_solve<hg::kACA, false>(ps, pt, size, seed, H, n, s, v)
+                     : hg::launch_rand_gather_solve<hg::kSKS, false>(ps, pt, size, seed, H, n, s, v);
+}
+
 }  // extern "C"
+

@@ -8,6 +8,7 @@ pipeline, adds the scoring step it implies, and returns the best hypothesis.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import NamedTuple
 
 import torch
@@ -132,13 +133,14 @@ def score(H: torch.Tensor, pool_src: torch.Tensor, pool_tar: torch.Tensor,
     return counts
 
 
-# ---- the reference's Table-8 pipeline in its own formats (GPU_Runtime Test.cu:1441-1451) ----
+# ---- the reference's Table-8 pipeline in its own formats (GPU_Runtime Test.cu:1443-1451) ----
 _ALGO_IDS = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
 
 
 def rand_mrg32k3a(count: int, seed: int = 11, device="cuda") -> torch.Tensor:
-    """``count`` MRG32K3A words (rocRAND), as curandGenerate fills the reference's index list
-    (.cu:1441-1444, seed 11); uint32 values in an int32 tensor."""
+    """``count`` MRG32K3A words, as curandGenerate fills the reference's index list
+    (.cu:1443-1446, seed 11): the hand-written generator, rocRAND's host-API words;
+    uint32 values in an int32 tensor."""
     if count < 0:
         raise ValueError(f"count must be >= 0, got {count}")
     dev = _gpu_device(device)
@@ -195,6 +197,34 @@ def gather_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, rand_list: torc
         _lib.call("hg_gather_solve_f64", _ALGO_IDS[algo], ps.data_ptr(), pt.data_ptr(), ps.shape[0],
                   rl.data_ptr(), H.data_ptr(), n, 1 if normalize else 0, _stream(dev))
     return H
+
+
+def rand_gather_solve(pool_src: torch.Tensor, pool_tar: torch.Tensor, n: int, seed: int = 11,
+                      algo: str = "aca", normalize: bool = False) -> torch.Tensor:
+    """The whole Table-8 flow in one launch (.cu:1443-1451 + :52-78 + :81-507): (9,n) float64
+    SoA H, bit for bit ``gather_solve(pool_src, pool_tar, rand_mrg32k3a(4*n, seed).view(4, n),
+    algo, normalize)``, with the MRG32K3A words made in registers."""
+    dev = _require_device(pool_src, pool_tar)
+    if algo not in _ALGO_IDS:
+        raise ValueError(f"algo must be one of {sorted(_ALGO_IDS)}, got {algo!r}")
+    if n < 0:
+        raise ValueError(f"n must be >= 0, got {n}")
+    ps, pt = _point_pool(pool_src), _point_pool(pool_tar)
+    if ps.shape[0] != pt.shape[0] or ps.shape[0] == 0:
+        raise ValueError("pool_src and pool_tar must hold the same, non-zero number of points")
+    H = torch.empty((9, n), dtype=torch.float64, device=dev)
+    with _guard(dev):
+        _lib.call("hg_rand_gather_solve_f64", _ALGO_IDS[algo], ps.data_ptr(), pt.data_ptr(),
+                  ps.shape[0], seed, H.data_ptr(), n, 1 if normalize else 0, _stream(dev))
+    return H
+
+
+def mrg32k3a_state(seed: int, subsequence: int = 0, offset: int = 0) -> tuple:
+    """The engine state curand_init / rocrand_init(seed, subsequence, offset) sets up, as
+    (x1[n-3], x1[n-2], x1[n-1], x2[n-3], x2[n-2], x2[n-1]) (host computation)."""
+    st = (ctypes.c_uint32 * 6)()
+    _lib.call("hg_mrg32k3a_state", seed, subsequence, offset, st)
+    return tuple(st)
 
 
 class RansacResult(NamedTuple):

@@ -126,6 +126,13 @@ def test_other_entry_validation(pkg):
         assert lib.hg_gather_solve_f64(algo, None, None, 5, None, None, n, flags, None) == want
     assert lib.hg_gather_solve_f64(0, None, None, 0, None, None, 4, 0, None) == 1  # size 0
     assert lib.hg_gather_solve_f64(0, 16, 16, 5, 16, 4, 4, 0, None) == 1           # H unaligned
+    for algo, flags, n, want in ((4, 0, 4, 1), (-1, 0, 4, 1), (0, 2, 4, 1), (0, 0, -1, 1),
+                                 (3, 1, 0, 0), (0, 0, 4, 1), (0, 0, (1 << 61) + 1, 1)):
+        assert lib.hg_rand_gather_solve_f64(algo, None, None, 5, 11, None, n, flags, None) == want
+    assert lib.hg_rand_gather_solve_f64(0, None, None, 0, 11, None, 4, 0, None) == 1  # size 0
+    assert lib.hg_rand_gather_solve_f64(0, 16, 8, 5, 11, 16, 4, 0, None) == 1  # pool not 16-B
+    assert lib.hg_rand_gather_solve_f64(0, 16, 16, 5, 11, 4, 4, 0, None) == 1  # H unaligned
+    assert lib.hg_mrg32k3a_state(11, 0, 0, None) == 1                             # NULL state
     assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
                                                None) == 1
     assert lib.hg_solve_one_f32(0, None, None, None, 1, None) == 1               # NULL points

@@ -102,6 +102,37 @@ def test_other_launchers_ignore_pending_error(hip, pkg, dev, oracle):
     np.testing.assert_array_equal(out.cpu().numpy(), oracle.fill_uniform(1000, 11, 0))
 
 
+def test_table8_launchers_ignore_pending_error(hip, pkg, dev, orc):
+    """the Table-8 entry points too (the MRG32K3A draws, get_rand_list, the fused
+    gather + solve and the fused draws + gather + solve)."""
+    stream = torch.cuda.current_stream(dev).cuda_stream
+    lib = pkg.lib()
+    w = load_golden("cpp_wall.npz")
+    ps = torch.from_numpy(w["pool_src"].astype(np.float64)).to(dev)
+    pt = torch.from_numpy(w["pool_tar"].astype(np.float64)).to(dev)
+    n = 1000
+    rl = torch.empty((4, n), dtype=torch.int32, device=dev)
+    d_src = torch.empty((8, n), dtype=torch.float64, device=dev)
+    d_tar = torch.empty((8, n), dtype=torch.float64, device=dev)
+    H1 = torch.empty((9, n), dtype=torch.float64, device=dev)
+    H2 = torch.empty((9, n), dtype=torch.float64, device=dev)
+    torch.cuda.synchronize(dev)
+    _pend(hip)
+    assert lib.hg_rand_mrg32k3a_u32(rl.data_ptr(), 4 * n, 11, stream) == 0
+    assert lib.hg_get_rand_list_f64(rl.data_ptr(), ps.shape[0], ps.data_ptr(), pt.data_ptr(),
+                                    d_src.data_ptr(), d_tar.data_ptr(), n, stream) == 0
+    assert lib.hg_gather_solve_f64(0, ps.data_ptr(), pt.data_ptr(), ps.shape[0], rl.data_ptr(),
+                                   H1.data_ptr(), n, 0, stream) == 0
+    assert lib.hg_rand_gather_solve_f64(0, ps.data_ptr(), pt.data_ptr(), ps.shape[0], 11,
+                                        H2.data_ptr(), n, 0, stream) == 0
+    assert hip.hipPeekAtLastError() == HIP_ERROR_INVALID_DEVICE
+    hip.hipGetLastError()
+    torch.cuda.synchronize(dev)
+    assert _bits_equal(orc, H1.cpu().numpy(), H2.cpu().numpy())
+    assert _bits_equal(orc, H1.cpu().numpy(),
+                       pkg.solve("aca", d_src, d_tar, normalize=False, layout="soa").cpu().numpy())
+
+
 def test_host_pointer_calls_ignore_pending_error(hip, pkg, dev, orc):
     """sks::runKernel_ACA on host pointers and hg_solve_host_f32 on pageable memory probe
     their pointers first (hipPointerGetAttributes succeeds on unregistered memory on this
