@@ -319,7 +319,7 @@ inline mrg::Packed mrg_seed_jump(uint64_t seed, uint64_t e) {  // A^e x0(seed)
 
 // Positions per thread below which the standalone generator stops splitting subsequences
 // over more threads (each thread's start costs four 3x3 products mod m).
-constexpr int64_t kMrgMinChunk = 16;
+constexpr int64_t kMrgMinChunk = 64;
 
 inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
                             hipStream_t s) {

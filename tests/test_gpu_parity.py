@@ -67,6 +67,31 @@ def test_golden_aca_vanilla(orc, pkg, dev):
         _bits(orc, H, g[f"{tag}_vanilla"], f"ACA_vanilla {tag}")
 
 
+@pytest.mark.parametrize("tag", ["uniform", "wall", "edge"])
+def test_golden_aca_f64_unnormalised(orc, pkg, dev, tag):
+    """The cal_Homo_ACA contract (GPU_Runtime Test.cu:81-151: binary64, unnormalised) pinned by
+    reference output: ACA_vanilla's statements run on float64 CPU tensors
+    (tests/golden/torch_aca_f64.npz).  hg_aca_f64 in the reference GPU layout (SoA, flags 0),
+    in AoS, through ACA_vanilla on float64 tensors, and -- for the point-file subsets -- the
+    fused get_rand_list + cal_Homo_ACA fed the subsets' own indices, all bit for bit."""
+    g = load_golden("torch_aca_f64.npz")
+    src, tar = g[f"{tag}_src"].reshape(-1, 8), g[f"{tag}_tar"].reshape(-1, 8)
+    want = g[f"{tag}_H"].reshape(-1, 9)
+    s, t = _t(src, dev), _t(tar, dev)
+    _bits(orc, pkg.solve("aca", s.T.contiguous(), t.T.contiguous(), normalize=False,
+                         layout="soa").T, want, f"{tag} soa")
+    _bits(orc, pkg.solve("aca", s, t, normalize=False), want, f"{tag} aos")
+    B = src.shape[0]
+    _bits(orc, pkg.ACA_vanilla(B, _t(g[f"{tag}_src"], dev), _t(g[f"{tag}_tar"], dev)).reshape(B, 9),
+          want, f"{tag} ACA_vanilla f64")
+    if tag == "wall":
+        w = load_golden("cpp_wall.npz")
+        ps = _t(w["pool_src"].astype(np.float64), dev)
+        pt = _t(w["pool_tar"].astype(np.float64), dev)
+        words = _t(np.ascontiguousarray(g["wall_idx"].T).view(np.int32), dev)  # (4,n): idx < size
+        _bits(orc, pkg.gather_solve(ps, pt, words, "aca").T, want, "fused get_rand_list + ACA")
+
+
 @pytest.mark.parametrize("key", ["int_rect", "f_rect", "f_rect_div125"])
 @pytest.mark.parametrize("scalar_kind", ["device", "host"])
 def test_golden_tensor_aca_rect(orc, pkg, dev, key, scalar_kind):

@@ -70,6 +70,28 @@ def test_oracle_unnormalised_vs_reference_aca_vanilla(orc, oracle):
         _assert_bits(orc, got, g[f"{tag}_vanilla"].reshape(-1, 9), f"ACA_vanilla {tag}")
 
 
+@pytest.mark.parametrize("tag", ["uniform", "wall", "edge"])
+def test_oracle_unnormalised_f64_vs_reference_aca_vanilla_f64(orc, oracle, tag):
+    """Unnormalised binary64 ACA -- cal_Homo_ACA's contract (GPU_Runtime Test.cu:81-151) --
+    pinned by reference output: ACA_vanilla's own statements executed on float64 CPU tensors
+    (tests/golden/torch_aca_f64.npz).  The same fixture normalised the C++ way
+    (ACA_SKS.cpp:94-98) equals the compiled reference's runKernel_ACA_double, so two
+    reference artifacts agree on these bits."""
+    g = load_golden("torch_aca_f64.npz")
+    src, tar = g[f"{tag}_src"].reshape(-1, 8), g[f"{tag}_tar"].reshape(-1, 8)
+    want = g[f"{tag}_H"].reshape(-1, 9)
+    _assert_bits(orc, oracle.solve("aca", src, tar, normalize=False), want, f"f64 {tag}")
+    _assert_bits(orc, oracle.solve("aca", np.ascontiguousarray(src.T), np.ascontiguousarray(tar.T),
+                                   normalize=False, layout="soa").T, want, f"f64 {tag} soa")
+    if orc.RefOracle.available():
+        norm = want.copy()
+        with np.errstate(divide="ignore", invalid="ignore"):
+            r = 1.0 / norm[:, 8]
+            norm[:, :8] *= r[:, None]
+        norm[:, 8] = 1.0
+        _assert_bits(orc, norm, orc.RefOracle().solve("aca", src, tar), f"f64 {tag} vs C++")
+
+
 @pytest.mark.parametrize("key,scale,div", [("int_rect", None, None), ("f_rect", 128.0, 1.0),
                                            ("f_rect_div125", 50.0, 1.25)])
 def test_oracle_vs_reference_tensor_aca_rect(orc, oracle, key, scale, div):

@@ -327,8 +327,49 @@ def torch_special() -> str:
             (torch.__version__, torch.backends.cpu.get_cpu_capability()))
 
 
+def torch_aca_f64() -> str:
+    """ACA_vanilla's own statements (Modules_Runtime_Test.py:322-382) executed on float64 CPU
+    tensors -- binary64 ACA without normalisation, the contract of the reference GPU kernel
+    cal_Homo_ACA (GPU_Runtime Test.cu:81-151).  The statements allocate H with torch.ones
+    (default dtype), so torch's default dtype is float64 while they run; every other tensor
+    follows the float64 inputs.  Inputs: uniform quads, 4-subsets of the reference's point
+    file (Point2f read as the harness reads it, widened to Point2d as .cu:1414-1416 does) and
+    the edge set.  Writes tests/golden/torch_aca_f64.npz; returns its manifest line."""
+    rng = np.random.default_rng(64)
+    n = 1024
+    uni_s = rng.uniform(-512, 512, (n, 4, 2))
+    uni_t = rng.uniform(-512, 512, (n, 4, 2))
+    ws, wt, widx = wall_problems(n, 64)
+    es, et = edge_problems()
+    out = {"wall_idx": widx}
+    prev = torch.get_default_dtype()
+    torch.set_default_dtype(torch.float64)
+    try:
+        for tag, src, tar in (("uniform", uni_s, uni_t),
+                              ("wall", ws.astype(np.float64).reshape(n, 4, 2),
+                               wt.astype(np.float64).reshape(n, 4, 2)),
+                              ("edge", es.astype(np.float64).reshape(-1, 4, 2),
+                               et.astype(np.float64).reshape(-1, 4, 2))):
+            H = run_ref_statements("ACA_vanilla", bs=src.shape[0], src=torch.from_numpy(src),
+                                   tar=torch.from_numpy(tar))["H"]
+            assert H.dtype == torch.float64
+            out[f"{tag}_src"], out[f"{tag}_tar"] = src, tar
+            out[f"{tag}_H"] = H.numpy().copy()
+    finally:
+        torch.set_default_dtype(prev)
+    np.savez_compressed(os.path.join(OUT, "torch_aca_f64.npz"), **out)
+    return ("torch_aca_f64.npz: ACA_vanilla statements of the reference on float64 CPU torch %s "
+            "(unnormalised binary64 ACA, the cal_Homo_ACA contract): 1024 uniform quads, 1024 "
+            "4-subsets of orig_pts_wall.txt, %d edge cases" % (torch.__version__, len(es)))
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["--torch-special"]:  # this fixture alone, appended to the manifest
+    if sys.argv[1:] == ["--torch-f64"]:  # this fixture alone, appended to the manifest
+        line = torch_aca_f64()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    elif sys.argv[1:] == ["--torch-special"]:  # this fixture alone, appended to the manifest
         line = torch_special()
         with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
             f.write("- " + line + "\n")
