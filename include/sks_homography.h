@@ -106,6 +106,29 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
                                     void* stream);
 
+/* TensorACA with scale / div broadcast the way the reference composition broadcasts them
+ * (Modules_Runtime_Test.py:301-302: torch.mul(div, X) and scale * h_temp, X and h_temp
+ * (B,3,1)): any shape broadcastable to (B,3,1) -- one value, one per problem ((B,1,1)),
+ * one per row ((3,1)), one per (problem, row) ((B,3,1)).  Value (b, r) is
+ * scale[b * scale_sb + r * scale_sr] (element strides; 0 along a broadcast dimension), the
+ * same for div.  Same arithmetic and bits as hg_tensor_aca_rect_f32 where the values agree.
+ * One lane per problem (the batch-uniform entry points above keep the LDS-staged kernel). */
+int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, int64_t B,
+                                 const float* scale, int64_t scale_sb, int64_t scale_sr,
+                                 const float* div, int64_t div_sb, int64_t div_sr, void* stream);
+
+/* Its backward: grad_tar (B,3,4), grad_src (B,3,4) when non-NULL, and per parameter, when
+ * its pointer is non-NULL, either each row's share of dL/dparam(b, r) ((3,B), row r at
+ * [r * B], when *_rows != 0) or each problem's three-row sum ((B), the per-problem partial
+ * of hg_tensor_aca_rect_backward_f32).  The caller sums them over the parameter's broadcast
+ * dimensions (hg_sum_rows_f32). */
+int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, int64_t scale_sb,
+                                          int64_t scale_sr, const float* div, int64_t div_sb,
+                                          int64_t div_sr, float* grad_src, float* grad_tar,
+                                          float* grad_scale, int scale_rows, float* grad_div,
+                                          int div_rows, void* stream);
+
 /* Compact TensorACA for deep-homography nets: the source is the
  * axis-aligned width x height rectangle with top-left corner (B,2) -- getInput's shape,
  * Modules_Runtime_Test.py:9-16 -- and the target is source + offsets (B,4,2), the

@@ -101,6 +101,20 @@ int hg_tune_gather_solve_f64(int variant, int algo, const double* pool_src, cons
                              uint32_t size, const uint32_t* rand_list, double* H, int64_t n,
                              void* stream);
 
+/* MRG32K3A (round 3).  rocRAND's own host API -- a fresh generator per call, as the reference
+ * harness creates one (GPU_Runtime Test.cu:1443-1446) -- the checker the hand-written
+ * generator is pinned against; synchronous.  ROCRAND_STATUS_ALLOCATION_FAILED ->
+ * hipErrorOutOfMemory, any other failure -> hipErrorLaunchFailure. */
+int hg_tune_rocrand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, void* stream);
+/* hg_rand_mrg32k3a_u32 with another split threshold (positions per thread). */
+int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
+                      void* stream);
+/* Fused draws + gather + solve, unnormalised ACA (0) / SKS (1): variant 0 pool in global
+ * memory, 1 pool in LDS beside the draws buffers (the shipped form when it fits). */
+int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
+                                  const double* pool_tar, uint32_t size, uint64_t seed, double* H,
+                                  int64_t n, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -206,31 +206,41 @@ DEFINE_BATCH(oracle_sks_f64, double, sks_one_f64, normalize_f64)
  *   H[r][0]  = tar[r][1] * c0 - b[r]
  *   H[r][1]  = div * (tar[r][2] * c1 - b[r])
  *   H[r][2]  = (scale * b[r] - src[0][0] * H[r][0]) - src[1][0] * H[r][1]   */
+/* One problem with per-row scale / div: the reference composition broadcasts them against
+ * the (B,3,1) columns (.py:301-302), so row r of H takes sc[r], dv[r]. */
+static void rect_one(const float* s, const float* t, float* h, const float* sc, const float* dv) {
+    float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4]; /* d[1] */
+    float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0]; /* d[0] */
+    float c0 = fmaf(ay, bz, -(az * by));
+    float c1 = fmaf(az, bx, -(ax * bz));
+    float c2 = fmaf(ax, by, -(ay * bx));
+    float S = ((c0 + c1) + c2) + 0.f;
+    float mx = s[0], my = s[4];
+    for (int r = 0; r < 3; ++r) {
+        float br = S * t[4 * r + 0];
+        float h0 = t[4 * r + 1] * c0 - br;
+        float h1 = dv[r] * (t[4 * r + 2] * c1 - br);
+        float sb = sc[r] * br;
+        float m0 = mx * h0;
+        float m1 = my * h1;
+        h[3 * r + 0] = h0;
+        h[3 * r + 1] = h1;
+        h[3 * r + 2] = (sb - m0) - m1;
+    }
+}
+
 int oracle_tensor_aca_rect_f32(const float* src, const float* tar, float* H, int64_t B,
                                float scale, float div) {
-    for (int64_t i = 0; i < B; ++i) {
-        const float* s = src + i * 12;
-        const float* t = tar + i * 12;
-        float* h = H + i * 9;
-        float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4]; /* d[1] */
-        float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0]; /* d[0] */
-        float c0 = fmaf(ay, bz, -(az * by));
-        float c1 = fmaf(az, bx, -(ax * bz));
-        float c2 = fmaf(ax, by, -(ay * bx));
-        float S = ((c0 + c1) + c2) + 0.f;
-        float mx = s[0], my = s[4];
-        for (int r = 0; r < 3; ++r) {
-            float br = S * t[4 * r + 0];
-            float h0 = t[4 * r + 1] * c0 - br;
-            float h1 = div * (t[4 * r + 2] * c1 - br);
-            float sb = scale * br;
-            float m0 = mx * h0;
-            float m1 = my * h1;
-            h[3 * r + 0] = h0;
-            h[3 * r + 1] = h1;
-            h[3 * r + 2] = (sb - m0) - m1;
-        }
-    }
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
+    for (int64_t i = 0; i < B; ++i) rect_one(src + i * 12, tar + i * 12, H + i * 9, sc, dv);
+    return 0;
+}
+
+/* scale / div given per (problem, row), expanded to (B,3) (the caller broadcasts). */
+int oracle_tensor_aca_rect_rows_f32(const float* src, const float* tar, float* H, int64_t B,
+                                    const float* scale, const float* div) {
+    for (int64_t i = 0; i < B; ++i)
+        rect_one(src + i * 12, tar + i * 12, H + i * 9, scale + i * 3, div + i * 3);
     return 0;
 }
 
@@ -310,58 +320,77 @@ double oracle_time_f32(int algo, const float* src, const float* tar, float* H, i
  * dL/dH -- the gradient ATen autograd produces for .py:294-302,
  * restated in the product kernel's fixed evaluation order (every op rounded on its
  * own except the forward's cross-product FMAs).  gsd: (B,2) per-problem partials. */
+static void rect_grad_one(const float* s, const float* t, const float* g, const float* sc,
+                          const float* dv, float* gs, float* gt, float* gsr, float* gdr,
+                          float* gsc_sum, float* gdv_sum) {
+    const float mx = s[0], my = s[4];
+    float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4];
+    float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0];
+    float c0 = fmaf(ay, bz, -(az * by));
+    float c1 = fmaf(az, bx, -(ax * bz));
+    float c2 = fmaf(ax, by, -(ay * bx));
+    float S = ((c0 + c1) + c2) + 0.f;
+    float gc0 = 0.f, gc1 = 0.f, gS = 0.f, gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
+    for (int r = 0; r < 3; ++r) {
+        float br = S * t[4 * r];
+        float h0 = t[4 * r + 1] * c0 - br;
+        float x = t[4 * r + 2] * c1 - br;
+        float h1 = dv[r] * x;
+        float g2 = g[3 * r + 2];
+        float gh0 = g[3 * r + 0] - mx * g2;
+        float gh1 = g[3 * r + 1] - my * g2;
+        gmx = gmx - g2 * h0;
+        gmy = gmy - g2 * h1;
+        gsr[r] = g2 * br;
+        gsc = gsc + gsr[r];
+        float gx = dv[r] * gh1;
+        gdr[r] = gh1 * x;
+        gdv = gdv + gdr[r];
+        float gb = (sc[r] * g2 - gh0) - gx;
+        gt[4 * r + 0] = gb * S;
+        gt[4 * r + 1] = gh0 * c0;
+        gt[4 * r + 2] = gx * c1;
+        gt[4 * r + 3] = 0.f;
+        gc0 = gc0 + gh0 * t[4 * r + 1];
+        gc1 = gc1 + gx * t[4 * r + 2];
+        gS = gS + gb * t[4 * r];
+    }
+    gc0 = gc0 + gS;
+    gc1 = gc1 + gS;
+    float gc2 = gS;
+    float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
+    float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
+    gt[5] = gt[5] + gax; gt[6] = gt[6] + gay; gt[7] = gt[7] + gaz;
+    gt[4] = gt[4] - ((gax + gay) + gaz);
+    gt[1] = gt[1] + gbx; gt[2] = gt[2] + gby; gt[3] = gt[3] + gbz;
+    gt[0] = gt[0] - ((gbx + gby) + gbz);
+    for (int k = 0; k < 12; ++k) gs[k] = 0.f;
+    gs[0] = gmx;
+    gs[4] = gmy;
+    *gsc_sum = gsc;
+    *gdv_sum = gdv;
+}
+
 int oracle_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* gH,
                                         int64_t B, float scale, float div, float* gsrc,
                                         float* gtar, float* gsd) {
-    for (int64_t i = 0; i < B; ++i) {
-        const float* t = tar + i * 12;
-        const float* g = gH + i * 9;
-        float* gt = gtar + i * 12;
-        const float mx = src[i * 12 + 0], my = src[i * 12 + 4];
-        float ax = t[5] - t[4], ay = t[6] - t[4], az = t[7] - t[4];
-        float bx = t[1] - t[0], by = t[2] - t[0], bz = t[3] - t[0];
-        float c0 = fmaf(ay, bz, -(az * by));
-        float c1 = fmaf(az, bx, -(ax * bz));
-        float c2 = fmaf(ax, by, -(ay * bx));
-        float S = ((c0 + c1) + c2) + 0.f;
-        float gc0 = 0.f, gc1 = 0.f, gS = 0.f, gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
-        for (int r = 0; r < 3; ++r) {
-            float br = S * t[4 * r];
-            float h0 = t[4 * r + 1] * c0 - br;
-            float x = t[4 * r + 2] * c1 - br;
-            float h1 = div * x;
-            float g2 = g[3 * r + 2];
-            float gh0 = g[3 * r + 0] - mx * g2;
-            float gh1 = g[3 * r + 1] - my * g2;
-            gmx = gmx - g2 * h0;
-            gmy = gmy - g2 * h1;
-            gsc = gsc + g2 * br;
-            float gx = div * gh1;
-            gdv = gdv + gh1 * x;
-            float gb = (scale * g2 - gh0) - gx;
-            gt[4 * r + 0] = gb * S;
-            gt[4 * r + 1] = gh0 * c0;
-            gt[4 * r + 2] = gx * c1;
-            gt[4 * r + 3] = 0.f;
-            gc0 = gc0 + gh0 * t[4 * r + 1];
-            gc1 = gc1 + gx * t[4 * r + 2];
-            gS = gS + gb * t[4 * r];
-        }
-        gc0 = gc0 + gS;
-        gc1 = gc1 + gS;
-        float gc2 = gS;
-        float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
-        float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
-        gt[5] = gt[5] + gax; gt[6] = gt[6] + gay; gt[7] = gt[7] + gaz;
-        gt[4] = gt[4] - ((gax + gay) + gaz);
-        gt[1] = gt[1] + gbx; gt[2] = gt[2] + gby; gt[3] = gt[3] + gbz;
-        gt[0] = gt[0] - ((gbx + gby) + gbz);
-        for (int k = 0; k < 12; ++k) gsrc[i * 12 + k] = 0.f;
-        gsrc[i * 12 + 0] = gmx;
-        gsrc[i * 12 + 4] = gmy;
-        gsd[i * 2 + 0] = gsc;
-        gsd[i * 2 + 1] = gdv;
-    }
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
+    float gsr[3], gdr[3];
+    for (int64_t i = 0; i < B; ++i)
+        rect_grad_one(src + i * 12, tar + i * 12, gH + i * 9, sc, dv, gsrc + i * 12, gtar + i * 12,
+                      gsr, gdr, gsd + i * 2, gsd + i * 2 + 1);
+    return 0;
+}
+
+/* Per-(problem, row) scale / div (B,3); writes each row's share of dL/dscale, dL/ddiv
+ * (gsr, gdr: (B,3)) and each problem's three-row sums (gss, gds: (B)). */
+int oracle_tensor_aca_rect_rows_backward_f32(const float* src, const float* tar, const float* gH,
+                                             int64_t B, const float* scale, const float* div,
+                                             float* gsrc, float* gtar, float* gsr, float* gdr,
+                                             float* gss, float* gds) {
+    for (int64_t i = 0; i < B; ++i)
+        rect_grad_one(src + i * 12, tar + i * 12, gH + i * 9, scale + i * 3, div + i * 3,
+                      gsrc + i * 12, gtar + i * 12, gsr + i * 3, gdr + i * 3, gss + i, gds + i);
     return 0;
 }
 

@@ -70,6 +70,12 @@ class Oracle:
                                                             ctypes.c_float, ctypes.c_float,
                                                             _f32p, _f32p, _f32p]
         lib.oracle_tensor_aca_rect_backward_f32.restype = ctypes.c_int
+        lib.oracle_tensor_aca_rect_rows_f32.argtypes = [_f32p, _f32p, _f32p, _i64, _f32p, _f32p]
+        lib.oracle_tensor_aca_rect_rows_f32.restype = ctypes.c_int
+        lib.oracle_tensor_aca_rect_rows_backward_f32.argtypes = [_f32p, _f32p, _f32p, _i64, _f32p,
+                                                                 _f32p, _f32p, _f32p, _f32p, _f32p,
+                                                                 _f32p, _f32p]
+        lib.oracle_tensor_aca_rect_rows_backward_f32.restype = ctypes.c_int
         lib.oracle_fill_bits_u32.argtypes = [ctypes.c_void_p, _i64, ctypes.c_uint64, ctypes.c_uint64]
         lib.oracle_ransac_score_f32.argtypes = [_f32p, _i64, _f32p, _f32p, ctypes.c_uint32,
                                                 ctypes.c_float, ctypes.c_void_p]
@@ -103,6 +109,44 @@ class Oracle:
         self.lib.oracle_tensor_aca_rect_f32(_ptr(src, _f32p), _ptr(tar, _f32p), _ptr(H, _f32p),
                                             B, float(np.float32(scale)), float(np.float32(div)))
         return H
+
+    @staticmethod
+    def _rows(x, B):
+        """scale / div (any shape broadcastable to (B,3,1), leading size-1 dimensions beyond
+        three dropped as the reference's column assignment drops them) as (B,3) float32."""
+        a = np.asarray(x, np.float32)
+        while a.ndim > 3 and a.shape[0] == 1:
+            a = a[0]
+        return np.ascontiguousarray(np.broadcast_to(a, (B, 3, 1)).reshape(B, 3))
+
+    def tensor_aca_rect_rows(self, src, tar, scale, div) -> np.ndarray:
+        """TensorACA with scale / div broadcast against the (B,3,1) columns (.py:301-302)."""
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tar = np.ascontiguousarray(tar, dtype=np.float32)
+        B = tar.shape[0]
+        sc, dv = self._rows(scale, B), self._rows(div, B)
+        H = np.empty((B, 3, 3), dtype=np.float32)
+        self.lib.oracle_tensor_aca_rect_rows_f32(_ptr(src, _f32p), _ptr(tar, _f32p),
+                                                 _ptr(H, _f32p), B, _ptr(sc, _f32p),
+                                                 _ptr(dv, _f32p))
+        return H
+
+    def tensor_aca_rect_rows_backward(self, src, tar, gH, scale, div):
+        """(grad_src, grad_tar, dscale per (problem, row) (B,3), ddiv (B,3), dscale per
+        problem (B) as three-row sums, ddiv (B))."""
+        src = np.ascontiguousarray(src, dtype=np.float32)
+        tar = np.ascontiguousarray(tar, dtype=np.float32)
+        gH = np.ascontiguousarray(gH, dtype=np.float32)
+        B = tar.shape[0]
+        sc, dv = self._rows(scale, B), self._rows(div, B)
+        gs, gt = np.empty((B, 3, 4), np.float32), np.empty((B, 3, 4), np.float32)
+        gsr, gdr = np.empty((B, 3), np.float32), np.empty((B, 3), np.float32)
+        gss, gds = np.empty(B, np.float32), np.empty(B, np.float32)
+        self.lib.oracle_tensor_aca_rect_rows_backward_f32(
+            _ptr(src, _f32p), _ptr(tar, _f32p), _ptr(gH, _f32p), B, _ptr(sc, _f32p),
+            _ptr(dv, _f32p), _ptr(gs, _f32p), _ptr(gt, _f32p), _ptr(gsr, _f32p), _ptr(gdr, _f32p),
+            _ptr(gss, _f32p), _ptr(gds, _f32p))
+        return gs, gt, gsr, gdr, gss, gds
 
     def tensor_aca_rect_backward(self, src, tar, gH, scale: float, div: float):
         """Returns (grad_src (B,3,4), grad_tar (B,3,4), per-problem (B,2) [dscale, ddiv])."""

@@ -35,6 +35,10 @@ SIGNATURES = {
     "hg_tensor_aca_rect_f32_hostscalar": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
                                            _vp], _int),
     "hg_tensor_aca_rect_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
+    "hg_tensor_aca_rect_bcast_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
+                                     _int),
+    "hg_tensor_aca_rect_bcast_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,
+                                               _i64, _vp, _vp, _vp, _int, _vp, _int, _vp], _int),
     "hg_tensor_aca_offsets_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
                                   _int),
     "hg_tensor_aca_offsets_backward_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,

@@ -566,6 +566,32 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
 #undef HG_RECT_BWD
 }
 
+int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, int64_t B,
+                                 const float* scale, int64_t scale_sb, int64_t scale_sr,
+                                 const float* div, int64_t div_sb, int64_t div_sr, void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !H || !scale || !div) return hg::kErrInvalid;
+    const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
+    return hg::launch(hg::tensor_aca_rect_bcast_kernel, hg::generic_grid(B), hg::kBlock, 0,
+                      reinterpret_cast<hipStream_t>(stream), src, tar, H, B, a);
+}
+
+int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, int64_t scale_sb,
+                                          int64_t scale_sr, const float* div, int64_t div_sb,
+                                          int64_t div_sr, float* grad_src, float* grad_tar,
+                                          float* grad_scale, int scale_rows, float* grad_div,
+                                          int div_rows, void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
+    const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
+    return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel, hg::generic_grid(B), hg::kBlock,
+                      0, reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, B, a, grad_src,
+                      grad_tar, grad_scale, scale_rows ? 1 : 0, grad_div, div_rows ? 1 : 0);
+}
+
 int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,
                               float width, float height, void* stream) {
     if (B < 0) return hg::kErrInvalid;

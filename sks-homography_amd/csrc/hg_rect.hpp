@@ -110,6 +110,86 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
 }
 
 // ---------------------------------------------------------------------------
+// TensorACA rect with scale / div broadcast as the reference composition broadcasts them
+// (.py:301-302: torch.mul(div, X) and scale * h_temp against (B,3,1) columns): value (b, r)
+// of each is p[b * sb + r * sr], element strides, 0 along a broadcast dimension -- a (B,1,1)
+// tensor gives one value per problem, (3,1) one per row, (B,3,1) one per (problem, row).
+// One lane per problem, grid-stride; the arithmetic of tensor_aca_rect_solve_rows.
+struct RectBcast {
+    const float* scale;
+    int64_t ssb, ssr;
+    const float* div;
+    int64_t dsb, dsr;
+};
+
+__device__ __forceinline__ void rect_bcast_load(const RectBcast& a, int64_t p, float (&sc)[3],
+                                                float (&dv)[3]) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        sc[r] = a.scale[p * a.ssb + r * a.ssr];
+        dv[r] = a.div[p * a.dsb + r * a.dsr];
+    }
+}
+
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H, int64_t B,
+    RectBcast a) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float tr[12], sc[3], dv[3], h[9];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+        rect_bcast_load(a, p, sc, dv);
+        tensor_aca_rect_solve_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[k];
+    }
+}
+
+// Its backward: dL/dtar, optionally dL/dsrc, and per parameter either each row's share
+// ((3,B): gs[r * B + p]) or the problem's three-row sum ((B): gs[p], the uniform kernels'
+// per-problem partial, ((0 + t0) + t1) + t2); the caller reduces them to the parameter's shape.
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_backward_kernel(
+    const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
+    int64_t B, RectBcast a, float* __restrict__ gsrc, float* __restrict__ gtar,
+    float* __restrict__ gsc, int sc_rows, float* __restrict__ gdv, int dv_rows) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        float tr[12], g[9], gt[12], sc[3], dv[3], gsr[3], gdr[3];
+#pragma unroll
+        for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        rect_bcast_load(a, p, sc, dv);
+        float gmx, gmy, gscale, gdiv;
+        tensor_aca_rect_grad_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, g, gt, gmx, gmy,
+                                  gscale, gdiv, gsr, gdr);
+#pragma unroll
+        for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
+        if (gsrc) {
+#pragma unroll
+            for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
+        }
+        if (gsc) {
+            if (sc_rows) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) gsc[r * B + p] = gsr[r];
+            } else {
+                gsc[p] = gscale;
+            }
+        }
+        if (gdv) {
+            if (dv_rows) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) gdv[r * B + p] = gdr[r];
+            } else {
+                gdv[p] = gdiv;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Compact TensorACA: corner (B,2) + offsets (B,4,2) -> H (B,3,3) = 8 + 32 + 36 B per
 // problem instead of the (B,3,4) tensors' 48 + 48 + 36.  Full tiles: both slabs by
 // LDS-DMA (P = 1: 512 B of corners + 2 KiB of offsets per wave), staged 16-B H stores.

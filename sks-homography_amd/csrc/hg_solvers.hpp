@@ -365,9 +365,13 @@ __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9
 // every other op rounds on its own.  tr = (3,4) target tensor rows {x, y, w} x cols {M, N, P, Q}.
 // SQUARE: the square specialisation of ACA_rect.m:28 (ratio 1, 44 FLOPs) -- drops the
 // multiply by div, which is exact when div == 1, so the bits are those of the general form.
+// Row forms: scale and div per row r of H -- the reference composition broadcasts them
+// against the (B,3,1) columns (.py:301-302), so a (B,1,1) tensor gives per-problem values
+// and a (B,3,1) one per-row values; the batch-uniform forms below pass one value thrice.
 template <bool SQUARE = false>
-__device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], float mx, float my,
-                                                      float scale, float div, float (&h)[9]) {
+__device__ __forceinline__ void tensor_aca_rect_solve_rows(const float (&tr)[12], float mx,
+                                                           float my, const float (&scale)[3],
+                                                           const float (&div)[3], float (&h)[9]) {
     const float ax = tr[5] - tr[4], ay = tr[6] - tr[4], az = tr[7] - tr[4];  // d[1]: MN, MP, MQ (y)
     const float bx = tr[1] - tr[0], by = tr[2] - tr[0], bz = tr[3] - tr[0];  // d[0]: MN, MP, MQ (x)
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
@@ -378,11 +382,18 @@ __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], flo
     for (int r = 0; r < 3; ++r) {
         const float b = sum * tr[4 * r];
         const float h0 = tr[4 * r + 1] * c0 - b;
-        const float h1 = SQUARE ? tr[4 * r + 2] * c1 - b : div * (tr[4 * r + 2] * c1 - b);
+        const float h1 = SQUARE ? tr[4 * r + 2] * c1 - b : div[r] * (tr[4 * r + 2] * c1 - b);
         h[3 * r + 0] = h0;
         h[3 * r + 1] = h1;
-        h[3 * r + 2] = (scale * b - mx * h0) - my * h1;
+        h[3 * r + 2] = (scale[r] * b - mx * h0) - my * h1;
     }
+}
+
+template <bool SQUARE = false>
+__device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], float mx, float my,
+                                                      float scale, float div, float (&h)[9]) {
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
+    tensor_aca_rect_solve_rows<SQUARE>(tr, mx, my, sc, dv, h);
 }
 
 // Compact deep-homography form: the source is the axis-aligned
@@ -410,10 +421,12 @@ __device__ __forceinline__ void rect_target_from_offsets(float mx, float my, flo
 // In: the forward's inputs and g = dL/dH (3x3).  Out: gt = dL/dtar (3,4), gmx/gmy =
 // dL/d src[0][0], src[1][0], gscale / gdiv = this problem's share of dL/dscale,
 // dL/ddiv.  Fixed evaluation order (restated op for op in oracle/hg_oracle.c).
-__device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,
-                                                     float scale, float div, const float (&g)[9],
-                                                     float (&gt)[12], float& gmx, float& gmy,
-                                                     float& gscale, float& gdiv) {
+// Row form: per-row scale / div (as tensor_aca_rect_solve_rows), and each row's own share of
+// dL/dscale[r], dL/ddiv[r] in gsr / gdr beside the per-problem sums gscale / gdiv.
+__device__ __forceinline__ void tensor_aca_rect_grad_rows(
+    const float (&tr)[12], float mx, float my, const float (&scale)[3], const float (&div)[3],
+    const float (&g)[9], float (&gt)[12], float& gmx, float& gmy, float& gscale, float& gdiv,
+    float (&gsr)[3], float (&gdr)[3]) {
     const float ax = tr[5] - tr[4], ay = tr[6] - tr[4], az = tr[7] - tr[4];
     const float bx = tr[1] - tr[0], by = tr[2] - tr[0], bz = tr[3] - tr[0];
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
@@ -427,16 +440,18 @@ __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], floa
         const float b = sum * tr[4 * r];
         const float h0 = tr[4 * r + 1] * c0 - b;
         const float x = tr[4 * r + 2] * c1 - b;
-        const float h1 = div * x;
+        const float h1 = div[r] * x;
         const float g2 = g[3 * r + 2];
         const float gh0 = g[3 * r + 0] - mx * g2;
         const float gh1 = g[3 * r + 1] - my * g2;
         gmx = gmx - g2 * h0;
         gmy = gmy - g2 * h1;
-        gscale = gscale + g2 * b;
-        const float gx = div * gh1;
-        gdiv = gdiv + gh1 * x;
-        const float gb = (scale * g2 - gh0) - gx;
+        gsr[r] = g2 * b;
+        gscale = gscale + gsr[r];
+        const float gx = div[r] * gh1;
+        gdr[r] = gh1 * x;
+        gdiv = gdiv + gdr[r];
+        const float gb = (scale[r] * g2 - gh0) - gx;
         gt[4 * r + 0] = gb * sum;
         gt[4 * r + 1] = gh0 * c0;
         gt[4 * r + 2] = gx * c1;
@@ -459,6 +474,15 @@ __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], floa
     gt[2] = gt[2] + gby;
     gt[3] = gt[3] + gbz;
     gt[0] = gt[0] - ((gbx + gby) + gbz);
+}
+
+__device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,
+                                                     float scale, float div, const float (&g)[9],
+                                                     float (&gt)[12], float& gmx, float& gmy,
+                                                     float& gscale, float& gdiv) {
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
+    float gsr[3], gdr[3];
+    tensor_aca_rect_grad_rows(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
 }
 
 }  // namespace hg

@@ -53,6 +53,46 @@ void check_out(const at::Tensor& out, at::IntArrayRef shape, const at::Device& d
 }
 
 // ------------------------------------------------------------------ TensorACA rect
+// scale / div as the reference composition takes them (.py:301-302): torch.mul(div, X) and
+// scale * h_temp broadcast against the (B,3,1) columns X, h_temp and are assigned into the
+// (B,3,1) column of H, so any shape whose broadcast with (B,3,1) is (B,3,1) -- after the
+// leading size-1 dimensions beyond three, which the assignment drops -- is accepted: one
+// value, (B,1,1) per problem, (3,1) per row, (B,3,1) per (problem, row).  Anything else
+// raises, as the reference's assignment would.
+struct Bcast {
+    int64_t sb = 0, sr = 0;  // element strides along b and r; 0 where broadcast
+    bool over_b = false, over_r = false;
+};
+
+Bcast bcast_of(const at::Tensor& t, int64_t B, const char* name) {
+    std::vector<int64_t> sz(t.sizes().begin(), t.sizes().end());
+    std::vector<int64_t> st(t.strides().begin(), t.strides().end());
+    while (sz.size() > 3 && sz.front() == 1) {
+        sz.erase(sz.begin());
+        st.erase(st.begin());
+    }
+    TORCH_CHECK(sz.size() <= 3, "sks_amd::tensor_aca_rect: ", name, " of shape ", t.sizes(),
+                " does not broadcast to the (B,3,1) column it scales (.py:301-302)");
+    const int64_t target[3] = {B, 3, 1};
+    int64_t s3[3] = {1, 1, 1}, t3[3] = {0, 0, 0};
+    const size_t off = 3 - sz.size();
+    for (size_t i = 0; i < sz.size(); ++i) {
+        s3[off + i] = sz[i];
+        t3[off + i] = st[i];
+    }
+    for (int j = 0; j < 3; ++j)
+        TORCH_CHECK(s3[j] == 1 || s3[j] == target[j], "sks_amd::tensor_aca_rect: ", name,
+                    " of shape ", t.sizes(), " does not broadcast to (", B, ",3,1) (.py:301-302)");
+    Bcast b;
+    b.over_b = s3[0] != 1;
+    b.over_r = s3[1] != 1;
+    b.sb = b.over_b ? t3[0] : 0;
+    b.sr = b.over_r ? t3[1] : 0;
+    return b;
+}
+
+bool one_value(const at::Tensor& t) { return t.numel() == 1; }
+
 at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& scale_,
                      const at::Tensor& div_, at::Tensor& out) {
     const at::Device dev = tar_.device();
@@ -61,20 +101,23 @@ at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::T
     on_gpu(scale_, "scale", dev);
     on_gpu(div_, "div", dev);
     check_rect(src_, tar_);
-    // batch-uniform, one element each (the reference derives them from sample 0 into (1,)
-    // tensors, .py:33-35); a per-sample tensor would not mean what it does in the reference's
-    // broadcasting composition, so it is refused rather than read at element 0
-    TORCH_CHECK(scale_.numel() == 1 && div_.numel() == 1,
-                "sks_amd: scale and div must hold one element each (batch-uniform, .py:33-35)");
     const int64_t B = tar_.size(0);
+    const Bcast sb = bcast_of(scale_, B, "scale"), db = bcast_of(div_, B, "div");
     check_out(out, {B, 3, 3}, dev);
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
-    const at::Tensor scale = scale_.contiguous(), div = div_.contiguous();
     const c10::DeviceGuard guard(dev);
-    hip_ok(hg_tensor_aca_rect_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
-                                  out.data_ptr<float>(), B, scale.data_ptr<float>(),
-                                  div.data_ptr<float>(), stream_of(tar)),
-           "hg_tensor_aca_rect_f32");
+    if (one_value(scale_) && one_value(div_)) {  // the reference's own (1,) tensors (.py:33-35)
+        hip_ok(hg_tensor_aca_rect_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                      out.data_ptr<float>(), B, scale_.data_ptr<float>(),
+                                      div_.data_ptr<float>(), stream_of(tar)),
+               "hg_tensor_aca_rect_f32");
+        return out;
+    }
+    hip_ok(hg_tensor_aca_rect_bcast_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                        out.data_ptr<float>(), B, scale_.data_ptr<float>(), sb.sb,
+                                        sb.sr, div_.data_ptr<float>(), db.sb, db.sr,
+                                        stream_of(tar)),
+           "hg_tensor_aca_rect_bcast_f32");
     return out;
 }
 
@@ -108,8 +151,23 @@ at::Tensor rect_scalar(const at::Tensor& src, const at::Tensor& tar, double scal
     return out;
 }
 
-// (grad_src (B,3,4) or (0,), grad_tar (B,3,4), [dscale, ddiv] (2,) or (0,))
-std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
+// A parameter's gradient from the kernel's partials: summed over the dimensions it was
+// broadcast along, in hg_sum_rows_f32's fixed order, and shaped like the parameter.
+at::Tensor reduce_param_grad(at::Tensor part, const Bcast& b, const at::Tensor& param, int64_t B,
+                             void* stream) {
+    if (b.over_b && b.over_r)  // (3,B) -> (B,3)
+        return part.view({3, B}).t().contiguous().reshape(param.sizes());
+    if (b.over_b) return part.reshape(param.sizes());  // (B): one value per problem
+    const int64_t rows = b.over_r ? 3 : 1;              // (3,B) or (B): summed over b
+    at::Tensor g = at::empty({rows}, part.options());
+    hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), rows, B, g.data_ptr<float>(), stream),
+           "hg_sum_rows_f32");
+    return g.reshape(param.sizes());
+}
+
+// (grad_src (B,3,4) or (0,), grad_tar (B,3,4), grad_scale, grad_div shaped like scale / div,
+// or (0,) when not needed)
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& grad_,
     const at::Tensor& scale_, const at::Tensor& div_, bool need_src, bool need_scale_div) {
     const at::Device dev = tar_.device();
@@ -119,32 +177,46 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor> rect_backward(
     on_gpu(scale_, "scale", dev);
     on_gpu(div_, "div", dev);
     check_rect(src_, tar_);
-    TORCH_CHECK(scale_.numel() == 1 && div_.numel() == 1,
-                "sks_amd: scale and div must hold one element each (batch-uniform, .py:33-35)");
     const int64_t B = tar_.size(0);
+    const Bcast sb = bcast_of(scale_, B, "scale"), db = bcast_of(div_, B, "div");
     TORCH_CHECK(grad_.dim() == 3 && grad_.size(0) == B && grad_.size(1) == 3 && grad_.size(2) == 3,
                 "sks_amd::tensor_aca_rect_backward: grad must be (B,3,3)");
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous(), grad = grad_.contiguous();
-    const at::Tensor scale = scale_.contiguous(), div = div_.contiguous();
     at::Tensor g_tar = at::empty({B, 3, 4}, tar.options());
     at::Tensor g_src = need_src ? at::empty({B, 3, 4}, tar.options()) : at::empty({0}, tar.options());
-    at::Tensor part = need_scale_div ? at::empty({2, B}, tar.options()) : at::empty({0}, tar.options());
+    at::Tensor none = at::empty({0}, tar.options());
     const c10::DeviceGuard guard(dev);
-    hip_ok(hg_tensor_aca_rect_backward_f32(
-               src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
-               scale.data_ptr<float>(), div.data_ptr<float>(),
-               need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
-               need_scale_div && B ? part.data_ptr<float>() : nullptr, stream_of(tar)),
-           "hg_tensor_aca_rect_backward_f32");
-    // per-problem partials summed on the device in a fixed order (hg_sum_rows_f32)
-    at::Tensor g_sd = part;
-    if (need_scale_div) {
-        g_sd = at::empty({2}, tar.options());
-        hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), 2, B, g_sd.data_ptr<float>(),
-                               stream_of(tar)),
+    void* st = stream_of(tar);
+    if (one_value(scale_) && one_value(div_)) {
+        at::Tensor part = need_scale_div ? at::empty({2, B}, tar.options()) : none;
+        hip_ok(hg_tensor_aca_rect_backward_f32(
+                   src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+                   scale_.data_ptr<float>(), div_.data_ptr<float>(),
+                   need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
+                   need_scale_div && B ? part.data_ptr<float>() : nullptr, st),
+               "hg_tensor_aca_rect_backward_f32");
+        if (!need_scale_div) return {g_src, g_tar, none, none};
+        // per-problem partials summed on the device in a fixed order (hg_sum_rows_f32)
+        at::Tensor g_sd = at::empty({2}, tar.options());
+        hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), 2, B, g_sd.data_ptr<float>(), st),
                "hg_sum_rows_f32");
+        return {g_src, g_tar, g_sd.slice(0, 0, 1).reshape(scale_.sizes()),
+                g_sd.slice(0, 1, 2).reshape(div_.sizes())};
     }
-    return {g_src, g_tar, g_sd};
+    // each parameter's partials: one per (row, problem) where it varies over rows, else the
+    // problem's three-row sum
+    at::Tensor ps = need_scale_div ? at::empty({sb.over_r ? 3 * B : B}, tar.options()) : none;
+    at::Tensor pd = need_scale_div ? at::empty({db.over_r ? 3 * B : B}, tar.options()) : none;
+    hip_ok(hg_tensor_aca_rect_bcast_backward_f32(
+               src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+               scale_.data_ptr<float>(), sb.sb, sb.sr, div_.data_ptr<float>(), db.sb, db.sr,
+               need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
+               need_scale_div && B ? ps.data_ptr<float>() : nullptr, sb.over_r ? 1 : 0,
+               need_scale_div && B ? pd.data_ptr<float>() : nullptr, db.over_r ? 1 : 0, st),
+           "hg_tensor_aca_rect_bcast_backward_f32");
+    if (!need_scale_div) return {g_src, g_tar, none, none};
+    return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, st),
+            reduce_param_grad(pd, db, div_, B, st)};
 }
 
 // ------------------------------------------------------------------ compact offsets form
@@ -314,12 +386,12 @@ at::Tensor call_rect(const at::Tensor& src, const at::Tensor& tar, const at::Ten
 
 // The backward ops are reached through the dispatcher too, so tracing (fake tensors,
 // AOT autograd) sees their Meta kernels instead of a raw launch.
-std::tuple<at::Tensor, at::Tensor, at::Tensor> call_rect_backward(
+std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> call_rect_backward(
     const at::Tensor& src, const at::Tensor& tar, const at::Tensor& grad, const at::Tensor& scale,
     const at::Tensor& div, bool need_src, bool need_sd) {
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::tensor_aca_rect_backward", "")
-                         .typed<std::tuple<at::Tensor, at::Tensor, at::Tensor>(
+                         .typed<std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>(
                              const at::Tensor&, const at::Tensor&, const at::Tensor&,
                              const at::Tensor&, const at::Tensor&, bool, bool)>();
     return op.call(src, tar, grad, scale, div, need_src, need_sd);
@@ -351,12 +423,11 @@ class RectFunction : public torch::autograd::Function<RectFunction> {
         const at::Tensor &src = saved[0], &tar = saved[1], &scale = saved[2], &div = saved[3];
         const bool need_src = ctx->needs_input_grad(0);
         const bool need_sd = ctx->needs_input_grad(2) || ctx->needs_input_grad(3);
-        auto [g_src, g_tar, g_sd] =
+        auto [g_src, g_tar, g_scale, g_div] =
             call_rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd);
         at::Tensor none;
         return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none,
-                ctx->needs_input_grad(2) ? g_sd.slice(0, 0, 1).reshape(scale.sizes()) : none,
-                ctx->needs_input_grad(3) ? g_sd.slice(0, 1, 2).reshape(div.sizes()) : none};
+                ctx->needs_input_grad(2) ? g_scale : none, ctx->needs_input_grad(3) ? g_div : none};
     }
 };
 
@@ -432,7 +503,7 @@ TORCH_LIBRARY(sks_amd, m) {
     m.def("tensor_aca_rect.scalar_out(Tensor src, Tensor tar, float scale, float div, *, "
           "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect_backward(Tensor src, Tensor tar, Tensor grad, Tensor scale, "
-          "Tensor div, bool need_src, bool need_scale_div) -> (Tensor, Tensor, Tensor)");
+          "Tensor div, bool need_src, bool need_scale_div) -> (Tensor, Tensor, Tensor, Tensor)");
     m.def("tensor_aca_offsets(Tensor corner, Tensor offsets, float width, float height) -> Tensor");
     m.def("tensor_aca_offsets.out(Tensor corner, Tensor offsets, float width, float height, *, "
           "Tensor(a!) out) -> Tensor(a!)");
@@ -463,21 +534,29 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
     });
     m.impl("aca", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
     m.impl("sks", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
-    m.impl("tensor_aca_rect", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&,
-                                 const at::Tensor&) { return meta_b33(t); });
+    m.impl("tensor_aca_rect", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor& sc,
+                                 const at::Tensor& dv) {
+        check_rect(s, t);
+        bcast_of(sc, t.size(0), "scale");  // the shapes the reference composition accepts
+        bcast_of(dv, t.size(0), "div");
+        return meta_b33(t);
+    });
     m.impl("tensor_aca_rect.scalar",
            [](const at::Tensor& s, const at::Tensor& t, double, double) { return meta_b33(t); });
     m.impl("tensor_aca_offsets", [](const at::Tensor& c, const at::Tensor& o, double, double) {
         return meta_b33(o);
     });
     m.impl("tensor_aca_rect_backward",
-           [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&, const at::Tensor&,
-              const at::Tensor&, bool need_src, bool need_sd) {
+           [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&, const at::Tensor& sc,
+              const at::Tensor& dv, bool need_src, bool need_sd) {
                const int64_t B = t.size(0);
                return std::make_tuple(need_src ? at::empty({B, 3, 4}, t.options())
                                                : at::empty({0}, t.options()),
                                       at::empty({B, 3, 4}, t.options()),
-                                      at::empty({need_sd ? 2 : 0}, t.options()));
+                                      need_sd ? at::empty(sc.sizes(), t.options())
+                                              : at::empty({0}, t.options()),
+                                      need_sd ? at::empty(dv.sizes(), t.options())
+                                              : at::empty({0}, t.options()));
            });
     m.impl("tensor_aca_offsets_backward",
            [](const at::Tensor& c, const at::Tensor& o, const at::Tensor&, double, double,

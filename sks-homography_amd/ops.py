@@ -208,16 +208,13 @@ Scalar = Union[float, int, torch.Tensor]
 
 
 def _dev_scalar(x, dev: torch.device) -> torch.Tensor:
-    """A batch-uniform scalar as a float32 GPU tensor (no copy when it already is one --
-    the reference keeps scale/div in (1,)-shaped tensors, .py:33-35; the op checks that
-    it sits on the batch's device)."""
+    """scale / div as a float32 GPU tensor: kept as it is when it already is one (the
+    reference keeps them in (1,)-shaped tensors, .py:33-35), else converted (differentiably).
+    Any shape the reference composition broadcasts against the (B,3,1) columns -- one value,
+    (B,1,1) per problem, (3,1) per row, (B,3,1) -- is accepted; the native op checks it."""
     if type(x) is torch.Tensor and x.dtype is torch.float32 and x.is_cuda:
-        return x  # the native op refuses more than one element
-    t = torch.as_tensor(x, dtype=torch.float32, device=dev).reshape(-1)
-    if t.numel() != 1:
-        raise ValueError(f"scale/div must be one batch-uniform value (.py:33-35), got "
-                         f"{t.numel()} elements")
-    return t
+        return x
+    return torch.as_tensor(x, dtype=torch.float32, device=dev)
 
 
 def _gpu_device(device) -> torch.device:
@@ -240,8 +237,10 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     """TensorACA rectangle->quad (Modules_Runtime_Test.py:286-309), unnormalised.
 
     src, tar: (B,3,4) float32 homogeneous (rows x, y, 1; columns M, N, P, Q).
-    scale, div: batch-uniform width and width/height -- Python numbers or one-element
-    float32 tensors (kept on device, as the reference keeps them).  Returns (B,3,3).
+    scale, div: width and width/height -- Python numbers, or tensors of any shape the
+    reference composition broadcasts against the (B,3,1) columns it scales (.py:301-302):
+    one value (the reference's own (1,) tensors, .py:33-35), (B,1,1) per problem, (3,1)
+    per row, (B,3,1); taken as float32 on tar's device.  Returns (B,3,3).
     Runs torch.ops.sks_amd.tensor_aca_rect (native, csrc/hg_torch_ops.cpp); with tensor
     scale/div and no ``out`` it is differentiable in all four inputs.
     """
@@ -259,9 +258,10 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
 def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor,
                              scale: Scalar, div: Scalar, need_src: bool = True,
                              need_scale_div: bool = True):
-    """Gradients of tensor_aca_rect: (dL/dsrc (B,3,4) or empty, dL/dtar (B,3,4),
-    [dL/dscale, dL/ddiv] (2,) or empty).  The per-problem scale/div partials from the
-    kernel are summed on the device (deterministically, in float32)."""
+    """Gradients of tensor_aca_rect: (dL/dsrc (B,3,4) or empty, dL/dtar (B,3,4), dL/dscale,
+    dL/ddiv shaped like scale and div, or empty).  The kernel's per-problem (or per-row)
+    partials are summed over the dimensions scale / div were broadcast along, on the device
+    (deterministically, in float32)."""
     _gpu_only(tar)
     return _OPS.tensor_aca_rect_backward.default(
         src, tar, grad, _dev_scalar(scale, tar.device), _dev_scalar(div, tar.device),

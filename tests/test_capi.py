@@ -133,6 +133,11 @@ def test_other_entry_validation(pkg):
     assert lib.hg_rand_gather_solve_f64(0, 16, 8, 5, 11, 16, 4, 0, None) == 1  # pool not 16-B
     assert lib.hg_rand_gather_solve_f64(0, 16, 16, 5, 11, 4, 4, 0, None) == 1  # H unaligned
     assert lib.hg_mrg32k3a_state(11, 0, 0, None) == 1                             # NULL state
+    assert lib.hg_tensor_aca_rect_bcast_f32(None, None, None, -1, None, 0, 0, None, 0, 0, None) == 1
+    assert lib.hg_tensor_aca_rect_bcast_f32(None, None, None, 0, None, 0, 0, None, 0, 0, None) == 0
+    assert lib.hg_tensor_aca_rect_bcast_f32(None, None, None, 4, None, 0, 0, None, 0, 0, None) == 1
+    assert lib.hg_tensor_aca_rect_bcast_backward_f32(None, None, None, 3, None, 0, 0, None, 0, 0,
+                                                     None, None, None, 0, None, 0, None) == 1
     assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
                                                None) == 1
     assert lib.hg_solve_one_f32(0, None, None, None, 1, None) == 1               # NULL points
@@ -257,7 +262,7 @@ def test_native_torch_ops_registered(pkg):
     assert ops.solve(m(5, 8), m(5, 8), 1, True, 0).shape == (5, 9)
     assert ops.solve(m(8, 7), m(8, 7), 2, False, 1).shape == (9, 7)
     g = ops.tensor_aca_rect_backward(m(5, 3, 4), m(5, 3, 4), m(5, 3, 3), m(1), m(1), True, False)
-    assert [tuple(x.shape) for x in g] == [(5, 3, 4), (5, 3, 4), (0,)]
+    assert [tuple(x.shape) for x in g] == [(5, 3, 4), (5, 3, 4), (0,), (0,)]
     with pytest.raises(NotImplementedError):
         ops.tensor_aca_offsets(torch.zeros(2, 2), torch.zeros(2, 4, 2), 1.0, 1.0)
     with open("/proc/self/maps") as f:

@@ -190,17 +190,50 @@ def test_rect_large_batch_vs_oracle(orc, oracle, pkg, dev):
     _bits(orc, pkg.tensor_aca_rect(sh, th, sc, dv), want, "rect 1M")
 
 
-def test_rect_close_to_torch_composed_on_gpu(pkg, dev):
-    """Against the reference's own ATen composition run on THIS GPU (ROCm kernels
-    may contract differently from ATen-CPU, so the bar is a tolerance: 1e-5 of the
-    row norm; the bit-exact bar is against the CPU-pinned fixtures above)."""
+@pytest.mark.parametrize("B", [65536, 1 << 20])
+def test_rect_close_to_torch_composed_on_gpu(pkg, dev, B):
+    """Against the reference's own ATen composition run on THIS GPU (the reference's
+    device='cuda' run, .py:393).  Inputs: the reference's own integer batches (adjust) and the
+    same with fractional targets.
+
+    The op is ATen-CPU bit for bit (asserted; tests/test_gpu_rect_aten_bits.py pins it on
+    random bits).  ROCm's ATen evaluates the composition differently from ATen-CPU (measured
+    and printed: torch.cross agrees bit for bit across the devices, torch.sum of the three
+    cross terms does not -- another summation order), and H's third column and w row cancel
+    (scale*b - mx*h0 - my*h1; c0 - S), so the reference composition on the GPU differs from
+    ITSELF on the CPU by ~1e-5 relative on fractional inputs (exact on integer ones).  north_star's 1e-6 bar therefore holds against the CPU
+    path (bit-exact) and cannot hold against the GPU composition for any CPU-exact
+    implementation; the bar here is that spread: per H (normwise) and per row, the op is no
+    farther from the GPU composition than the reference on the CPU is.  The measured maxima,
+    and how far torch.cross alone moves between the devices, are printed."""
     import bench
     torch.manual_seed(0)
-    _, _, sh, th, sc, dv = pkg.adjust(dev, 65536)
-    ours = pkg.TensorACA_rect(65536, sh, th, sc, dv).double()
-    theirs = bench.torch_tensor_aca_rect(sh, th, sc, dv).double()
-    err = (ours - theirs).norm(dim=2) / theirs.norm(dim=2)
-    assert err.max().item() < 1e-5
+    _, _, sh, th, sc, dv = pkg.adjust(dev, B)
+    thf = th + torch.rand_like(th)
+    thf[:, 2, :] = 1.0
+    for tag, t in (("integer", th), ("fractional", thf)):
+        ours = pkg.TensorACA_rect(B, sh, t, sc, dv).double()
+        theirs = bench.torch_tensor_aca_rect(sh, t, sc, dv).double()
+        cpu = bench.torch_tensor_aca_rect(sh.cpu(), t.cpu(), sc.cpu(), dv.cpu())
+        assert torch.equal(ours.float().cpu(), cpu), f"{tag}: op differs from ATen-CPU"
+        cpu_d = cpu.double().to(dev)
+
+        def gaps(x):
+            mat = ((x - theirs).flatten(1).norm(dim=1) / theirs.flatten(1).norm(dim=1)).max().item()
+            row = ((x - theirs).norm(dim=2) / theirs.norm(dim=2)).max().item()
+            return mat, row
+
+        (mat, row), (smat, srow) = gaps(ours), gaps(cpu_d)
+        d = t[:, :, 1:] - t[:, :, 0:1]
+        cg = torch.cross(d[:, 1:2, :], d[:, 0:1, :], dim=2)
+        cc = torch.cross(d[:, 1:2, :].cpu(), d[:, 0:1, :].cpu(), dim=2)
+        cross_diff = int((cg.cpu() != cc).sum())
+        sum_diff = int((torch.sum(cc, dim=2) != torch.sum(cg, dim=2).cpu()).sum())
+        print(f"\nTensorACA vs ATen composition on the GPU, B={B} {tag}: per H {mat:.3e}, per "
+              f"row {row:.3e}; the reference on the CPU vs on the GPU: per H {smat:.3e}, per row "
+              f"{srow:.3e}; torch.cross CPU vs GPU: {cross_diff} of {cc.numel()} elements differ, "
+              f"torch.sum of the cross terms: {sum_diff} of {B}")
+        assert mat <= max(1e-6, smat) and row <= max(1e-6, srow), (tag, mat, row, smat, srow)
 
 
 # -------------------------------------------------------------- other entries
@@ -373,7 +406,7 @@ def test_rect_backward_kernel_vs_oracle(orc, oracle, pkg, dev):
         for scale, div in ((128.0, 1.0), (50.0, 1.25)):
             s_t = torch.tensor([scale], device=dev)
             d_t = torch.tensor([div], device=dev)
-            g_src, g_tar, _ = pkg.tensor_aca_rect_backward(sh, th, gH, s_t, d_t, True, False)
+            g_src, g_tar, _, _ = pkg.tensor_aca_rect_backward(sh, th, gH, s_t, d_t, True, False)
             ws, wt, wsd = oracle.tensor_aca_rect_backward(sh.cpu().numpy(), th.cpu().numpy(),
                                                           gH.cpu().numpy(), scale, div)
             _bits(orc, g_tar, wt, f"grad_tar B={B}")

@@ -81,9 +81,10 @@ def test_rect_and_vanilla_equal_reference_special_fixture(orc, pkg, dev, tag, sc
     assert ok.all(), f"ACA_vanilla: {int((~ok).sum())} differ"
 
 
-def test_scale_and_div_must_be_batch_uniform(pkg, dev):
-    """scale / div hold one value for the whole batch (the reference derives them from sample
-    0 into (1,) tensors, .py:33-35): a multi-element one is refused, never read at element 0."""
+def test_scale_and_div_shapes_the_reference_refuses(pkg, dev):
+    """A (2,) scale or div does not broadcast to the (B,3,1) column it scales, so the
+    reference's own composition refuses it (.py:301-302); so do the op and its backward (the
+    accepted broadcast shapes are tests/test_gpu_rect_bcast.py's)."""
     torch.manual_seed(0)
     _, _, sh, th, sc, dv = pkg.adjust(dev, 16)
     assert pkg.TensorACA_rect(16, sh, th, sc, dv).shape == (16, 3, 3)

@@ -1,0 +1,137 @@
+"""TensorACA with scale / div broadcast as the reference composition broadcasts them
+(Modules_Runtime_Test.py:301-302: torch.mul(div, X) and scale * h_temp against the (B,3,1)
+columns, assigned into the (B,3,1) column of H).
+
+Pins (tests/golden/torch_rect_bcast.npz: the reference's own statements on CPU torch, B = 64,
+17 shapes plus two mixed cases):
+  * every shape the composition accepts -- one value, (B,1,1) per problem, (3,1) per row,
+    (B,3,1), with or without leading size-1 dimensions -- gives the reference's H bit for bit,
+    through torch.ops.sks_amd.tensor_aca_rect, reference_api.TensorACA_rect and the C ABI;
+  * every shape it refuses raises;
+  * the backward returns gradients shaped like scale / div: bit for bit the oracle's per-row
+    partials reduced in hg_sum_rows_f32's order, and within 1e-5 (of the largest magnitude)
+    of ATen autograd through the reference statements (the measured gap is printed).
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+from test_gpu_parity import _bits, _sum_rows_restated
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return load_golden("torch_rect_bcast.npz")
+
+
+def _cases(gold):
+    return [(k, str(n), bool(a)) for k, (n, a) in enumerate(zip(gold["cases"], gold["accepted"]))]
+
+
+def _t(a, dev):
+    return torch.from_numpy(np.array(a)).to(dev)  # keeps 0-d arrays 0-d
+
+
+def test_forward_bits_and_refusals(orc, pkg, dev, gold):
+    sh, th = _t(gold["src_h"], dev), _t(gold["tar_h"], dev)
+    B = sh.shape[0]
+    for k, name, acc in _cases(gold):
+        sc, dv = _t(gold[f"c{k}_scale"], dev), _t(gold[f"c{k}_div"], dev)
+        if not acc:
+            with pytest.raises((RuntimeError, ValueError)):
+                pkg.tensor_aca_rect(sh, th, sc, dv)
+            continue
+        want = gold[f"c{k}_H"]
+        _bits(orc, pkg.tensor_aca_rect(sh, th, sc, dv), want, f"op {name}")
+        _bits(orc, pkg.TensorACA_rect(B, sh, th, sc, dv), want, f"TensorACA_rect {name}")
+        out = torch.empty(B, 3, 3, device=dev)
+        _bits(orc, pkg.tensor_aca_rect(sh, th, sc, dv, out=out), want, f"out {name}")
+        # non-contiguous and expanded views of the same values
+        sc_e = sc.expand(sc.shape) if sc.dim() == 0 else sc.transpose(0, -1).transpose(0, -1)
+        _bits(orc, pkg.tensor_aca_rect(sh, th, sc_e, dv), want, f"view {name}")
+
+
+def test_forward_expanded_and_strided_parameters(orc, oracle, pkg, dev):
+    """A (B,3,1) parameter given as an expanded (1,3,1) view and as a strided slice of a
+    larger tensor gives the values it holds."""
+    B = 1000
+    torch.manual_seed(3)
+    _, _, sh, th, _, _ = pkg.adjust(dev, B)
+    th = th + torch.rand_like(th)
+    th[:, 2, :] = 1.0
+    per_row = torch.rand(1, 3, 1, device=dev) * 64 + 64
+    big = torch.rand(B, 3, 4, device=dev) + 0.5
+    dv = big[:, :, 2:3]  # (B,3,1), strides (12, 4, 1)
+    want = oracle.tensor_aca_rect_rows(sh.cpu().numpy(), th.cpu().numpy(),
+                                       per_row.cpu().numpy(), dv.cpu().numpy())
+    _bits(orc, pkg.tensor_aca_rect(sh, th, per_row.expand(B, 3, 1), dv), want, "expanded/strided")
+    _bits(orc, pkg.tensor_aca_rect(sh, th, per_row, dv.contiguous()), want, "contiguous")
+
+
+def _reduce_like(part_rows, part_prob, shape, B):
+    """The op's reduction of the kernel partials to the parameter's shape (restated)."""
+    sz = list(shape)
+    while len(sz) > 3 and sz[0] == 1:
+        sz = sz[1:]
+    s3 = [1] * (3 - len(sz)) + sz
+    over_b, over_r = s3[0] != 1, s3[1] != 1
+    if over_b and over_r:
+        return part_rows.reshape(shape)
+    if over_b:
+        return part_prob.reshape(shape)
+    if over_r:
+        return _sum_rows_restated(np.ascontiguousarray(part_rows.T)).reshape(shape)
+    return _sum_rows_restated(part_prob.reshape(1, B)).reshape(shape)
+
+
+def test_backward_shapes_bits_and_aten(orc, oracle, pkg, dev, gold):
+    sh, th, gH = _t(gold["src_h"], dev), _t(gold["tar_h"], dev), _t(gold["gH"], dev)
+    B = sh.shape[0]
+    worst = 0.0
+    for k, name, acc in _cases(gold):
+        if not acc:
+            continue
+        sc_np, dv_np = gold[f"c{k}_scale"], gold[f"c{k}_div"]
+        sc, dv = _t(sc_np, dev), _t(dv_np, dev)
+        g_src, g_tar, g_sc, g_dv = pkg.tensor_aca_rect_backward(sh, th, gH, sc, dv, True, True)
+        assert tuple(g_sc.shape) == sc_np.shape and tuple(g_dv.shape) == dv_np.shape, name
+        ws, wt, gsr, gdr, gss, gds = oracle.tensor_aca_rect_rows_backward(
+            gold["src_h"], gold["tar_h"], gold["gH"], sc_np, dv_np)
+        _bits(orc, g_tar, wt, f"grad_tar {name}")
+        _bits(orc, g_src, ws, f"grad_src {name}")
+        _bits(orc, g_sc, _reduce_like(gsr, gss, sc_np.shape, B), f"grad_scale {name}")
+        _bits(orc, g_dv, _reduce_like(gdr, gds, dv_np.shape, B), f"grad_div {name}")
+        for got, key in ((g_tar, "gtar"), (g_sc, "gscale"), (g_dv, "gdiv")):
+            want = gold[f"c{k}_{key}"]
+            err = float(np.abs(got.cpu().numpy() - want).max() / np.abs(want).max())
+            worst = max(worst, err)
+            assert err <= 1e-5, f"{key} {name}: {err:.2e} from ATen autograd"
+        # through autograd: the same gradients reach leaf tensors of scale / div's shapes
+        scg, dvg, thg = sc.clone().requires_grad_(), dv.clone().requires_grad_(), th.clone().requires_grad_()
+        (pkg.TensorACA_rect(B, sh, thg, scg, dvg) * gH).sum().backward()
+        _bits(orc, scg.grad, g_sc.cpu().numpy(), f"autograd scale {name}")
+        _bits(orc, dvg.grad, g_dv.cpu().numpy(), f"autograd div {name}")
+        _bits(orc, thg.grad, g_tar.cpu().numpy(), f"autograd tar {name}")
+    print(f"\nbroadcast TensorACA backward vs ATen autograd (reference statements, CPU): "
+          f"max relative-to-max gap {worst:.2e}")
+
+
+def test_c_abi_strides(orc, oracle, pkg, dev):
+    """hg_tensor_aca_rect_bcast_f32 with explicit element strides (0 = broadcast)."""
+    B = 513
+    torch.manual_seed(5)
+    _, _, sh, th, _, _ = pkg.adjust(dev, B)
+    th = th + torch.rand_like(th)
+    th[:, 2, :] = 1.0
+    sc = torch.rand(B, device=dev) * 64 + 64        # per problem: stride 1 along b
+    dv = torch.rand(3, device=dev) + 0.5            # per row: stride 1 along r
+    H = torch.empty(B, 3, 3, device=dev)
+    pkg._lib.call("hg_tensor_aca_rect_bcast_f32", sh.data_ptr(), th.data_ptr(), H.data_ptr(), B,
+                  sc.data_ptr(), 1, 0, dv.data_ptr(), 0, 1, torch.cuda.current_stream(dev).cuda_stream)
+    want = oracle.tensor_aca_rect_rows(sh.cpu().numpy(), th.cpu().numpy(),
+                                       sc.cpu().numpy().reshape(B, 1, 1),
+                                       dv.cpu().numpy().reshape(3, 1))
+    _bits(orc, H, want, "C ABI strides")

@@ -299,3 +299,44 @@ def test_aca_vanilla_restatement_equals_reference_special_fixture(orc, oracle):
                        normalize=False).reshape(B, 3, 3)
     ok = orc.same_bits(got, g["vanilla"])
     assert ok.all(), int((~ok).sum())
+
+
+def _bcast_cases():
+    g = load_golden("torch_rect_bcast.npz")
+    return g, [(k, str(n), bool(a)) for k, (n, a) in enumerate(zip(g["cases"], g["accepted"]))]
+
+
+def test_oracle_rect_broadcast_scale_div_vs_reference(orc, oracle):
+    """TensorACA with per-problem / per-row scale and div (the reference composition's own
+    broadcasting, .py:301-302): the oracle's row form equals the reference statements' H bit
+    for bit on every shape the composition accepts (tests/golden/torch_rect_bcast.npz), and
+    its gradient of tar is within 1e-6 of ATen autograd's through those statements."""
+    g, cases = _bcast_cases()
+    assert sum(a for _, _, a in cases) >= 9 and sum(not a for _, _, a in cases) >= 8
+    for k, name, acc in cases:
+        if not acc:
+            continue
+        sc, dv = g[f"c{k}_scale"], g[f"c{k}_div"]
+        _assert_bits(orc, oracle.tensor_aca_rect_rows(g["src_h"], g["tar_h"], sc, dv),
+                     g[f"c{k}_H"], f"rect {name}")
+        _, gt, *_ = oracle.tensor_aca_rect_rows_backward(g["src_h"], g["tar_h"], g["gH"], sc, dv)
+        want = g[f"c{k}_gtar"]
+        assert np.abs(gt - want).max() <= 1e-6 * np.abs(want).max(), name
+
+
+def test_rect_op_accepts_the_reference_shapes_on_meta(pkg):
+    """torch.ops.sks_amd.tensor_aca_rect accepts exactly the scale / div shapes the reference
+    composition accepts and refuses the others (checked on meta tensors: the shape rule is
+    the op's own, no GPU needed)."""
+    import torch
+    g, cases = _bcast_cases()
+    B = 64
+    m = lambda *s: torch.empty(*s, device="meta")  # noqa: E731
+    op = torch.ops.sks_amd.tensor_aca_rect.default
+    for k, name, acc in cases:
+        sc, dv = g[f"c{k}_scale"], g[f"c{k}_div"]
+        if acc:
+            assert op(m(B, 3, 4), m(B, 3, 4), m(sc.shape), m(dv.shape)).shape == (B, 3, 3), name
+        else:
+            with pytest.raises(RuntimeError):
+                op(m(B, 3, 4), m(B, 3, 4), m(sc.shape), m(dv.shape))

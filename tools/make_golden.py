@@ -363,8 +363,68 @@ def torch_aca_f64() -> str:
             "4-subsets of orig_pts_wall.txt, %d edge cases" % (torch.__version__, len(es)))
 
 
+BCAST_SHAPES = ["()", "(1,)", "(1,1,1)", "(1,1,1,1)", "(B,1,1)", "(1,B,1,1)", "(3,1)", "(1,3,1)",
+                "(B,3,1)", "(B,)", "(B,1)", "(3,)", "(2,)", "(B,3)", "(B,3,2)", "(2,B,3,1)",
+                "(2,1,1,1)"]
+
+
+def torch_bcast() -> str:
+    """TensorACA_rect's own statements (Modules_Runtime_Test.py:294-302) with scale / div of
+    every shape in BCAST_SHAPES (B = 64), on CPU torch: whether the composition accepts the
+    shape (its broadcasting and the (B,3,1) column assignment decide), H where it does, and
+    the gradients ATen autograd gives through those statements (dL/dtar, dL/dscale, dL/ddiv
+    for L = sum(H * gH)).  scale and div get the same shape in each case, plus two mixed
+    cases.  Writes tests/golden/torch_rect_bcast.npz; returns its manifest line."""
+    B = 64
+    g = torch.Generator().manual_seed(77)
+    src = torch.rand((B, 4, 2), generator=g) * 128 + torch.tensor([[0, 0], [128, 0], [0, 128],
+                                                                   [128, 128.0]])
+    tar = src + torch.rand((B, 4, 2), generator=g) * 32
+    ones = torch.ones((B, 1, 4))
+    src_h = torch.cat((src.transpose(1, 2), ones), dim=1)
+    tar_h = torch.cat((tar.transpose(1, 2), ones), dim=1)
+    gH = torch.randn((B, 3, 3), generator=g)
+    out = {"src_h": src_h.numpy(), "tar_h": tar_h.numpy(), "gH": gH.numpy()}
+    cases = [(sh, sh) for sh in BCAST_SHAPES] + [("(1,)", "(B,1,1)"), ("(3,1)", "(B,3,1)")]
+    names, accepted = [], []
+    for k, (ss, ds) in enumerate(cases):
+        shp = lambda t: tuple(eval(t, {"B": B}))  # noqa: E731
+        scale = (torch.rand(shp(ss), generator=g) * 64 + 64).float()
+        div = (torch.rand(shp(ds), generator=g) + 0.5).float()
+        tr = tar_h.clone().requires_grad_(True)
+        sc = scale.clone().requires_grad_(True)
+        dv = div.clone().requires_grad_(True)
+        try:
+            H = run_ref_statements("TensorACA_rect", bs=B, src=src_h, tar=tr, scale=sc,
+                                   div=dv)["H"]
+            ok = True
+        except RuntimeError:
+            ok = False
+        names.append(f"{ss}|{ds}")
+        accepted.append(ok)
+        out[f"c{k}_scale"], out[f"c{k}_div"] = scale.numpy(), div.numpy()
+        if ok:
+            (H * gH).sum().backward()
+            out[f"c{k}_H"] = H.detach().numpy().copy()
+            out[f"c{k}_gtar"] = tr.grad.numpy().copy()
+            out[f"c{k}_gscale"] = sc.grad.numpy().copy()
+            out[f"c{k}_gdiv"] = dv.grad.numpy().copy()
+    out["cases"] = np.array(names)
+    out["accepted"] = np.array(accepted)
+    np.savez_compressed(os.path.join(OUT, "torch_rect_bcast.npz"), **out)
+    return ("torch_rect_bcast.npz: TensorACA_rect statements of the reference on CPU torch %s "
+            "(ATen CPU capability %s), B = 64, scale/div of %d shapes (accepted or refused by "
+            "the composition itself), H and the ATen autograd gradients of sum(H * gH)"
+            % (torch.__version__, torch.backends.cpu.get_cpu_capability(), len(cases)))
+
+
 if __name__ == "__main__":
-    if sys.argv[1:] == ["--torch-f64"]:  # this fixture alone, appended to the manifest
+    if sys.argv[1:] == ["--torch-bcast"]:  # this fixture alone, appended to the manifest
+        line = torch_bcast()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    elif sys.argv[1:] == ["--torch-f64"]:  # this fixture alone, appended to the manifest
         line = torch_aca_f64()
         with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
             f.write("- " + line + "\n")
