@@ -361,12 +361,39 @@ def graph_of(d: Dist, fn, calls: int):
     return g
 
 
+PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+
+
+def traffic_source() -> dict:
+    """Where `roofline.traffic` comes from: the committed rocprofv3 PMC summary, the run it
+    was reduced from, and whether the headline kernel's sources still have the digest they
+    were measured on (a changed kernel makes the committed figure stale: traffic is then
+    reported as null until the PMC passes are re-run)."""
+    sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
+    try:
+        import build_lib
+        now = build_lib.sources_digest("aos")
+    finally:
+        sys.path.pop(0)
+    try:
+        with open(PMC_TRAFFIC) as f:
+            prov = json.load(f).get("provenance", {})
+    except (OSError, ValueError):
+        prov = {}
+    measured = prov.get("sources_aos", {}).get("sha256")
+    return {"file": os.path.relpath(PMC_TRAFFIC, ROOT), "pmc_run": prov.get("pmc_run"),
+            "sources_sha256_measured": measured, "sources_sha256_now": now["sha256"],
+            "sources_match": measured == now["sha256"]}
+
+
 def pmc_traffic(kernel_key: str):
     """Per-launch HBM bytes of `kernel_key` from the committed rocprofv3 PMC summary
-    (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py), or None."""
-    path = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py), or None -- also None when
+    the kernel sources changed since it was measured (traffic_source)."""
+    if not traffic_source()["sources_match"]:
+        return None
     try:
-        with open(path) as f:
+        with open(PMC_TRAFFIC) as f:
             rec = json.load(f)
         return rec[kernel_key]
     except (OSError, KeyError, ValueError):
@@ -1055,6 +1082,7 @@ def main():
             "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
+            "traffic_source": traffic_source(),
             "kernel": kernel,
             "algorithmic_bytes_per_launch": n * bpp_head,
             "launch_ms": round(ms_launch, 5),

@@ -32,6 +32,27 @@ COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math",
           f"-I{os.path.join(ROOT, 'include')}", f"-I{CSRC}"]
 
 
+# The sources a kernel's measured HBM traffic depends on (profiles/pmc_traffic.json records
+# their digest; bench.py reports the PMC figure only while the tree still matches it).
+TRAFFIC_SOURCES = {
+    "aos": ["csrc/hg_aos.hpp", "csrc/hg_solvers.hpp", "csrc/hg_launch.hpp", "csrc/hg_kernels.hip"],
+}
+
+
+def sources_digest(kind: str = "aos") -> dict:
+    """sha256 of each file of TRAFFIC_SOURCES[kind] (paths relative to the package) and of
+    their concatenation, in a fixed order."""
+    import hashlib
+    files, whole = {}, hashlib.sha256()
+    for rel in TRAFFIC_SOURCES[kind]:
+        data = open(os.path.join(HERE, rel), "rb").read()
+        files[rel] = hashlib.sha256(data).hexdigest()[:16]
+        whole.update(rel.encode() + b"\0" + data)
+    flags = " ".join([f"--offload-arch={ARCH}"] + COMMON[:5])  # not the -I paths
+    whole.update(flags.encode())
+    return {"files": files, "flags": flags, "sha256": whole.hexdigest()[:16]}
+
+
 def hipcc() -> str:
     for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):

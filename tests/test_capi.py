@@ -319,3 +319,18 @@ def test_read_points_rounds_once_like_sscanf(pkg, tmp_path):
     # the first value by exact rounding of the rational: above the midpoint -> the upper neighbour
     lo, hi = Fraction(1), Fraction(1) + Fraction(1, 2**23)
     assert Fraction(tricky[0]) > (lo + hi) / 2 and Fraction(float(got[0])) == hi
+
+
+def test_pmc_traffic_matches_the_kernel_sources():
+    """profiles/pmc_traffic.json's PMC figures were measured on kernel sources whose digest it
+    records; bench.py reports them as `roofline.traffic` only while the tree still has that
+    digest.  A change to the headline kernel's sources fails here until the PMC passes are
+    re-run (tools/gpu_round.sh pmc, tools/pmc_traffic.py) -- the committed figure is never
+    silently reused for a different kernel."""
+    import bench
+    src = bench.traffic_source()
+    assert src["sources_sha256_measured"], "profiles/pmc_traffic.json has no source digest"
+    assert src["sources_match"], (f"kernel sources changed since the PMC run "
+                                  f"({src['sources_sha256_measured']} -> "
+                                  f"{src['sources_sha256_now']}): re-measure the traffic")
+    assert bench.pmc_traffic("aca_f32_aos_norm") is not None

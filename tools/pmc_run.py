@@ -62,6 +62,13 @@ def main():
     ps64, pt64 = ps.double(), pt.double()
     for _ in range(REPS):
         pkg.gather_solve(ps64, pt64, rl, "aca")
+    # round 3: the hand-written MRG32K3A draws (40 M words = 4 x 10 M) and the draws fused
+    # into the gather + solve (no words in memory: 72 B of H per hypothesis)
+    for _ in range(REPS):
+        pkg.rand_mrg32k3a(4 * n, 11, dev)
+    del rl
+    for _ in range(REPS):
+        pkg.rand_gather_solve(ps64, pt64, n, 11, "aca")
     torch.cuda.synchronize()
     print("pmc workload done")
 

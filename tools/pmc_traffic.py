@@ -32,6 +32,9 @@ KEYS = {
     "sample_solve_lds": ("void hg::sample_solve_lds_kernel", None),
     "solve_soa": ("void hg::solve_soa_vec", None),
     "gather_solve_f64_aca": ("void hg::gather_solve_f64_kernel<0", 10_000_000 * 88),
+    # round 3: the MRG32K3A draws alone (40 M words) and fused with the gather + solve
+    "mrg_words": ("hg::mrg_words_kernel", 40_000_000 * 4),
+    "rand_gather_solve_f64_aca": ("void hg::mrg_gather_solve_f64_kernel<0", 10_000_000 * 72),
 }
 
 
@@ -72,6 +75,16 @@ def main():
                                                                       "sks_f32_aos_norm")}
     doc = dict(flat)
     doc["detail"] = res
+    # provenance: which run, and the kernel sources it was measured on (bench.py reports the
+    # figure only while the tree's sources still have this digest; tests/test_capi.py checks)
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
+                                    "sks-homography_amd"))
+    import build_lib
+    doc["provenance"] = {
+        "pmc_run": {"fetch_dir": sys.argv[1], "write_dir": sys.argv[2],
+                    "tag": os.environ.get("PMC_TAG", "")},
+        "sources_aos": build_lib.sources_digest("aos"),
+    }
     doc["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, csv; "
                      "bytes = KiB*1024, FETCH x2 (gfx950 wide-read correction, calibrated on "
                      "stream_copy); median over the launches of `python3 tools/pmc_run.py` (each kernel 5x at "
