@@ -661,22 +661,54 @@ def reference_layout(d: Dist, pkg):
 
 def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
     """The reference harness's sampling flow in its own formats (GPU_Runtime Test.cu:
-    1443-1451) on its own point file, N = 1M: MRG32K3A words (rocRAND, seed 11), then
-    get_rand_list + cal_Homo_ACA/SKS -- unfused (gather to (8,N) rows, then the SoA solver)
-    and fused (hg_gather_solve_f64: 16 B of words in, 72 B of H out per hypothesis).
-    Table 8 times cal_Homo_* alone (245 / 436 us at 1M)."""
+    1443-1451) on its own point file, N = 1M: 4N MRG32K3A words (seed 11), get_rand_list,
+    cal_Homo_ACA/SKS.  Draws: the hand-written generator (rocRAND's host-API words, bit for
+    bit) against rocrand_generate itself with a fresh generator per call, as the harness
+    creates one.  Pipeline: draws + gather + solve in ONE launch (hg_rand_gather_solve_f64:
+    72 B of H per hypothesis, no words in memory) against the two launches (draws, then
+    hg_gather_solve_f64: +16 B of words written and read) and the unfused gather-then-solve;
+    at 1 M and 10 M, beside a write-only stream of the same 72 B per hypothesis (the ceiling
+    of a launch that only writes).  Table 8 times cal_Homo_* alone (245 / 436 us at 1M)."""
+    import ctypes
+    tune = pkg._lib.tune()
+    tune.hg_tune_rocrand_mrg32k3a_u32.argtypes = [ctypes.c_void_p, ctypes.c_int64,
+                                                  ctypes.c_uint64, ctypes.c_void_p]
+    wr = tune.hg_tune_copy
+    wr.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    stream = torch.cuda.current_stream(d.dev).cuda_stream
     g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
     ps = torch.from_numpy(g["pool_src"]).to(d.dev).double()  # Point2f -> Point2d (.cu:1414-1416)
     pt = torch.from_numpy(g["pool_tar"]).to(d.dev).double()
-    f_draw = lambda: pkg.rand_mrg32k3a(4 * n, SEED, d.dev)  # noqa: E731
-    rl = f_draw().view(4, n)
-    for _ in range(3):
+    words = torch.empty(4 * n, dtype=torch.int32, device=d.dev)
+    f_draw = lambda: pkg._lib.call("hg_rand_mrg32k3a_u32", words.data_ptr(), 4 * n, SEED, stream)  # noqa: E731
+    for _ in range(5):
         f_draw()
-    _, ms_draw = timed_region(d, f_draw, 20)
-    out = {"n": n, "pool": int(ps.shape[0]), "draws_us": round(ms_draw * 1e3, 2)}
+    ms_draw = launch_stats(d, f_draw, groups=20)["median_us"] * 1e-3
+    ref_words = torch.empty_like(words)
+    f_roc = lambda: tune.hg_tune_rocrand_mrg32k3a_u32(ref_words.data_ptr(), 4 * n, SEED, stream)  # noqa: E731
+    f_roc()
+    _, ms_roc = timed_region(d, f_roc, 5)
+    f_draw()
+    rl = words.view(4, n)
+    out = {"n": n, "pool": int(ps.shape[0]),
+           "draws": {"words": 4 * n, "us": round(ms_draw * 1e3, 2),
+                     "gbps_written": round(4 * n * 4 / (ms_draw * 1e-3) / 1e9, 1),
+                     "rocrand_generate_us": round(ms_roc * 1e3, 1),
+                     "speedup_vs_rocrand": round(ms_roc / ms_draw, 1),
+                     "bit_identical_to_rocrand": bool(torch.equal(words, ref_words))}}
+    del ref_words
     for algo in ("aca", "sks"):
+        aid = {"aca": 0, "sks": 1}[algo]
         H = torch.empty((9, n), dtype=torch.float64, device=d.dev)
+        H1 = torch.empty((9, n), dtype=torch.float64, device=d.dev)
         f_fused = lambda: pkg.gather_solve(ps, pt, rl, algo)  # noqa: E731
+        f_one = lambda: pkg._lib.call("hg_rand_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(),  # noqa: E731
+                                      ps.shape[0], SEED, H1.data_ptr(), n, 0, stream)
+
+        def f_two():
+            f_draw()
+            pkg._lib.call("hg_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(), ps.shape[0],
+                          words.data_ptr(), H.data_ptr(), n, 0, stream)
 
         def f_split():
             s_, t_ = pkg.get_rand_list(rl, ps, pt)
@@ -685,29 +717,60 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
         for _ in range(10):
             f_fused()
             f_split()
-        _, ms_fused = timed_region(d, f_fused, 200)
-        _, ms_split = timed_region(d, f_split, 200)
+            f_one()
+        ms_fused = launch_stats(d, f_fused, groups=20)["median_us"] * 1e-3
+        ms_one = launch_stats(d, f_one, groups=20)["median_us"] * 1e-3
+        _, ms_two = timed_region(d, f_two, 100)
+        _, ms_split = timed_region(d, f_split, 100)
         f_split()
         same = bool(torch.equal(f_fused().view(torch.int64), H.view(torch.int64)))
-        out[algo] = {"fused_us": round(ms_fused * 1e3, 2),
+        f_one()
+        same_one = bool(torch.equal(H1.view(torch.int64), H.view(torch.int64)))
+        out[algo] = {"draws_gather_solve_one_launch_us": round(ms_one * 1e3, 2),
+                     "draws_then_gather_solve_us": round(ms_two * 1e3, 2),
+                     "gather_solve_from_words_us": round(ms_fused * 1e3, 2),
                      "fused_gbps": round(n * 88 / (ms_fused * 1e-3) / 1e9, 1),
-                     "fused_frac": round(n * 88 / (ms_fused * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                      "gather_then_solve_us": round(ms_split * 1e3, 2),
                      "table8_solver_us": TABLE8_US[algo],
-                     "fused_speedup_vs_table8_solver": round(TABLE8_US[algo] / (ms_fused * 1e3), 2),
-                     "fused_bit_identical_to_unfused": same}
-        del H
-    # the fused kernel's HBM figure at the headline's batch size (88 B per hypothesis)
+                     "one_launch_speedup_vs_table8_solver": round(TABLE8_US[algo] / (ms_one * 1e3), 2),
+                     "fused_bit_identical_to_unfused": same,
+                     "one_launch_bit_identical_to_draws_then_fused": same_one}
+        del H, H1
+    del words, rl
+    # 10 M hypotheses (the headline's batch): the one-launch pipeline against a write-only
+    # stream of its 72 B per hypothesis, and the two-launch form
     big = 10 * n
-    rl_b = pkg.rand_mrg32k3a(4 * big, SEED, d.dev).view(4, big)
-    f_big = lambda: pkg.gather_solve(ps, pt, rl_b, "aca")  # noqa: E731
-    for _ in range(5):
-        f_big()
-    _, ms_big = timed_region(d, f_big, 50)
-    out["aca_large"] = {"n": big, "fused_us": round(ms_big * 1e3, 2),
-                        "fused_gbps": round(big * 88 / (ms_big * 1e-3) / 1e9, 1),
-                        "fused_frac": round(big * 88 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)}
-    del rl_b
+    wbuf = torch.empty(big * 18, dtype=torch.float32, device=d.dev)
+    f_write = lambda: wr(5, None, wbuf.data_ptr(), big * 72, stream)  # noqa: E731
+    wb = torch.empty(4 * big, dtype=torch.int32, device=d.dev)
+    for algo in ("aca", "sks"):
+        aid = {"aca": 0, "sks": 1}[algo]
+        Hb = torch.empty((9, big), dtype=torch.float64, device=d.dev)
+        f_one = lambda: pkg._lib.call("hg_rand_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(),  # noqa: E731
+                                      ps.shape[0], SEED, Hb.data_ptr(), big, 0, stream)
+
+        def f_two():
+            pkg._lib.call("hg_rand_mrg32k3a_u32", wb.data_ptr(), 4 * big, SEED, stream)
+            pkg._lib.call("hg_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(), ps.shape[0],
+                          wb.data_ptr(), Hb.data_ptr(), big, 0, stream)
+
+        for _ in range(5):
+            f_one()
+            f_two()
+            f_write()
+        ms_one = launch_stats(d, f_one, groups=10)["median_us"] * 1e-3
+        ms_write = launch_stats(d, f_write, groups=10)["median_us"] * 1e-3
+        _, ms_two = timed_region(d, f_two, 20)
+        out[f"{algo}_large"] = {
+            "n": big, "draws_gather_solve_one_launch_us": round(ms_one * 1e3, 2),
+            "G_hyp_per_s": round(big / (ms_one * 1e-3) / 1e9, 2),
+            "gbps_H": round(big * 72 / (ms_one * 1e-3) / 1e9, 1),
+            "frac": round(big * 72 / (ms_one * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "write_only_stream_gbps": round(big * 72 / (ms_write * 1e-3) / 1e9, 1),
+            "frac_of_write_only_stream": round(ms_write / ms_one, 4),
+            "draws_then_gather_solve_us": round(ms_two * 1e3, 2)}
+        del Hb
+    del wbuf, wb
     return out
 
 
