@@ -75,7 +75,9 @@ if [[ -f "$REF_SRC" ]]; then
     echo "built oracle/_ref/libsks_ref_native.so (speed build, not bit-exact)"
 fi
 
-# The reference's own CUDA kernels, compiled by hipcc for gfx950 straight from the file
+# A STAND-IN build of the reference's CUDA kernel statements (nvcc and the CUDA headers are
+# absent: hipcc and a prepended HIP header stand in for them, so this is a cross-check of
+# statement-order IEEE evaluation, not the reference's own build), compiled for gfx950 straight from the file
 # (sed picks the kernel lines, oracle/ref_cu_driver.hip follows them in the same
 # translation unit and launches them as the reference's host code does).  -ffp-contract=off:
 # the reference's statements evaluated in order, every operation rounded on its own --

@@ -265,11 +265,12 @@ REF_CU_SO = os.environ.get("SKS_REF_CU_SO", os.path.join(HERE, "_ref", "libsks_r
 
 
 class RefCuOracle:
-    """The reference's own GPU kernels -- cal_Homo_ACA / _SKS / _GE / _GPT, lines 81-507 of
-    "GPU_Runtime Test.cu" -- compiled by hipcc from the file where it lies
-    (oracle/build.sh, oracle/ref_cu_driver.hip; -ffp-contract=off) and launched as the
-    reference's host code launches them.  SoA binary64, unnormalised (GE/GPT: H[8] = 1).
-    Runs on the GPU (a checker: tests only)."""
+    """The statements of cal_Homo_ACA / _SKS / _GE / _GPT (lines 81-507 of "GPU_Runtime
+    Test.cu") compiled by hipcc behind a prepended HIP header (oracle/build.sh,
+    oracle/ref_cu_driver.hip; -ffp-contract=off) and launched as the reference's host code
+    launches them.  A STAND-IN build (nvcc and the CUDA headers are absent): a cross-check of
+    statement-order IEEE evaluation, not the reference's own build's output.  SoA binary64,
+    unnormalised (GE/GPT: H[8] = 1).  Runs on the GPU (a checker: tests only)."""
 
     ALGO = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
 

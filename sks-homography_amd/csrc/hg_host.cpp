@@ -78,6 +78,11 @@ int classify(View& v) {
 // library-owned range as pageable, and holds a reference on each registration it uses
 // until its kernel has finished; the last reference unregisters.  A needed range that
 // overlaps registrations without lying inside one waits until they are released.
+// Consequence: two slices of one allocation run at once only when the split
+// is page-aligned or one slice's pages lie inside the other's registration; slices that
+// merely share an edge page (a split inside a page) take turns -- the second waits for the
+// first to finish, and a waiting call can be passed by calls that share an existing
+// registration.  Correctness never depends on which happens.
 struct Registration {
     host::Range r;
     int refs;

@@ -1,16 +1,17 @@
-"""The binary64 SoA kernels against the REFERENCE's own GPU kernels, bit for bit.
+"""The binary64 SoA kernels against a STAND-IN build of the reference's GPU kernel
+statements, bit for bit -- a restatement check, not a parity pin.
 
-oracle/_ref/libsks_ref_cu.so is the reference's cal_Homo_ACA / cal_Homo_SKS /
-cal_Homo_GE / cal_Homo_GPT ("GPU_Runtime Test.cu:81-507"), compiled by hipcc from the file
-where it lies with -ffp-contract=off (every operation rounded on its own, in the reference's
-statement order: the same convention as the C++ checker) and launched as the reference's
-host drivers launch them (<<<ceil(N/32), 32>>>, SoA (8,N) -> (9,N), unnormalised).  These
-pin, against the reference itself rather than a restatement:
-  * a5/a6 -- cal_Homo_ACA/SKS, the unnormalised f64 contract (hg_aca_f64 / hg_sks_f64,
-    HG_LAYOUT_SOA, flags 0), previously pinned only through the normalised C++ outputs;
-  * (f).4 -- cal_Homo_GE (hg_ge_f64) and cal_Homo_GPT (hg_gpt_f64), previously pinned
-    only by the builder's restatement (GE) or LAPACK to a tolerance (GPT);
-and the CPU oracle's restatement of the same four, on uniform, wall-pool and edge inputs.
+oracle/_ref/libsks_ref_cu.so holds the statements of cal_Homo_ACA / cal_Homo_SKS /
+cal_Homo_GE / cal_Homo_GPT ("GPU_Runtime Test.cu:81-507") compiled by hipcc behind a
+prepended HIP header (nvcc and the CUDA headers are not in the image), -ffp-contract=off
+(every operation rounded on its own, in the statement order), launched as the reference's
+host drivers launch them (<<<ceil(N/32), 32>>>, SoA (8,N) -> (9,N), unnormalised).  It
+checks that our kernels evaluate those statements in order with IEEE rounding; it does
+not show what the reference's own nvcc build produces.  What pins the rows:
+unnormalised binary64 ACA by the reference's ACA_vanilla statements run in float64
+(test_gpu_parity.py::test_golden_aca_f64_unnormalised); unnormalised binary64 SKS, GE f64
+(cal_Homo_GE) and GPT-LU (cal_Homo_GPT) by restatement only -- parity unpinned.
+Also the CPU oracle's restatement of the same four, on uniform, wall-pool and edge inputs.
 """
 import numpy as np
 import pytest

@@ -5,8 +5,8 @@ hg_rand_mrg32k3a_u32 / hg_get_rand_list_f64 / hg_gather_solve_f64.
 Pins:
   * get_rand_list: the (8,n) rows equal a numpy restatement of its statements (an exact
     gather: every bit);
-  * the fused gather + solve equals the reference's OWN cal_Homo_{ACA,SKS,GE,GPT} kernels
-    (oracle/_ref/libsks_ref_cu.so, compiled by hipcc from the .cu) run on those rows, bit for
+  * the fused gather + solve equals the cal_Homo_{ACA,SKS,GE,GPT} statements (the hipcc
+    stand-in build oracle/_ref/libsks_ref_cu.so, a cross-check -- DESIGN.md §3) run on those rows, bit for
     bit, NaN for NaN -- on the reference's own point file and on pools of arbitrary binary64
     bit patterns, through the LDS-pool form (small pools, and the 2540-pair wall file with
     the LDS opt-in) and the global-gather form (pools over 160 KiB);

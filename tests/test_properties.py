@@ -47,15 +47,16 @@ def test_oracle_recovers_true_homography_f64(oracle, case):
 def test_oracle_aca_sks_agree_f32(oracle, case):
     """Two different binary32 formulations of one homography agree to the conditioning of a
     binary32 solve: quads ~700 px from the origin and projective terms to 2e-5 leave ~1e-3
-    relative disagreement in the worst cases hypothesis finds (one found 1.08e-3), so the
-    bar is 1e-2 -- far below any real disagreement (a wrong formula is O(1) off)."""
+    relative disagreement in the worst cases of this derandomized set (the largest is
+    1.08e-3), so the bar is 2e-3, just above it (a 10x looser bar would let a
+    mis-rounded term through)."""
     src, Ht = case
     tar = _project(Ht, src)
     s = src.reshape(1, 8).astype(np.float32)
     t = tar.reshape(1, 8).astype(np.float32)
     a = oracle.solve("aca", s, t)[0].astype(np.float64)
     k = oracle.solve("sks", s, t)[0].astype(np.float64)
-    assert np.linalg.norm(a - k) / np.linalg.norm(a) < 1e-2
+    assert np.linalg.norm(a - k) / np.linalg.norm(a) < 2e-3
 
 
 @pytest.mark.gpu
