@@ -142,6 +142,18 @@ int main(int argc, char** argv) {
         std::printf("  fused gather + cal_Homo_ACA: %lld of %lld words differ from gather-then-solve\n",
                     (long long)differ, (long long)(9 * n));
         if (differ) ++failures;
+        // draws + gather + cal_Homo_ACA in one launch (the words never reach memory): the
+        // same bits again
+        CHECK(hg_rand_gather_solve_f64(HG_ALGO_ACA, d_src_in, d_tar_in, (uint32_t)npool, 11ULL, dg,
+                                       n, 0, nullptr));
+        CHECK(hipMemcpy(hf.data(), dg, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
+        differ = 0;
+        for (int64_t i = 0; i < 9 * n; ++i)
+            differ += std::memcmp(&hf[i], &ha[i], sizeof(double)) != 0 &&
+                      !(std::isnan(hf[i]) && std::isnan(ha[i]));
+        std::printf("  draws + gather + cal_Homo_ACA in one launch: %lld of %lld words differ\n",
+                    (long long)differ, (long long)(9 * n));
+        if (differ) ++failures;
         int64_t agree = 0, finite = 0;
         for (int64_t i = 0; i < n; ++i) {
             const double w = ha[8 * n + i];

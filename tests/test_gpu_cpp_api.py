@@ -57,8 +57,8 @@ def test_cpp_runtime_harness(pkg, dev, tmp_path):
     """examples/runtime_test.cpp -- the reference GPU harness's flow in native C++ over the
     C ABI: reads the reference's point-file format (written here from the committed
     orig_pts_wall.txt fixture), draws 4*N MRG32K3A words, gathers the 4-subsets on the device
-    (get_rand_list), times ACA/SKS/GPT/GE per N, checks ACA against GE and the fused gather +
-    solve against gather-then-solve bit for bit."""
+    (get_rand_list), times ACA/SKS/GPT/GE per N, checks ACA against GE, and the fused gather +
+    solve and the one-launch draws + gather + solve against gather-then-solve bit for bit."""
     import numpy as np
     from conftest import load_golden
     g = load_golden("cpp_wall.npz")
@@ -79,4 +79,5 @@ def test_cpp_runtime_harness(pkg, dev, tmp_path):
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr
     assert "cal_Homo_ACA N=100000" in r.stdout and "cal_Homo_GE  N=100000" in r.stdout
-    assert "0 of 900000 words differ" in r.stdout, r.stdout
+    assert "0 of 900000 words differ from gather-then-solve" in r.stdout, r.stdout
+    assert "one launch: 0 of 900000 words differ" in r.stdout, r.stdout
