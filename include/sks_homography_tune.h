@@ -67,6 +67,10 @@ double hg_tune_launch_loop(int algo, int elem, const void* src, const void* tar,
  * sc1 / sc1|nt, 6-11 buffer loads with the same bits (one sink dword per lane into dst). */
 int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void* stream);
 
+/* The one-launch Table-8 kernel's H store pattern alone: blocks of 1024 lanes own `classes`
+ * consecutive residue classes (64 ... 1024) and store 9 SoA rows per hypothesis. */
+int hg_tune_mrg_pattern(int classes, double* H, int64_t n, void* stream);
+
 /* Row-stream probe: RI input / RO output rows of row_bytes at pitch_bytes; variant 0 (16,9),
  * 1 (16,8), 2 (8,4), 3 (4,2), 4 (2,1), 5 (16,9) with 4 chunks per lane, 6 (32,16). */
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
@@ -110,7 +114,10 @@ int hg_tune_rocrand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, vo
 int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
                       void* stream);
 /* Fused draws + gather + solve, unnormalised ACA (0) / SKS (1): variant 0 pool in global
- * memory, 1 pool in LDS beside the draws buffers (the shipped form when it fits). */
+ * memory, 1 pool in LDS beside the draws buffers (the shipped form when it fits); 2 ... 8 the
+ * shipped form with the solve (2), the table jumps of the engine starts (3), the engine
+ * steps (4) or combinations removed (5 = 2+3, 6 = 2+4, 7 = 3+4, 8 = all) -- wrong bits,
+ * timing only. */
 int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
                                   const double* pool_tar, uint32_t size, uint64_t seed, double* H,
                                   int64_t n, void* stream);

@@ -201,7 +201,27 @@ constexpr size_t mrg_words_lds() { return (size_t)2 * 4 * 4 * (mrg_gather_block<
 constexpr int kMrgGroupBatch = 8;  // groups whose engine bases one pass makes
 constexpr size_t kMrgStaticLds = 2 * kMrgGroupBatch * 24 * 4;
 
-template <int ALGO, bool NORM, bool POOL_LDS>
+// Ablations for the tune library only (wrong bits, timing only): the shipped kernel is ABL 0.
+enum MrgAblation : int {
+    kMrgAblNone = 0,
+    kMrgAblNoSolve = 1,   // draws + gather, H = a cheap function of the gathered points
+    kMrgAblNoStart = 2,   // engines start from the host states, no table jumps
+    kMrgAblNoDraws = 4,   // no engine steps: the words are the lane's own index
+    kMrgAblNoGather = 8,  // no pool reads: the points are the words themselves
+    kMrgSt16 = 16,        // H rows stored as 16-B pairs of adjacent hypotheses (n even)
+    kMrgStDefault = 32,   // H stores with the default cache policy instead of non-temporal
+};
+
+// the value of the other lane of an even/odd lane pair (DPP quad_perm [1, 0, 3, 2])
+__device__ __forceinline__ double pair_swap(double x) {
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, 0xB1, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), 0xB1, 0xF, 0xF, false);
+    return __longlong_as_double((long long)(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo));
+}
+typedef double hg_dbl2 __attribute__((ext_vector_type(2)));
+
+template <int ALGO, bool NORM, bool POOL_LDS, int ABL = kMrgAblNone>
 __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64_kernel(
     uint32_t size, uint64_t magic, const double2* __restrict__ pool_src,
     const double2* __restrict__ pool_tar, double* __restrict__ H, int64_t n,
@@ -229,7 +249,7 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
         // of group i, row kk -- first through the table's low level, then the high one
         const int bi = threadIdx.x / 24, br = threadIdx.x % 24, bk = br / 6, bt = br % 6;
         const int64_t bg = g0 + bi * stride;
-        const bool bl = threadIdx.x < 24 * kMrgGroupBatch && bg < groups;
+        const bool bl = (ABL & kMrgAblNoStart) == 0 && threadIdx.x < 24 * kMrgGroupBatch && bg < groups;
         const int64_t braw = bg * kC + a.b[bl ? bk : 0];  // < 2^18
         const int bcarry = braw >= mrg::kOrder;
         const uint32_t bbase = (uint32_t)(braw & (mrg::kOrder - 1));
@@ -244,7 +264,10 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
         if (g >= groups) break;
         const int64_t h0 = g * kC + c;
         mrg::State st;
-        {
+        if constexpr ((ABL & kMrgAblNoStart) != 0) {
+            st = mrg::unpack(a.y[k][0]);
+            st.x1[0] += c;
+        } else {
             // the group's first class already wrapped (g C + b_k >= 2^17): every class of the
             // row is at position a_k + 1, and its base was made from y[k][1]
             const int64_t raw = g * kC + a.b[k];
@@ -262,6 +285,14 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
         // steps per phase m mod 3 (a block-uniform branch), so no step moves the state
         auto gen = [&](int buf, int phase) {
             uint32_t* w = words + (buf * 4 + k) * kQ * kC + c;
+            if constexpr ((ABL & kMrgAblNoDraws) != 0) {
+                const uint32_t x = (uint32_t)threadIdx.x * 2654435761u + (uint32_t)phase;
+                w[0] = x;
+                w[kC] = x ^ 1u;
+                w[2 * kC] = x ^ 2u;
+                w[3 * kC] = x ^ 3u;
+                return;
+            }
             auto four = [&](auto p) {
                 constexpr int P = decltype(p)::value;
                 w[0] = mrg::step<P % 3>(st);
@@ -282,14 +313,17 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
             phase = phase == 2 ? 0 : phase + 1;  // the phase of chunk q0 / 4 + 1
             if (q0 + kQ < qn) gen(buf ^ 1, phase);
             const int64_t h = h0 + ((q0 + k) << mrg::kOrderLog2);
-            if (h < n) {
+            if ((ABL & kMrgSt16) != 0 || h < n) {
                 double s[8], t[8], hh[9];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t w = words[((buf * 4 + r) * kQ + k) * kC + c];
                     const uint32_t ix = fastmod_u32(w, magic, size);
                     double2 ps, pt;
-                    if constexpr (POOL_LDS) {
+                    if constexpr ((ABL & kMrgAblNoGather) != 0) {
+                        ps = double2((double)w, (double)(w >> 1));
+                        pt = double2((double)(w >> 2), (double)(w >> 3));
+                    } else if constexpr (POOL_LDS) {
                         ps = pool[2 * ix];
                         pt = pool[2 * ix + 1];
                     } else {
@@ -299,9 +333,38 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
                     s[2 * r] = ps.x; s[2 * r + 1] = ps.y;
                     t[2 * r] = pt.x; t[2 * r + 1] = pt.y;
                 }
-                solve<ALGO, NORM>(s, t, hh);
+                if constexpr ((ABL & kMrgAblNoSolve) != 0) {
 #pragma unroll
-                for (int r = 0; r < 9; ++r) __builtin_nontemporal_store(hh[r], H + h + r * n);
+                    for (int r = 0; r < 8; ++r) hh[r] = s[r] + t[7 - r];
+                    hh[8] = s[0];
+                } else {
+                    solve<ALGO, NORM>(s, t, hh);
+                }
+                if constexpr ((ABL & kMrgSt16) != 0) {
+                    // even lane: row r of (h, h + 1); odd lane: row r + 1 of (h - 1, h)
+                    const int odd = threadIdx.x & 1;
+                    const int64_t he = h - odd;
+#pragma unroll
+                    for (int r = 0; r < 8; r += 2) {
+                        const double got = pair_swap(odd ? hh[r] : hh[r + 1]);
+                        const hg_dbl2 v = odd ? hg_dbl2{got, hh[r + 1]} : hg_dbl2{hh[r], got};
+                        hg_dbl2* p = reinterpret_cast<hg_dbl2*>(H + (r + odd) * n + he);
+                        if (he < n) {
+                            if constexpr ((ABL & kMrgStDefault) != 0) *p = v;
+                            else __builtin_nontemporal_store(v, p);
+                        }
+                    }
+                    if (h < n) {
+                        if constexpr ((ABL & kMrgStDefault) != 0) H[h + 8 * n] = hh[8];
+                        else __builtin_nontemporal_store(hh[8], H + h + 8 * n);
+                    }
+                } else if constexpr ((ABL & kMrgStDefault) != 0) {
+#pragma unroll
+                    for (int r = 0; r < 9; ++r) H[h + r * n] = hh[r];
+                } else {
+#pragma unroll
+                    for (int r = 0; r < 9; ++r) __builtin_nontemporal_store(hh[r], H + h + r * n);
+                }
             }
             __syncthreads();
         }
@@ -342,7 +405,7 @@ inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t
 
 // variant: -1 shipped (pool in LDS when it fits beside the draws buffer), 0 pool in global
 // memory
-template <int ALGO, bool NORM>
+template <int ALGO, bool NORM, int ABL = kMrgAblNone>
 inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32_t size,
                                     uint64_t seed, double* H, int64_t n, hipStream_t s,
                                     int variant = -1) {
@@ -366,8 +429,8 @@ inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32
     const size_t words = mrg_words_lds<ALGO>();
     const bool pool_lds = variant != 0 && kMrgStaticLds + words + (size_t)size * 32 <= kLdsMax;
     const size_t lds = pool_lds ? words + (size_t)size * 32 : words;
-    auto k = pool_lds ? mrg_gather_solve_f64_kernel<ALGO, NORM, true>
-                      : mrg_gather_solve_f64_kernel<ALGO, NORM, false>;
+    auto k = pool_lds ? mrg_gather_solve_f64_kernel<ALGO, NORM, true, ABL>
+                      : mrg_gather_solve_f64_kernel<ALGO, NORM, false, ABL>;
     if (lds + kMrgStaticLds > kSampleLdsMax && !lds_opt_in(k, kMrgStaticLds))
         return (int)hipErrorInvalidValue;
     int64_t per_cu = (int64_t)(kLdsMax / (lds + kMrgStaticLds));

@@ -438,6 +438,77 @@ int hg_tune_policy(int variant, const void* src, void* dst, int64_t bytes, void*
     return (int)hipGetLastError();
 }
 
+// The one-launch Table-8 kernel's H store pattern alone (no LDS, no barriers): block g owns
+// C consecutive residue classes (mod 2^17) and walks their positions Q at a time, lane
+// (qq, c) storing the 9 SoA rows of hypothesis g C + c + (q0 + qq) 2^17 (8-B nt stores).
+// C = 256, Q = 4 is the shipped kernel's shape.
+}  // extern "C"
+
+template <int C>
+__global__ __launch_bounds__(1024) void mrg_pattern_kernel(double* __restrict__ H, int64_t n) {
+    constexpr int Q = 1024 / C;
+    const int qq = threadIdx.x / C, c = threadIdx.x % C;
+    const int64_t groups = ((n < (1 << 17) ? n : (1 << 17)) + C - 1) / C;
+    for (int64_t g = blockIdx.x; g < groups; g += gridDim.x) {
+        const int64_t h0 = g * C + c;
+        const int64_t qn = (n - g * C + (1 << 17) - 1) >> 17;
+        for (int64_t q0 = 0; q0 < qn; q0 += Q) {
+            const int64_t h = h0 + ((q0 + qq) << 17);
+            if (h < n) {
+#pragma unroll
+                for (int r = 0; r < 9; ++r) __builtin_nontemporal_store((double)(h + r), H + h + r * n);
+            }
+        }
+    }
+}
+
+// the same 9 SoA rows written in hypothesis order (grid-stride, 8-B nt stores), and one row
+// (W = 16: two hypotheses per lane, 16-B stores; NT: non-temporal or default policy)
+template <int R, int W = 8, bool NT = true>
+__global__ __launch_bounds__(1024) void seq_rows_kernel(double* __restrict__ H, int64_t n) {
+    typedef double d2 __attribute__((ext_vector_type(2)));
+    constexpr int P = W / 8;
+    for (int64_t h = ((int64_t)blockIdx.x * 1024 + threadIdx.x) * P; h < n;
+         h += (int64_t)gridDim.x * 1024 * P) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            if constexpr (W == 16) {
+                const d2 v = {(double)(h + r), (double)(h + r + 1)};
+                if constexpr (NT) __builtin_nontemporal_store(v, reinterpret_cast<d2*>(H + h + r * n));
+                else *reinterpret_cast<d2*>(H + h + r * n) = v;
+            } else {
+                if constexpr (NT) __builtin_nontemporal_store((double)(h + r), H + h + r * n);
+                else H[h + r * n] = (double)(h + r);
+            }
+        }
+    }
+}
+
+extern "C" {
+
+int hg_tune_mrg_pattern(int classes, double* H, int64_t n, void* stream) {
+    if (n <= 0 || !H) return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const unsigned grid = (unsigned)hg::cu_count();
+    switch (classes) {
+        case 0: seq_rows_kernel<9><<<grid * 8, 1024, 0, st>>>(H, n); break;    // 9 rows, h in order
+        case 1: seq_rows_kernel<1><<<grid * 8, 1024, 0, st>>>(H, 9 * n); break;  // one row of 9 n
+        case 2: seq_rows_kernel<1, 16, true><<<grid * 8, 1024, 0, st>>>(H, 9 * n); break;
+        case 3: seq_rows_kernel<1, 8, false><<<grid * 8, 1024, 0, st>>>(H, 9 * n); break;
+        case 4: seq_rows_kernel<1, 16, false><<<grid * 8, 1024, 0, st>>>(H, 9 * n); break;
+        case 5: seq_rows_kernel<9, 16, true><<<grid * 8, 1024, 0, st>>>(H, n); break;
+        case 6: seq_rows_kernel<9, 16, false><<<grid * 8, 1024, 0, st>>>(H, n); break;
+        case 7: seq_rows_kernel<9, 8, false><<<grid * 8, 1024, 0, st>>>(H, n); break;
+        case 64: mrg_pattern_kernel<64><<<grid, 1024, 0, st>>>(H, n); break;
+        case 128: mrg_pattern_kernel<128><<<grid, 1024, 0, st>>>(H, n); break;
+        case 256: mrg_pattern_kernel<256><<<grid, 1024, 0, st>>>(H, n); break;
+        case 512: mrg_pattern_kernel<512><<<grid, 1024, 0, st>>>(H, n); break;
+        case 1024: mrg_pattern_kernel<1024><<<grid, 1024, 0, st>>>(H, n); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
 // Row-stream probe: variant -> (RI, RO, U); see row_streams.  in / out hold RI / RO rows
 // of row_bytes at a pitch of pitch_bytes (both multiples of 16).
 int hg_tune_streams(int variant, const void* in, void* out, int64_t row_bytes,
@@ -800,18 +871,61 @@ int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_c
 }
 
 // Fused draws + gather + solve (unnormalised ACA / SKS): 0 = pool in global memory,
-// 1 = pool in LDS beside the draws buffer (shipped when it fits).
+// 1 = pool in LDS beside the draws buffer (shipped when it fits); 2 ... 8 = the shipped
+// form with parts removed (wrong bits, timing only: where the launch's time goes) --
+// 2 no solve, 3 no table jumps at the engine starts, 4 no engine steps, 5 = 2 + 3,
+// 6 = 2 + 4, 7 = 3 + 4, 8 = all three (the gather and the H stores alone).
+}  // extern "C"
+
+template <int ALGO>
+static int rand_gather_variant(int variant, const double2* ps, const double2* pt, uint32_t size,
+                               uint64_t seed, double* H, int64_t n, hipStream_t s) {
+    using namespace hg;
+    switch (variant) {
+        case 0: return launch_rand_gather_solve<ALGO, false>(ps, pt, size, seed, H, n, s, 0);
+        case 1: return launch_rand_gather_solve<ALGO, false>(ps, pt, size, seed, H, n, s, -1);
+        case 2: return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve>(ps, pt, size, seed, H, n, s);
+        case 3: return launch_rand_gather_solve<ALGO, false, kMrgAblNoStart>(ps, pt, size, seed, H, n, s);
+        case 4: return launch_rand_gather_solve<ALGO, false, kMrgAblNoDraws>(ps, pt, size, seed, H, n, s);
+        case 5: return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart>(ps, pt, size, seed, H, n, s);
+        case 6: return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoDraws>(ps, pt, size, seed, H, n, s);
+        case 7: return launch_rand_gather_solve<ALGO, false, kMrgAblNoStart | kMrgAblNoDraws>(ps, pt, size, seed, H, n, s);
+        case 8:
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart | kMrgAblNoDraws>(
+                ps, pt, size, seed, H, n, s);
+        case 9:  // the H stores alone (no draws, starts, pool reads or solve)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart | kMrgAblNoDraws |
+                                                         kMrgAblNoGather>(ps, pt, size, seed, H, n, s);
+        case 10:  // shipped + 16-B paired stores (bit-exact; n even, H 16-B aligned)
+            return launch_rand_gather_solve<ALGO, false, kMrgSt16>(ps, pt, size, seed, H, n, s);
+        case 12:  // 9 with the pool left in global memory (no 81 KB LDS copy: 2 blocks per CU)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart | kMrgAblNoDraws |
+                                                         kMrgAblNoGather>(ps, pt, size, seed, H, n, s, 0);
+        case 13:  // shipped with default-policy stores
+            return launch_rand_gather_solve<ALGO, false, kMrgStDefault>(ps, pt, size, seed, H, n, s);
+        case 14:  // shipped with default-policy 16-B paired stores
+            return launch_rand_gather_solve<ALGO, false, kMrgSt16 | kMrgStDefault>(ps, pt, size, seed, H, n, s);
+        case 11:  // 9 with 16-B paired stores
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart | kMrgAblNoDraws |
+                                                         kMrgAblNoGather | kMrgSt16>(ps, pt, size, seed, H, n, s);
+        default: return (int)hipErrorInvalidValue;
+    }
+}
+
+extern "C" {
+
 int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
                                   const double* pool_tar, uint32_t size, uint64_t seed, double* H,
                                   int64_t n, void* stream) {
-    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 1)
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 14)
+        return (int)hipErrorInvalidValue;
+    if ((variant == 10 || variant == 11 || variant == 14) && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15)))
         return (int)hipErrorInvalidValue;
     const auto* ps = reinterpret_cast<const double2*>(pool_src);
     const auto* pt = reinterpret_cast<const double2*>(pool_tar);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int v = variant == 0 ? 0 : -1;
-    return algo == 0 ? hg::launch_rand_gather_solve<hg::kACA, false>(ps, pt, size, seed, H, n, s, v)
-                     : hg::launch_rand_gather_solve<hg::kSKS, false>(ps, pt, size, seed, H, n, s, v);
+    return algo == 0 ? rand_gather_variant<hg::kACA>(variant, ps, pt, size, seed, H, n, s)
+                     : rand_gather_variant<hg::kSKS>(variant, ps, pt, size, seed, H, n, s);
 }
 
 }  // extern "C"
