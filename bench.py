@@ -689,10 +689,19 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
     f_roc()
     _, ms_roc = timed_region(d, f_roc, 5)
     f_draw()
+    # the launch's yardstick: a write-only stream of the same 16 B per hypothesis (16-B stores)
+    wsmall = torch.empty(4 * n, dtype=torch.int32, device=d.dev)
+    f_wsmall = lambda: wr(5, None, wsmall.data_ptr(), 4 * n * 4, stream)  # noqa: E731
+    for _ in range(5):
+        f_wsmall()
+    ms_wsmall = launch_stats(d, f_wsmall, groups=20)["median_us"] * 1e-3
+    del wsmall
     rl = words.view(4, n)
     out = {"n": n, "pool": int(ps.shape[0]),
            "draws": {"words": 4 * n, "us": round(ms_draw * 1e3, 2),
                      "gbps_written": round(4 * n * 4 / (ms_draw * 1e-3) / 1e9, 1),
+                     "write_only_stream_us": round(ms_wsmall * 1e3, 2),
+                     "frac_of_write_only_stream": round(ms_wsmall / ms_draw, 4),
                      "rocrand_generate_us": round(ms_roc * 1e3, 1),
                      "speedup_vs_rocrand": round(ms_roc / ms_draw, 1),
                      "bit_identical_to_rocrand": bool(torch.equal(words, ref_words))}}

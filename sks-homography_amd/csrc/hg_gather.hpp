@@ -42,13 +42,18 @@ __device__ __forceinline__ uint32_t mrg_entry_dot(const uint32_t* e, int t, cons
 // its own l < 256 and writes its positions -- lane-consecutive subsequences, so every store
 // instruction covers 256 contiguous bytes.  Default-policy stores: the words are read again
 // by the gather that follows, from the MALL when they fit.
+// ABL (tune library only, wrong bits): 1 no table jumps (the lane starts from y[j]), 2 no
+// engine steps (the words are the lane's index)
+template <int ABL = 0>
 __global__ __launch_bounds__(kBlock) void mrg_words_kernel(uint32_t* __restrict__ out,
                                                            mrg::WordsArgs a) {
     static_assert(kBlock == mrg::kLo, "one table row per lane");
     __shared__ uint32_t base[6];
     const int j = blockIdx.y;
-    if (threadIdx.x < 6) base[threadIdx.x] = mrg_entry_dot(kMrgJump.hi[blockIdx.x], threadIdx.x, a.y[j].w);
-    __syncthreads();
+    if constexpr ((ABL & 1) == 0) {
+        if (threadIdx.x < 6) base[threadIdx.x] = mrg_entry_dot(kMrgJump.hi[blockIdx.x], threadIdx.x, a.y[j].w);
+        __syncthreads();
+    }
     const int64_t s = (int64_t)blockIdx.x * kBlock + threadIdx.x;
     const int64_t cols = a.count < mrg::kOrder ? a.count : mrg::kOrder;
     if (s >= cols) return;
@@ -56,13 +61,24 @@ __global__ __launch_bounds__(kBlock) void mrg_words_kernel(uint32_t* __restrict_
     const int64_t q = (int64_t)j * a.chunk;
     const int64_t q_end = q + a.chunk < q_end_s ? q + a.chunk : q_end_s;
     if (q >= q_end) return;
-    const uint32_t v[6] = {base[0], base[1], base[2], base[3], base[4], base[5]};
-    mrg::State st = mrg_apply_lo(threadIdx.x, v);
+    mrg::State st;
+    if constexpr ((ABL & 1) != 0) {
+        st = mrg::unpack(a.y[j]);
+        st.x1[0] += threadIdx.x;
+    } else {
+        const uint32_t v[6] = {base[0], base[1], base[2], base[3], base[4], base[5]};
+        st = mrg_apply_lo(threadIdx.x, v);
+    }
     // block-uniform base pointer (positions advance it), the lane's subsequence as offset
     uint32_t* o = out + (q << mrg::kOrderLog2) + (int64_t)blockIdx.x * kBlock;
     const uint32_t lane = threadIdx.x;
     const int64_t left = q_end - q;
     int64_t i = 0;
+    if constexpr ((ABL & 2) != 0) {
+        const uint32_t x = (uint32_t)__double2hiint(st.x1[0]) ^ lane;
+        for (; i < left; ++i, o += mrg::kOrder) o[lane] = x + (uint32_t)i;
+        return;
+    }
     for (; i + 3 <= left; i += 3, o += 3 * mrg::kOrder) {  // three steps: the state stays put
         o[lane] = mrg::step<0>(st);
         o[mrg::kOrder + lane] = mrg::step<1>(st);
@@ -384,6 +400,7 @@ inline mrg::Packed mrg_seed_jump(uint64_t seed, uint64_t e) {  // A^e x0(seed)
 // over more threads (each thread's start costs four 3x3 products mod m).
 constexpr int64_t kMrgMinChunk = 64;
 
+template <int ABL = 0>
 inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
                             hipStream_t s) {
     mrg::WordsArgs a{};
@@ -400,7 +417,7 @@ inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t
                            mrg::host_jump(kMrgPow.p2, 2, (uint64_t)(j * a.chunk), x2));
     const int64_t cols = count < mrg::kOrder ? count : mrg::kOrder;
     const dim3 grid((unsigned)((cols + kBlock - 1) / kBlock), (unsigned)chunks);
-    return launch(mrg_words_kernel, grid, dim3(kBlock), 0, s, out, a);
+    return launch(mrg_words_kernel<ABL>, grid, dim3(kBlock), 0, s, out, a);
 }
 
 // variant: -1 shipped (pool in LDS when it fits beside the draws buffer), 0 pool in global

@@ -864,10 +864,20 @@ int hg_tune_rocrand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, vo
 }
 
 // The standalone generator with another split threshold (positions per thread).
+// min_chunk >= 2^20 + 1 ... : ablations (wrong bits, timing only) at the shipped split --
+// 2^20 + 1 no table jumps, 2^20 + 2 no engine steps, 2^20 + 3 neither.
 int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
                       void* stream) {
     if (count <= 0 || !out || min_chunk < 1) return (int)hipErrorInvalidValue;
-    return hg::launch_mrg_words(out, count, seed, min_chunk, reinterpret_cast<hipStream_t>(stream));
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t abl = min_chunk > (1 << 20) ? min_chunk - (1 << 20) : 0;
+    switch (abl) {
+        case 0: return hg::launch_mrg_words(out, count, seed, min_chunk, s);
+        case 1: return hg::launch_mrg_words<1>(out, count, seed, hg::kMrgMinChunk, s);
+        case 2: return hg::launch_mrg_words<2>(out, count, seed, hg::kMrgMinChunk, s);
+        case 3: return hg::launch_mrg_words<3>(out, count, seed, hg::kMrgMinChunk, s);
+        default: return (int)hipErrorInvalidValue;
+    }
 }
 
 // Fused draws + gather + solve (unnormalised ACA / SKS): 0 = pool in global memory,

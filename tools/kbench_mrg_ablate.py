@@ -41,6 +41,23 @@ def main():
     pt = torch.from_numpy(g["pool_tar"].astype(np.float64)).to(dev)
     sizes = [int(x) for x in os.environ.get("KB_SIZES", "1000000,10000000").split(",")]
     out = {}
+    # the standalone words kernel: shipped, without the table jumps, without the engine steps,
+    # without both (hg_tune_mrg_words min_chunk 2^20 + 1 / 2 / 3), and a write-only stream of
+    # the same bytes (hg_tune_copy variant 5)
+    t.hg_tune_mrg_words.argtypes = [vp, i64, u64, i64, vp]
+    t.hg_tune_copy.argtypes = [ctypes.c_int, vp, vp, i64, vp]
+    for count in (4 * s_ for s_ in sizes):
+        wb = torch.empty(count, dtype=torch.int32, device=dev)
+        fns = {name: (lambda a=a: t.hg_tune_mrg_words(wb.data_ptr(), count, 11, a, st))
+               for name, a in (("words_shipped", 64), ("words_no_start", (1 << 20) + 1),
+                               ("words_no_steps", (1 << 20) + 2), ("words_neither", (1 << 20) + 3))}
+        fns["write_only"] = lambda: t.hg_tune_copy(5, None, wb.data_ptr(), count * 4, st)
+        for f in fns.values():
+            assert f() == 0
+        r = timeit(fns, 20)
+        out[f"words {count}"] = r
+        print("words", count, r, flush=True)
+        del wb
     for algo, aid in (("aca", 0), ("sks", 1)):
         for n in sizes:
             H = torch.empty((9, n), dtype=torch.float64, device=dev)

@@ -23,7 +23,7 @@ import statistics
 import sys
 
 KEYS = {
-    # key: (kernel-name prefix, algorithmic bytes per launch or None, grid filter)
+    # key: (a substring of the kernel name, algorithmic bytes per launch or None)
     "aca_f32_aos_norm": ("void hg::solve_aos<0, true, float", 10_000_000 * 100),
     "sks_f32_aos_norm": ("void hg::solve_aos<1, true, float", 10_000_000 * 100),
     "stream_copy": ("hg::stream_copy_kernel", None),
@@ -33,7 +33,7 @@ KEYS = {
     "solve_soa": ("void hg::solve_soa_vec", None),
     "gather_solve_f64_aca": ("void hg::gather_solve_f64_kernel<0", 10_000_000 * 88),
     # round 3: the MRG32K3A draws alone (40 M words) and fused with the gather + solve
-    "mrg_words": ("hg::mrg_words_kernel", 40_000_000 * 4),
+    "mrg_words": ("hg::mrg_words_kernel<0>", 40_000_000 * 4),  # r03: "hg::mrg_words_kernel(" before the ablation template
     "rand_gather_solve_f64_aca": ("void hg::mrg_gather_solve_f64_kernel<0", 10_000_000 * 72),
 }
 
@@ -51,10 +51,10 @@ def main():
     out_path = sys.argv[3] if len(sys.argv) > 3 else None
     res = {}
     for key, (prefix, algo_bytes) in KEYS.items():
-        groups = sorted({g for (k, g) in fetch if k.startswith(prefix)})
+        groups = sorted({g for (k, g) in fetch if prefix in k})
         for g in groups:
-            f = [v for (k, gg), vs in fetch.items() if k.startswith(prefix) and gg == g for v in vs]
-            w = [v for (k, gg), vs in write.items() if k.startswith(prefix) and gg == g for v in vs]
+            f = [v for (k, gg), vs in fetch.items() if prefix in k and gg == g for v in vs]
+            w = [v for (k, gg), vs in write.items() if prefix in k and gg == g for v in vs]
             if not f or not w:
                 continue
             fb = statistics.median(f) * 1024 * 2
