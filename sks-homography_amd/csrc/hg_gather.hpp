@@ -13,7 +13,7 @@
 
 namespace hg {
 
-// J^l and J^(512 h) for the subsequence jumps, evaluated by the compiler (internal linkage:
+// J^l and J^(256 h) for the subsequence jumps, evaluated by the compiler (internal linkage:
 // each translation unit holds its own copy of the 61 KiB)
 static __constant__ mrg::JumpTable kMrgJump = mrg::make_jump_table();
 static constexpr mrg::PowTable kMrgPow = mrg::make_pow_table();
