@@ -317,9 +317,13 @@ double oracle_time_f32(int algo, const float* src, const float* tar, float* H, i
 
 /* ------------------------------------------------- TensorACA backward ------ */
 /* dL/dtar, dL/dsrc (M's x, y), dL/dscale, dL/ddiv for TensorACA_rect given
- * dL/dH -- the gradient ATen autograd produces for .py:294-302,
- * restated in the product kernel's fixed evaluation order (every op rounded on its
- * own except the forward's cross-product FMAs).  gsd: (B,2) per-problem partials. */
+ * dL/dH -- the gradient ATen autograd produces through the reference statements
+ * (.py:296-302), op for op in the autograd graph's CPU order: H assembled in
+ * place (columns 0 and 1 read back by column 2; zero-filled slice gradients add +0),
+ * dL/dh_temp accumulated from scale*h_temp, div's column, then column 0; sums to broadcast
+ * shapes from +0; the cross product's backward is ATen's FMA-contracted cross again.
+ * Pinned by tests/golden/torch_rect_grad.npz.  dL/dsrc is an extension (autograd cannot
+ * differentiate the in-place statements w.r.t. src).  gsd: (B,2) per-problem partials. */
 static void rect_grad_one(const float* s, const float* t, const float* g, const float* sc,
                           const float* dv, float* gs, float* gt, float* gsr, float* gdr,
                           float* gsc_sum, float* gdv_sum) {
@@ -330,40 +334,41 @@ static void rect_grad_one(const float* s, const float* t, const float* g, const 
     float c1 = fmaf(az, bx, -(ax * bz));
     float c2 = fmaf(ax, by, -(ay * bx));
     float S = ((c0 + c1) + c2) + 0.f;
-    float gc0 = 0.f, gc1 = 0.f, gS = 0.f, gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
+    float gh0[3], gy[3], ght[3], gmx = 0.f, gmy = 0.f, gsc = 0.f, gdv = 0.f;
     for (int r = 0; r < 3; ++r) {
         float br = S * t[4 * r];
         float h0 = t[4 * r + 1] * c0 - br;
         float x = t[4 * r + 2] * c1 - br;
         float h1 = dv[r] * x;
         float g2 = g[3 * r + 2];
-        float gh0 = g[3 * r + 0] - mx * g2;
-        float gh1 = g[3 * r + 1] - my * g2;
+        gh0[r] = (g[3 * r + 0] - mx * g2) + 0.f;   /* + the zero-filled slice gradient */
+        float gh1 = (g[3 * r + 1] - my * g2) + 0.f;
         gmx = gmx - g2 * h0;
         gmy = gmy - g2 * h1;
         gsr[r] = g2 * br;
         gsc = gsc + gsr[r];
-        float gx = dv[r] * gh1;
+        gy[r] = dv[r] * gh1;
         gdr[r] = gh1 * x;
         gdv = gdv + gdr[r];
-        float gb = (sc[r] * g2 - gh0) - gx;
-        gt[4 * r + 0] = gb * S;
-        gt[4 * r + 1] = gh0 * c0;
-        gt[4 * r + 2] = gx * c1;
-        gt[4 * r + 3] = 0.f;
-        gc0 = gc0 + gh0 * t[4 * r + 1];
-        gc1 = gc1 + gx * t[4 * r + 2];
-        gS = gS + gb * t[4 * r];
+        ght[r] = (sc[r] * g2 - gy[r]) - gh0[r];     /* arrival order of dL/dh_temp */
     }
-    gc0 = gc0 + gS;
-    gc1 = gc1 + gS;
-    float gc2 = gS;
-    float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
-    float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
-    gt[5] = gt[5] + gax; gt[6] = gt[6] + gay; gt[7] = gt[7] + gaz;
-    gt[4] = gt[4] - ((gax + gay) + gaz);
-    gt[1] = gt[1] + gbx; gt[2] = gt[2] + gby; gt[3] = gt[3] + gbz;
-    gt[0] = gt[0] - ((gbx + gby) + gbz);
+    float gS = ((ght[0] * t[0] + ght[1] * t[4]) + ght[2] * t[8]) + 0.f;
+    float s0 = ((gh0[0] * t[1] + gh0[1] * t[5]) + gh0[2] * t[9]) + 0.f;
+    float s1 = ((gy[0] * t[2] + gy[1] * t[6]) + gy[2] * t[10]) + 0.f;
+    float gc0 = (gS + s0) + 0.f, gc1 = (gS + s1) + 0.f, gc2 = gS + 0.f;
+    /* Q4 = a x b, a = D's y row, b = its x row: dL/da = b x gc, dL/db = gc x a */
+    float d[3][3] = {{fmaf(gc1, az, -(gc2 * ay)) + 0.f, fmaf(gc2, ax, -(gc0 * az)) + 0.f,
+                      fmaf(gc0, ay, -(gc1 * ax)) + 0.f},
+                     {fmaf(by, gc2, -(bz * gc1)) + 0.f, fmaf(bz, gc0, -(bx * gc2)) + 0.f,
+                      fmaf(bx, gc1, -(by * gc0)) + 0.f},
+                     {0.f, 0.f, 0.f}};
+    for (int r = 0; r < 3; ++r) {
+        float sneg = (((-d[r][0]) + (-d[r][1])) + (-d[r][2])) + 0.f;
+        gt[4 * r + 0] = (ght[r] * S + sneg) + 0.f;
+        gt[4 * r + 1] = (d[r][0] + gh0[r] * c0) + 0.f;
+        gt[4 * r + 2] = (d[r][1] + gy[r] * c1) + 0.f;
+        gt[4 * r + 3] = d[r][2] + 0.f;
+    }
     for (int k = 0; k < 12; ++k) gs[k] = 0.f;
     gs[0] = gmx;
     gs[4] = gmy;

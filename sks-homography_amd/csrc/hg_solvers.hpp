@@ -416,11 +416,23 @@ __device__ __forceinline__ void rect_target_from_offsets(float mx, float my, flo
     tr[8] = tr[9] = tr[10] = tr[11] = 1.f;
 }
 
-// Reverse-mode derivative of tensor_aca_rect_solve (the gradients ATen autograd
-// gives the reference's composed TensorACA_rect, .py:294-302).
-// In: the forward's inputs and g = dL/dH (3x3).  Out: gt = dL/dtar (3,4), gmx/gmy =
-// dL/d src[0][0], src[1][0], gscale / gdiv = this problem's share of dL/dscale,
-// dL/ddiv.  Fixed evaluation order (restated op for op in oracle/hg_oracle.c).
+// Reverse-mode derivative of tensor_aca_rect_solve: the gradients ATen autograd gives
+// through the reference's own statements (.py:296-302), op for op as the
+// autograd graph evaluates them on the CPU (restated in oracle/hg_oracle.c, pinned by
+// tests/golden/torch_rect_grad.npz):
+//   * H is assembled in place from zeros, and column 2 reads columns 0 and 1 back: dL/dH's
+//     columns 0 and 1 gain  -src * g2  and a zero-filled slice gradient (+0);
+//   * dL/dh_temp accumulates in the order the graph delivers it: from scale*h_temp, then
+//     from div's column, then from column 0;
+//   * every reduction to a broadcast operand's shape (sum_to_size) and every sum with a
+//     zero-filled slice gradient (slices of D, Q4, tar) ends in + 0 (ATen's accumulators
+//     start from +0, so a sum of -0 terms gives +0);
+//   * the cross product's backward is ATen's cross again (dL/da = b x gc, dL/db = gc x a),
+//     one product per component contracted into an FMA like the forward.
+// In: the forward's inputs and g = dL/dH (3x3).  Out: gt = dL/dtar (3,4); gmx/gmy = dL/d
+// src[0][0], src[1][0] (an extension: the reference statements cannot differentiate src --
+// autograd refuses the in-place H); gscale / gdiv = this problem's share of dL/dscale,
+// dL/ddiv (three-row sums from +0, as sum_to_size gives a (B,1,1) parameter).
 // Row form: per-row scale / div (as tensor_aca_rect_solve_rows), and each row's own share of
 // dL/dscale[r], dL/ddiv[r] in gsr / gdr beside the per-problem sums gscale / gdiv.
 __device__ __forceinline__ void tensor_aca_rect_grad_rows(
@@ -433,7 +445,7 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
     const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
     const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
     const float sum = ((c0 + c1) + c2) + 0.f;  // torch.sum starts from +0
-    float gc0 = 0.f, gc1 = 0.f, gs = 0.f;
+    float gh0[3], gy[3], ght[3];
     gmx = 0.f; gmy = 0.f; gscale = 0.f; gdiv = 0.f;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
@@ -442,38 +454,41 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
         const float x = tr[4 * r + 2] * c1 - b;
         const float h1 = div[r] * x;
         const float g2 = g[3 * r + 2];
-        const float gh0 = g[3 * r + 0] - mx * g2;
-        const float gh1 = g[3 * r + 1] - my * g2;
+        gh0[r] = (g[3 * r + 0] - mx * g2) + 0.f;
+        const float gh1 = (g[3 * r + 1] - my * g2) + 0.f;
         gmx = gmx - g2 * h0;
         gmy = gmy - g2 * h1;
         gsr[r] = g2 * b;
         gscale = gscale + gsr[r];
-        const float gx = div[r] * gh1;
+        gy[r] = div[r] * gh1;
         gdr[r] = gh1 * x;
         gdiv = gdiv + gdr[r];
-        const float gb = (scale[r] * g2 - gh0) - gx;
-        gt[4 * r + 0] = gb * sum;
-        gt[4 * r + 1] = gh0 * c0;
-        gt[4 * r + 2] = gx * c1;
-        gt[4 * r + 3] = 0.f;
-        gc0 = gc0 + gh0 * tr[4 * r + 1];
-        gc1 = gc1 + gx * tr[4 * r + 2];
-        gs = gs + gb * tr[4 * r];
+        ght[r] = (scale[r] * g2 - gy[r]) - gh0[r];
     }
-    gc0 = gc0 + gs;
-    gc1 = gc1 + gs;
-    const float gc2 = gs;
-    // c = a x b:  dL/da = b x gc,  dL/db = gc x a
-    const float gax = by * gc2 - bz * gc1, gay = bz * gc0 - bx * gc2, gaz = bx * gc1 - by * gc0;
-    const float gbx = gc1 * az - gc2 * ay, gby = gc2 * ax - gc0 * az, gbz = gc0 * ay - gc1 * ax;
-    gt[5] = gt[5] + gax;
-    gt[6] = gt[6] + gay;
-    gt[7] = gt[7] + gaz;
-    gt[4] = gt[4] - ((gax + gay) + gaz);
-    gt[1] = gt[1] + gbx;
-    gt[2] = gt[2] + gby;
-    gt[3] = gt[3] + gbz;
-    gt[0] = gt[0] - ((gbx + gby) + gbz);
+    // dL/dsum, dL/dQ4[0], dL/dQ4[1]: sums over the rows to the (B,1,1) shapes
+    const float gS = ((ght[0] * tr[0] + ght[1] * tr[4]) + ght[2] * tr[8]) + 0.f;
+    const float s0 = ((gh0[0] * tr[1] + gh0[1] * tr[5]) + gh0[2] * tr[9]) + 0.f;
+    const float s1 = ((gy[0] * tr[2] + gy[1] * tr[6]) + gy[2] * tr[10]) + 0.f;
+    const float gc0 = (gS + s0) + 0.f, gc1 = (gS + s1) + 0.f, gc2 = gS + 0.f;
+    // Q4 = a x b (a = D's y row, b = its x row): dL/da = b x gc, dL/db = gc x a
+    float d[2][3];
+    d[1][0] = __builtin_fmaf(by, gc2, -(bz * gc1)) + 0.f;
+    d[1][1] = __builtin_fmaf(bz, gc0, -(bx * gc2)) + 0.f;
+    d[1][2] = __builtin_fmaf(bx, gc1, -(by * gc0)) + 0.f;
+    d[0][0] = __builtin_fmaf(gc1, az, -(gc2 * ay)) + 0.f;
+    d[0][1] = __builtin_fmaf(gc2, ax, -(gc0 * az)) + 0.f;
+    d[0][2] = __builtin_fmaf(gc0, ay, -(gc1 * ax)) + 0.f;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        // D = tar[:, :, 1:] - tar[:, :, 0:1]; D's w row has no gradient (+0)
+        const float d0 = r < 2 ? d[r][0] : 0.f, d1 = r < 2 ? d[r][1] : 0.f;
+        const float d2 = r < 2 ? d[r][2] : 0.f;
+        const float sneg = (((-d0) + (-d1)) + (-d2)) + 0.f;
+        gt[4 * r + 0] = (ght[r] * sum + sneg) + 0.f;
+        gt[4 * r + 1] = (d0 + gh0[r] * c0) + 0.f;
+        gt[4 * r + 2] = (d1 + gy[r] * c1) + 0.f;
+        gt[4 * r + 3] = d2 + 0.f;
+    }
 }
 
 __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,

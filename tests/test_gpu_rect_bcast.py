@@ -9,8 +9,11 @@ Pins (tests/golden/torch_rect_bcast.npz: the reference's own statements on CPU t
     through torch.ops.sks_amd.tensor_aca_rect, reference_api.TensorACA_rect and the C ABI;
   * every shape it refuses raises;
   * the backward returns gradients shaped like scale / div: bit for bit the oracle's per-row
-    partials reduced in hg_sum_rows_f32's order, and within 1e-5 (of the largest magnitude)
-    of ATen autograd through the reference statements (the measured gap is printed).
+    partials reduced in hg_sum_rows_f32's order; against ATen autograd through the reference
+    statements dL/dtar is bit for bit, and so are dL/dscale, dL/ddiv wherever ATen reduces
+    them per problem or not at all; a parameter without a batch dimension is summed over the
+    batch in ATen's own vectorised order, so there the bar is 1e-5 of the largest magnitude
+    (the measured gap is printed).
 """
 import numpy as np
 import pytest
@@ -87,6 +90,14 @@ def _reduce_like(part_rows, part_prob, shape, B):
     return _sum_rows_restated(part_prob.reshape(1, B)).reshape(shape)
 
 
+def _batch_summed(shape, B):
+    """Whether ATen reduces a parameter of this shape over the batch (no B dimension)."""
+    sz = list(shape)
+    while len(sz) > 3 and sz[0] == 1:
+        sz = sz[1:]
+    return ([1] * (3 - len(sz)) + sz)[0] != B
+
+
 def test_backward_shapes_bits_and_aten(orc, oracle, pkg, dev, gold):
     sh, th, gH = _t(gold["src_h"], dev), _t(gold["tar_h"], dev), _t(gold["gH"], dev)
     B = sh.shape[0]
@@ -104,11 +115,18 @@ def test_backward_shapes_bits_and_aten(orc, oracle, pkg, dev, gold):
         _bits(orc, g_src, ws, f"grad_src {name}")
         _bits(orc, g_sc, _reduce_like(gsr, gss, sc_np.shape, B), f"grad_scale {name}")
         _bits(orc, g_dv, _reduce_like(gdr, gds, dv_np.shape, B), f"grad_div {name}")
-        for got, key in ((g_tar, "gtar"), (g_sc, "gscale"), (g_dv, "gdiv")):
+        # ATen autograd through the reference statements: dL/dtar bit for bit; a parameter
+        # ATen reduces per problem or not at all bit for bit; one it sums over the batch
+        # (its vectorised order, not ours) to binary32 accumulation error
+        _bits(orc, g_tar, gold[f"c{k}_gtar"], f"ATen grad_tar {name}")
+        for got, key in ((g_sc, "gscale"), (g_dv, "gdiv")):
             want = gold[f"c{k}_{key}"]
-            err = float(np.abs(got.cpu().numpy() - want).max() / np.abs(want).max())
-            worst = max(worst, err)
-            assert err <= 1e-5, f"{key} {name}: {err:.2e} from ATen autograd"
+            if _batch_summed(want.shape, B):
+                err = float(np.abs(got.cpu().numpy() - want).max() / np.abs(want).max())
+                worst = max(worst, err)
+                assert err <= 1e-5, f"{key} {name}: {err:.2e} from ATen autograd"
+            else:
+                _bits(orc, got, want, f"ATen {key} {name}")
         # through autograd: the same gradients reach leaf tensors of scale / div's shapes
         scg, dvg, thg = sc.clone().requires_grad_(), dv.clone().requires_grad_(), th.clone().requires_grad_()
         (pkg.TensorACA_rect(B, sh, thg, scg, dvg) * gH).sum().backward()
@@ -116,7 +134,7 @@ def test_backward_shapes_bits_and_aten(orc, oracle, pkg, dev, gold):
         _bits(orc, dvg.grad, g_dv.cpu().numpy(), f"autograd div {name}")
         _bits(orc, thg.grad, g_tar.cpu().numpy(), f"autograd tar {name}")
     print(f"\nbroadcast TensorACA backward vs ATen autograd (reference statements, CPU): "
-          f"max relative-to-max gap {worst:.2e}")
+          f"batch-summed parameters' max relative-to-max gap {worst:.2e}")
 
 
 def test_c_abi_strides(orc, oracle, pkg, dev):

@@ -1,0 +1,118 @@
+"""TensorACA_rect's backward on the GPU against ATen autograd through the reference's own
+statements (Modules_Runtime_Test.py:294-302), bit for bit.
+
+The reference gets its gradients from ATen autograd over its seven statements.  Those write
+H in place, and column 2 reads columns 0 and 1 back, so autograd differentiates them with
+respect to tar, scale and div only (with src requiring grad its backward raises; recorded in
+the fixture).  The product's backward (hg_solvers.hpp tensor_aca_rect_grad_rows) restates the
+autograd graph op for op: the zero-filled slice gradients (+0), the order dL/dh_temp arrives
+in, ATen's FMA-contracted cross product as the cross's backward.
+
+Pins:
+  * tests/golden/torch_rect_grad.npz (tools/make_golden.py --torch-grad, the reference's
+    statements under autograd on CPU torch here): dL/dtar in every case, dL/dscale and dL/ddiv
+    where ATen reduces them per problem or not at all -- through the op's backward and
+    torch.autograd;
+  * ATen autograd through the same statements on THIS box's CPU, 200 003 problems each of
+    random bit patterns, a special-value mixture and quads over 20 decades (AVX-512 hosts:
+    ATen's cross takes its FMA path there; skipped, not weakened, elsewhere).
+A batch-uniform (1,) scale / div gradient is a batch-wide sum in ATen's vectorised order;
+the op sums the same per-problem terms in its own fixed order (hg_sum_rows_f32), so there
+the bar is binary32 accumulation error, with the measured gap printed.
+"""
+import zlib
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import load_golden
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def gold():
+    return load_golden("torch_rect_grad.npz")
+
+
+def _same(orc, got, want, what):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else np.asarray(got)
+    ok = orc.same_bits(np.ascontiguousarray(got, np.float32), np.ascontiguousarray(want, np.float32))
+    assert ok.all(), f"{what}: {int((~ok).sum())}/{ok.size} differ; first at {np.argwhere(~ok)[:3].tolist()}"
+
+
+def test_backward_equals_reference_autograd_fixture(orc, oracle, pkg, dev, gold):
+    assert bool(gold["src_grad_refused"])
+    worst = 0.0
+    for tag in (str(t) for t in gold["cases"]):
+        src, tar, gH = (torch.from_numpy(gold[f"{tag}_{k}"]).to(dev) for k in ("src", "tar", "gH"))
+        sc_np, dv_np = gold[f"{tag}_scale"], gold[f"{tag}_div"]
+        sc, dv = torch.from_numpy(sc_np).to(dev), torch.from_numpy(dv_np).to(dev)
+        B = tar.shape[0]
+        _, g_tar, g_sc, g_dv = pkg.tensor_aca_rect_backward(src, tar, gH, sc, dv, False, True)
+        _same(orc, g_tar, gold[f"{tag}_gtar"], f"grad tar {tag}")
+        # through torch.autograd, src constant as in the reference
+        t = tar.clone().requires_grad_()
+        s_, d_ = sc.clone().requires_grad_(), dv.clone().requires_grad_()
+        pkg.TensorACA_rect(B, src, t, s_, d_).backward(gH)
+        _same(orc, t.grad, gold[f"{tag}_gtar"], f"autograd tar {tag}")
+        *_, gss, gds = oracle.tensor_aca_rect_rows_backward(
+            gold[f"{tag}_src"], gold[f"{tag}_tar"], gold[f"{tag}_gH"], sc_np, dv_np)
+        for got, via, key, part in ((g_sc, s_.grad, "gscale", gss), (g_dv, d_.grad, "gdiv", gds)):
+            want = gold[f"{tag}_{key}"]
+            _same(orc, via, got.cpu().numpy(), f"autograd {key} {tag}")
+            if sc_np.size > 1:
+                _same(orc, got, want, f"{key} {tag}")
+            elif np.isfinite(want).all():
+                # two orders of one binary32 batch sum: the bar is relative to the sum of the
+                # terms' magnitudes (the sum itself may cancel)
+                gap = abs(float(got.item()) - float(want[0])) / np.abs(part).astype(np.float64).sum()
+                worst = max(worst, gap)
+                assert gap <= 1e-5, (tag, key, gap)
+            else:
+                assert not np.isfinite(got.item()), (tag, key)
+    print(f"\nbatch-uniform scale/div gradient vs ATen's batch sum: max gap {worst:.2e} of the "
+          f"sum of the per-problem terms' magnitudes")
+
+
+B = 200_003
+SPECIALS = np.array([0.0, -0.0, 1.0, -1.0, 2.0, 0.5, 3.0, 1024.0, np.inf, -np.inf, np.nan,
+                     1e-45, -1.2e-40, 3e38, -3e38], np.float32)
+WEIGHTS = np.array([8, 6, 8, 6, 6, 4, 4, 4, 1, 1, 1, 1, 1, 1, 1], np.float64)
+
+
+def _inputs(kind, rng, shape):
+    if kind == "random_bits":
+        return rng.integers(0, 2**32 - 1, size=shape, dtype=np.uint32, endpoint=True).view(np.float32)
+    if kind == "special_mixture":
+        return rng.choice(SPECIALS, size=shape, p=WEIGHTS / WEIGHTS.sum()).astype(np.float32)
+    return (rng.uniform(-1, 1, shape) * 10.0 ** rng.integers(-10, 11, (shape[0], 1, 1))).astype(np.float32)
+
+
+@pytest.mark.parametrize("kind", ["random_bits", "special_mixture", "scaled"])
+@pytest.mark.parametrize("per_problem", [False, True])
+def test_backward_equals_aten_autograd_on_box_cpu(orc, pkg, dev, kind, per_problem):
+    """bench.torch_tensor_aca_rect (the reference's statements) under autograd on this box's
+    CPU: dL/dtar bit for bit, and with per-problem (B,1,1) scale / div their gradients too."""
+    if not orc.cpu_has_avx512():
+        pytest.skip("ATen's CPU cross takes its AVX-512 FMA path only on an AVX-512 host")
+    import bench
+    rng = np.random.default_rng(zlib.crc32(repr((kind, per_problem)).encode()))
+    src, tar = _inputs(kind, rng, (B, 3, 4)), _inputs(kind, rng, (B, 3, 4))
+    gH = _inputs(kind, rng, (B, 3, 3))
+    if per_problem:
+        sc = (rng.random((B, 1, 1)) * 64 + 64).astype(np.float32)
+        dv = (rng.random((B, 1, 1)) + 0.5).astype(np.float32)
+    else:
+        sc, dv = np.array([50.0], np.float32), np.array([1.25], np.float32)
+    t = torch.from_numpy(tar).requires_grad_()
+    s_, d_ = torch.from_numpy(sc).requires_grad_(), torch.from_numpy(dv).requires_grad_()
+    bench.torch_tensor_aca_rect(torch.from_numpy(src), t, s_, d_).backward(torch.from_numpy(gH))
+    _, g_tar, g_sc, g_dv = pkg.tensor_aca_rect_backward(
+        torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev), torch.from_numpy(gH).to(dev),
+        torch.from_numpy(sc).to(dev), torch.from_numpy(dv).to(dev), False, True)
+    _same(orc, g_tar, t.grad.numpy(), f"grad tar {kind}")
+    if per_problem:
+        _same(orc, g_sc, s_.grad.numpy(), f"grad scale {kind}")
+        _same(orc, g_dv, d_.grad.numpy(), f"grad div {kind}")

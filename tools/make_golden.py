@@ -418,9 +418,99 @@ def torch_bcast() -> str:
             % (torch.__version__, torch.backends.cpu.get_cpu_capability(), len(cases)))
 
 
+def torch_rect_grad() -> str:
+    """The gradients ATen autograd gives through TensorACA_rect's own statements
+    (Modules_Runtime_Test.py:294-302) on CPU torch: dL/dtar, dL/dscale, dL/ddiv for
+    H.backward(gH), src held constant -- with src requiring grad the statements fail in
+    backward (H is written in place after column 2 has read columns 0 and 1), which is
+    recorded too.  Cases: the reference's own adjust() batches (seed 0) with integer gH full
+    of signed zeros and identity problems (all cross terms 0); fractional quads; special
+    values; random bit patterns; per-problem (B,1,1) and per-(problem, row) (B,3,1)
+    scale / div.  Writes tests/golden/torch_rect_grad.npz; returns its manifest line."""
+    gen = ref_generators()
+    rng = np.random.default_rng(4242)
+    out = {}
+    vals = np.array([0.0, -0.0, 1.0, -1.0, 2.0, 0.5, 1024.0, np.inf, -np.inf, np.nan, 1e-45,
+                     -1.2e-40, 3e38], np.float32)
+
+    def frac(B):
+        g = torch.Generator().manual_seed(B)
+        s = torch.rand((B, 4, 2), generator=g) * 128 + torch.tensor([[0, 0], [128, 0], [0, 128],
+                                                                     [128, 128.0]])
+        t = s + torch.rand((B, 4, 2), generator=g) * 32
+        ones = torch.ones((B, 1, 4))
+        return (torch.cat((s.transpose(1, 2), ones), dim=1).numpy(),
+                torch.cat((t.transpose(1, 2), ones), dim=1).numpy())
+
+    cases = []
+    torch.manual_seed(0)
+    B = 2048
+    _, _, s_int, t_int, sc_int, dv_int = gen["adjust"]("cpu", B)
+    s_int, t_int = s_int.numpy().copy(), t_int.numpy().copy()
+    t_int[: B // 16, 0:2, :] = s_int[: B // 16, 0:2, :]  # identity problems
+    g_int = rng.integers(-3, 4, (B, 3, 3)).astype(np.float32)
+    g_int[rng.random((B, 3, 3)) < 0.3] = -0.0
+    g_int[B // 16: B // 8] = -0.0
+    cases.append(("int", s_int, t_int, g_int, sc_int.numpy(), dv_int.numpy()))
+    s_f, t_f = frac(B)
+    cases.append(("frac", s_f, t_f, rng.standard_normal((B, 3, 3)).astype(np.float32),
+                  np.array([50.0], np.float32), np.array([1.25], np.float32)))
+    Bs = 1024
+    pick = lambda *shape: rng.choice(vals, size=shape).astype(np.float32)  # noqa: E731
+    for tag, sc, dv in (("special", 50.0, 1.25), ("special_inf", np.inf, 0.5)):
+        cases.append((tag, pick(Bs, 3, 4), pick(Bs, 3, 4), pick(Bs, 3, 3),
+                      np.array([sc], np.float32), np.array([dv], np.float32)))
+    bits = lambda *shape: rng.integers(0, 2**32 - 1, size=shape, dtype=np.uint32,  # noqa: E731
+                                       endpoint=True).view(np.float32)
+    cases.append(("bits", bits(Bs, 3, 4), bits(Bs, 3, 4), bits(Bs, 3, 3),
+                  np.array([50.0], np.float32), np.array([1.25], np.float32)))
+    s_p, t_p = frac(Bs)
+    g_p = rng.standard_normal((Bs, 3, 3)).astype(np.float32)
+    cases.append(("per_problem", s_p, t_p, g_p,
+                  (rng.random((Bs, 1, 1)) * 64 + 64).astype(np.float32),
+                  (rng.random((Bs, 1, 1)) + 0.5).astype(np.float32)))
+    cases.append(("per_row", s_p, t_p, g_p, (rng.random((Bs, 3, 1)) * 64 + 64).astype(np.float32),
+                  (rng.random((Bs, 3, 1)) + 0.5).astype(np.float32)))
+    names = []
+    for tag, src, tar, gH, scale, div in cases:
+        tr = torch.from_numpy(tar.copy()).requires_grad_(True)
+        sc = torch.from_numpy(scale.copy()).requires_grad_(True)
+        dv = torch.from_numpy(div.copy()).requires_grad_(True)
+        H = run_ref_statements("TensorACA_rect", bs=tar.shape[0], src=torch.from_numpy(src),
+                               tar=tr, scale=sc, div=dv)["H"]
+        H.backward(torch.from_numpy(gH))
+        names.append(tag)
+        out.update({f"{tag}_src": src, f"{tag}_tar": tar, f"{tag}_gH": gH, f"{tag}_scale": scale,
+                    f"{tag}_div": div, f"{tag}_gtar": tr.grad.numpy().copy(),
+                    f"{tag}_gscale": sc.grad.numpy().copy(), f"{tag}_gdiv": dv.grad.numpy().copy()})
+    # src requiring grad: the statements' backward refuses (in-place H)
+    sr = torch.from_numpy(s_f.copy()).requires_grad_(True)
+    H = run_ref_statements("TensorACA_rect", bs=B, src=sr, tar=torch.from_numpy(t_f),
+                           scale=torch.tensor([50.0]), div=torch.tensor([1.25]))["H"]
+    try:
+        H.backward(torch.ones_like(H))
+        refused = False
+    except RuntimeError:
+        refused = True
+    out["src_grad_refused"] = np.array(refused)
+    out["cases"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "torch_rect_grad.npz"), **out)
+    return ("torch_rect_grad.npz: ATen autograd through the reference's TensorACA_rect statements "
+            "on CPU torch %s (ATen CPU capability %s): dL/dtar, dL/dscale, dL/ddiv for "
+            "H.backward(gH) on %s (src constant: with src requiring grad the statements' "
+            "backward raises -- recorded: %s)" % (torch.__version__,
+                                                   torch.backends.cpu.get_cpu_capability(),
+                                                   ", ".join(names), refused))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--torch-bcast"]:  # this fixture alone, appended to the manifest
         line = torch_bcast()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    elif sys.argv[1:] == ["--torch-grad"]:  # this fixture alone, appended to the manifest
+        line = torch_rect_grad()
         with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
             f.write("- " + line + "\n")
         print(line)
