@@ -525,6 +525,58 @@ def torch_tensor_aca_rect(src, tar, scale, div):
     return H
 
 
+def torch_aca_vanilla(src, tar):
+    """The reference's composed ACA_vanilla (Modules_Runtime_Test.py:322-382) as the same
+    sequence of tensor operations -- the same selects, products, differences and column
+    writes in the same order, so autograd builds the same graph (the CPU suite pins its H
+    and gradients to tests/golden/torch_vanilla_grad.npz).  For timing on the same GPU and
+    as the GPU tests' autograd checker on the box's CPU.  Names follow hg_solvers.hpp."""
+    bs = src.shape[0]
+    sn_x = src[:, 1, 0] - src[:, 0, 0]                       # :322-329
+    sn_y = src[:, 1, 1] - src[:, 0, 1]
+    sp_x = src[:, 2, 0] - src[:, 0, 0]
+    sp_y = src[:, 2, 1] - src[:, 0, 1]
+    sq_x = src[:, 3, 0] - src[:, 0, 0]
+    sq_y = src[:, 3, 1] - src[:, 0, 1]
+    det_s = sn_x * sp_y - sn_y * sp_x                        # :331-333
+    qs_x = sp_y * sq_x - sp_x * sq_y
+    qs_y = sn_x * sq_y - sn_y * sq_x
+    tn_x = tar[:, 1, 0] - tar[:, 0, 0]                       # :335-342
+    tn_y = tar[:, 1, 1] - tar[:, 0, 1]
+    tp_x = tar[:, 2, 0] - tar[:, 0, 0]
+    tp_y = tar[:, 2, 1] - tar[:, 0, 1]
+    tq_x = tar[:, 3, 0] - tar[:, 0, 0]
+    tq_y = tar[:, 3, 1] - tar[:, 0, 1]
+    det_t = tn_x * tp_y - tn_y * tp_x                        # :344-346
+    qt_x = tp_y * tq_x - tp_x * tq_y
+    qt_y = tn_x * tq_y - tn_y * tq_x
+    r = det_s - qs_x - qs_y                                  # :348-353
+    c11 = qs_y * qt_x * r
+    c22 = qs_x * qt_y * r
+    c33 = qs_x * qs_y * (det_t - qt_x - qt_y)
+    c31 = c11 - c33
+    c32 = c22 - c33
+    m0 = tar[:, 0, 0] * c33                                  # :355-360
+    m1 = tar[:, 0, 1] * c33
+    a11 = tar[:, 1, 0] * c11 - m0
+    a12 = tar[:, 2, 0] * c22 - m0
+    a21 = tar[:, 1, 1] * c11 - m1
+    a22 = tar[:, 2, 1] * c22 - m1
+    h0 = a11 * sp_y - a12 * sn_y                             # :362-370
+    h1 = a12 * sn_x - a11 * sp_x
+    h3 = a21 * sp_y - a22 * sn_y
+    h4 = a22 * sn_x - a21 * sp_x
+    h6 = c31 * sp_y - c32 * sn_y
+    h7 = c32 * sn_x - c31 * sp_x
+    h2 = m0 * det_s - h0 * src[:, 0, 0] - h1 * src[:, 0, 1]
+    h5 = m1 * det_s - h3 * src[:, 0, 0] - h4 * src[:, 0, 1]
+    h8 = c33 * det_s - h6 * src[:, 0, 0] - h7 * src[:, 0, 1]
+    H = torch.ones((bs, 9), device=src.device, dtype=src.dtype)   # :372-382
+    for k, v in enumerate((h0, h1, h2, h3, h4, h5, h6, h7, h8)):
+        H[:, k] = v
+    return H.reshape(bs, 3, 3)
+
+
 # TensorACA rect in the reference's (B,3,4) layout: 48 B tar + 48 B src (whole records: the
 # two floats used, src[:,0,0] and src[:,1,0], touch every 32-B sector) + 36 B H
 RECT_LAYOUT_MIN_BYTES = 132
@@ -577,6 +629,59 @@ def table8_sweep(d: Dist, pkg):
                          "table8_us": ref_us, "speedup_vs_table8": round(ref_us / native, 2)})
         out[algo] = rows
     return out
+
+
+def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 1024):
+    """ACA_vanilla as a differentiable loss term (deep homography with general quads):
+    forward + backward of the reference's ATen composition (torch_aca_vanilla: the same
+    graph, so the same gradient bits) against ours (torch.ops.sks_amd.aca + one
+    hg_aca_backward_f32 launch) at the config-4 batch, eager; and the backward kernel alone
+    at 16 M problems against its 164 B per problem (32 + 32 + 36 in, 32 + 32 out)."""
+    torch.manual_seed(0)
+    src, tar, *_ = pkg.adjust(d.dev, batch)
+    tar = (tar + torch.rand_like(tar)).contiguous()
+    gH = torch.randn(batch, 3, 3, device=d.dev)
+    S, T = src.clone().requires_grad_(), tar.clone().requires_grad_()
+
+    def step(fn):
+        def f():
+            S.grad = None
+            T.grad = None
+            fn(S, T).backward(gH)
+        return f
+
+    f_ours = step(lambda a, b: pkg.ACA_vanilla(batch, a, b))
+    f_torch = step(torch_aca_vanilla)
+    f_ours()
+    ours = (S.grad.clone(), T.grad.clone())
+    f_torch()
+    same = bool(torch.equal(ours[0], S.grad) and torch.equal(ours[1], T.grad))
+    for _ in range(20):
+        f_ours()
+        f_torch()
+    _, ms_o = timed_region(d, f_ours, 200)
+    _, ms_t = timed_region(d, f_torch, 200)
+    del S, T, src, tar, gH
+    n = big
+    s = torch.rand(n, 8, device=d.dev) * 1024
+    t = torch.rand(n, 8, device=d.dev) * 1024
+    g = torch.randn(n, 9, device=d.dev)
+    gs, gt = torch.empty_like(s), torch.empty_like(t)
+    stream = torch.cuda.current_stream(d.dev).cuda_stream
+    f_k = lambda: pkg._lib.call("hg_aca_backward_f32", s.data_ptr(), t.data_ptr(),  # noqa: E731
+                                g.data_ptr(), n, gs.data_ptr(), gt.data_ptr(), stream)
+    for _ in range(5):
+        f_k()
+    _, ms_k = timed_region(d, f_k, 50)
+    del s, t, g, gs, gt
+    gbps = n * 164 / (ms_k * 1e-3) / 1e9
+    return {"batch": batch, "fwd_bwd_us_per_call": round(ms_o * 1e3, 2),
+            "torch_composed_fwd_bwd_us_per_call": round(ms_t * 1e3, 2),
+            "speedup_vs_torch": round(ms_t / ms_o, 2),
+            "gradients_bit_identical_to_torch_composed_on_gpu": same,
+            "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
+            "backward_large_gbps": round(gbps, 1), "backward_large_frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "backward_bytes_per_problem": 164}
 
 
 def grouped_section(d: Dist, pkg, k: int = 64, m: int = 1000):
@@ -1329,6 +1434,7 @@ def main():
                     big * RECT_LAYOUT_MIN_BYTES / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             }
             del bs_h, bt_h, Hb
+            line["aca_vanilla_autograd"] = vanilla_autograd_section(d, pkg, args.rect_batch)
             line["reference_layout"] = reference_layout(d, pkg)
             line["table8_sweep"] = table8_sweep(d, pkg)
             line["table8_pipeline"] = table8_pipeline_section(d, pkg)

@@ -145,6 +145,17 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
                                        float height, float* grad_offsets, float* grad_corner,
                                        void* stream);
 
+/* Backward of the unnormalised general-quad ACA (ACA_vanilla, PyTorch Codes/
+ * Modules_Runtime_Test.py:312-388, which ATen autograd differentiates w.r.t. src and tar):
+ * src, tar (n,8) = (n,4,2) AoS, grad_H (n,9) -> grad_src, grad_tar (n,8), either may be
+ * NULL (not both).  The gradients ATen autograd gives through the reference's statements,
+ * bit for bit (operations in the autograd engine's order; hg_solvers.hpp aca_vanilla_grad).
+ * 16-B aligned float buffers take the LDS-staged kernel. */
+int hg_aca_backward_f32(const float* src, const float* tar, const float* grad_H, int64_t n,
+                        float* grad_src, float* grad_tar, void* stream);
+int hg_aca_backward_f64(const double* src, const double* tar, const double* grad_H, int64_t n,
+                        double* grad_src, double* grad_tar, void* stream);
+
 /* Synthetic input stream: out[i] = lo + (hi - lo) * u(i), u(i) = top 24 bits of
  * splitmix64(seed * 0xD1B54A32D192ED03 + offset + i) * 2^-24.  Counter based, so a
  * rank can generate its own shard (offset = first element) and a host can

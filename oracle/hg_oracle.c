@@ -399,6 +399,220 @@ int oracle_tensor_aca_rect_rows_backward_f32(const float* src, const float* tar,
     return 0;
 }
 
+/* ---------------------------------------------- ACA_vanilla backward ------ */
+/* The gradients ATen autograd gives through ACA_vanilla's statements
+ * (PyTorch Codes/Modules_Runtime_Test.py:322-382): the engine runs the graph's nodes in
+ * reverse creation order, so every value's gradient terms arrive from its last use first
+ * (H's copies :373-381, then :370 back to :322) and are summed in that order; a - b gives
+ * (g, -g), a * b gives (g*b, g*a); the leaves' gradients add the zero-filled select
+ * gradients' +0.  ACC keeps autograd's first-store-then-add accumulation.  Restated
+ * independently of csrc/hg_solvers.hpp aca_vanilla_grad; pinned by
+ * tests/golden/torch_vanilla_grad.npz. */
+#define ACC(v, c) do { __typeof__(v) c_ = (c); if (v##_n++) v = v + c_; else v = c_; } while (0)
+#define G(v) float v = 0; int v##_n = 0
+static void vanilla_grad_f32(const float* s, const float* t, const float* g, float* gs, float* gt) {
+  const float s00 = s[0], s01 = s[1], s10 = s[2], s11 = s[3], s20 = s[4], s21 = s[5], s30 = s[6], s31 = s[7];
+  const float t00 = t[0], t01 = t[1], t10 = t[2], t11 = t[3], t20 = t[4], t21 = t[5], t30 = t[6], t31 = t[7];
+  /* forward */
+  float M1N1_X = s10 - s00, M1N1_Y = s11 - s01, M1P1_X = s20 - s00, M1P1_Y = s21 - s01;
+  float M1Q1_X = s30 - s00, M1Q1_Y = s31 - s01;
+  float fA1 = M1N1_X * M1P1_Y - M1N1_Y * M1P1_X;
+  float Q3_x = M1P1_Y * M1Q1_X - M1P1_X * M1Q1_Y;
+  float Q3_y = M1N1_X * M1Q1_Y - M1N1_Y * M1Q1_X;
+  float M2N2_X = t10 - t00, M2N2_Y = t11 - t01, M2P2_X = t20 - t00, M2P2_Y = t21 - t01;
+  float M2Q2_X = t30 - t00, M2Q2_Y = t31 - t01;
+  float fA2 = M2N2_X * M2P2_Y - M2N2_Y * M2P2_X;
+  float Q4_x = M2P2_Y * M2Q2_X - M2P2_X * M2Q2_Y;
+  float Q4_y = M2N2_X * M2Q2_Y - M2N2_Y * M2Q2_X;
+  float tt1 = fA1 - Q3_x - Q3_y;
+  float P20 = Q3_y * Q4_x, C11 = P20 * tt1;
+  float P21 = Q3_x * Q4_y, C22 = P21 * tt1;
+  float P22 = Q3_x * Q3_y, E22 = fA2 - Q4_x - Q4_y, C33 = P22 * E22;
+  float C31 = C11 - C33, C32 = C22 - C33;
+  float tt3 = t00 * C33, tt4 = t01 * C33;
+  float H1_11 = t10 * C11 - tt3, H1_12 = t20 * C22 - tt3, H1_21 = t11 * C11 - tt4, H1_22 = t21 * C22 - tt4;
+  float res_0 = H1_11 * M1P1_Y - H1_12 * M1N1_Y;
+  float res_1 = H1_12 * M1N1_X - H1_11 * M1P1_X;
+  float res_3 = H1_21 * M1P1_Y - H1_22 * M1N1_Y;
+  float res_4 = H1_22 * M1N1_X - H1_21 * M1P1_X;
+  float res_6 = C31 * M1P1_Y - C32 * M1N1_Y;
+  float res_7 = C32 * M1N1_X - C31 * M1P1_X;
+  /* backward; acc(x, c): first contribution stored, later ones added */
+  G(gr0); G(gr1); G(gr3); G(gr4); G(gr6); G(gr7);
+  G(gs00); G(gs01); G(gt00); G(gt01);
+  G(gC33); G(gfA1); G(gtt3); G(gtt4); G(gC31); G(gC32); G(gC11); G(gC22);
+  G(gH11); G(gH12); G(gH21); G(gH22);
+  G(gM1PX); G(gM1PY); G(gM1NX); G(gM1NY); G(gM1QX); G(gM1QY);
+  G(gM2PX); G(gM2PY); G(gM2NX); G(gM2NY); G(gM2QX); G(gM2QY);
+  G(gQ3x); G(gQ3y); G(gQ4x); G(gQ4y); G(gtt1); G(gfA2);
+  /* H copies (columns 8..0 deliver first) */
+  ACC(gr7, g[7]); ACC(gr6, g[6]); ACC(gr4, g[4]); ACC(gr3, g[3]); ACC(gr1, g[1]); ACC(gr0, g[0]);
+  float G8 = g[8], G5 = g[5], G2 = g[2];
+  /* 39 */ ACC(gr7, (-G8) * s01); ACC(gs01, (-G8) * res_7); ACC(gr6, (-G8) * s00); ACC(gs00, (-G8) * res_6);
+           ACC(gC33, G8 * fA1); ACC(gfA1, G8 * C33);
+  /* 38 */ ACC(gr4, (-G5) * s01); ACC(gs01, (-G5) * res_4); ACC(gr3, (-G5) * s00); ACC(gs00, (-G5) * res_3);
+           ACC(gtt4, G5 * fA1); ACC(gfA1, G5 * tt4);
+  /* 37 */ ACC(gr1, (-G2) * s01); ACC(gs01, (-G2) * res_1); ACC(gr0, (-G2) * s00); ACC(gs00, (-G2) * res_0);
+           ACC(gtt3, G2 * fA1); ACC(gfA1, G2 * tt3);
+  /* 36 */ { float q = gr7; ACC(gC31, (-q) * M1P1_X); ACC(gM1PX, (-q) * C31); ACC(gC32, q * M1N1_X); ACC(gM1NX, q * C32); }
+  /* 35 */ { float q = gr6; ACC(gC32, (-q) * M1N1_Y); ACC(gM1NY, (-q) * C32); ACC(gC31, q * M1P1_Y); ACC(gM1PY, q * C31); }
+  /* 34 */ { float q = gr4; ACC(gH21, (-q) * M1P1_X); ACC(gM1PX, (-q) * H1_21); ACC(gH22, q * M1N1_X); ACC(gM1NX, q * H1_22); }
+  /* 33 */ { float q = gr3; ACC(gH22, (-q) * M1N1_Y); ACC(gM1NY, (-q) * H1_22); ACC(gH21, q * M1P1_Y); ACC(gM1PY, q * H1_21); }
+  /* 32 */ { float q = gr1; ACC(gH11, (-q) * M1P1_X); ACC(gM1PX, (-q) * H1_11); ACC(gH12, q * M1N1_X); ACC(gM1NX, q * H1_12); }
+  /* 31 */ { float q = gr0; ACC(gH12, (-q) * M1N1_Y); ACC(gM1NY, (-q) * H1_12); ACC(gH11, q * M1P1_Y); ACC(gM1PY, q * H1_11); }
+  float gt10 = 0, gt11 = 0, gt20 = 0, gt21 = 0; int gt10_n = 0, gt11_n = 0, gt20_n = 0, gt21_n = 0;
+  /* 30 */ { float q = gH22; ACC(gtt4, -q); ACC(gt21, q * C22); ACC(gC22, q * t21); }
+  /* 29 */ { float q = gH21; ACC(gtt4, -q); ACC(gt11, q * C11); ACC(gC11, q * t11); }
+  /* 28 */ { float q = gH12; ACC(gtt3, -q); ACC(gt20, q * C22); ACC(gC22, q * t20); }
+  /* 27 */ { float q = gH11; ACC(gtt3, -q); ACC(gt10, q * C11); ACC(gC11, q * t10); }
+  /* 26 */ { float q = gtt4; ACC(gt01, q * C33); ACC(gC33, q * t01); }
+  /* 25 */ { float q = gtt3; ACC(gt00, q * C33); ACC(gC33, q * t00); }
+  /* 24 */ { float q = gC32; ACC(gC22, q); ACC(gC33, -q); }
+  /* 23 */ { float q = gC31; ACC(gC11, q); ACC(gC33, -q); }
+  /* 22 */ { float q = gC33; float gP = q * E22, gE = q * P22;
+             ACC(gQ4y, -gE); ACC(gfA2, gE); ACC(gQ4x, -gE);
+             ACC(gQ3x, gP * Q3_y); ACC(gQ3y, gP * Q3_x); }
+  /* 21 */ { float q = gC22; float gP = q * tt1; ACC(gtt1, q * P21); ACC(gQ3x, gP * Q4_y); ACC(gQ4y, gP * Q3_x); }
+  /* 20 */ { float q = gC11; float gP = q * tt1; ACC(gtt1, q * P20); ACC(gQ3y, gP * Q4_x); ACC(gQ4x, gP * Q3_y); }
+  /* 19 */ { float q = gtt1; ACC(gQ3y, -q); ACC(gfA1, q); ACC(gQ3x, -q); }
+  /* 18 */ { float q = gQ4y; ACC(gM2NY, (-q) * M2Q2_X); ACC(gM2QX, (-q) * M2N2_Y); ACC(gM2NX, q * M2Q2_Y); ACC(gM2QY, q * M2N2_X); }
+  /* 17 */ { float q = gQ4x; ACC(gM2PX, (-q) * M2Q2_Y); ACC(gM2QY, (-q) * M2P2_X); ACC(gM2PY, q * M2Q2_X); ACC(gM2QX, q * M2P2_Y); }
+  /* 16 */ { float q = gfA2; ACC(gM2NY, (-q) * M2P2_X); ACC(gM2PX, (-q) * M2N2_Y); ACC(gM2NX, q * M2P2_Y); ACC(gM2PY, q * M2N2_X); }
+  float gt30 = 0, gt31 = 0; int gt30_n = 0, gt31_n = 0;
+  /* 15 */ ACC(gt31, gM2QY); ACC(gt01, -gM2QY);
+  /* 14 */ ACC(gt30, gM2QX); ACC(gt00, -gM2QX);
+  /* 13 */ ACC(gt21, gM2PY); ACC(gt01, -gM2PY);
+  /* 12 */ ACC(gt20, gM2PX); ACC(gt00, -gM2PX);
+  /* 11 */ ACC(gt11, gM2NY); ACC(gt01, -gM2NY);
+  /* 10 */ ACC(gt10, gM2NX); ACC(gt00, -gM2NX);
+  /* 9 */ { float q = gQ3y; ACC(gM1NY, (-q) * M1Q1_X); ACC(gM1QX, (-q) * M1N1_Y); ACC(gM1NX, q * M1Q1_Y); ACC(gM1QY, q * M1N1_X); }
+  /* 8 */ { float q = gQ3x; ACC(gM1PX, (-q) * M1Q1_Y); ACC(gM1QY, (-q) * M1P1_X); ACC(gM1PY, q * M1Q1_X); ACC(gM1QX, q * M1P1_Y); }
+  /* 7 */ { float q = gfA1; ACC(gM1NY, (-q) * M1P1_X); ACC(gM1PX, (-q) * M1N1_Y); ACC(gM1NX, q * M1P1_Y); ACC(gM1PY, q * M1N1_X); }
+  float gs10 = 0, gs11 = 0, gs20 = 0, gs21 = 0, gs30 = 0, gs31 = 0;
+  int gs10_n = 0, gs11_n = 0, gs20_n = 0, gs21_n = 0, gs30_n = 0, gs31_n = 0;
+  /* 6 */ ACC(gs31, gM1QY); ACC(gs01, -gM1QY);
+  /* 5 */ ACC(gs30, gM1QX); ACC(gs00, -gM1QX);
+  /* 4 */ ACC(gs21, gM1PY); ACC(gs01, -gM1PY);
+  /* 3 */ ACC(gs20, gM1PX); ACC(gs00, -gM1PX);
+  /* 2 */ ACC(gs11, gM1NY); ACC(gs01, -gM1NY);
+  /* 1 */ ACC(gs10, gM1NX); ACC(gs00, -gM1NX);
+  gs[0] = gs00 + (float)0; gs[1] = gs01 + (float)0; gs[2] = gs10 + (float)0; gs[3] = gs11 + (float)0;
+  gs[4] = gs20 + (float)0; gs[5] = gs21 + (float)0; gs[6] = gs30 + (float)0; gs[7] = gs31 + (float)0;
+  gt[0] = gt00 + (float)0; gt[1] = gt01 + (float)0; gt[2] = gt10 + (float)0; gt[3] = gt11 + (float)0;
+  gt[4] = gt20 + (float)0; gt[5] = gt21 + (float)0; gt[6] = gt30 + (float)0; gt[7] = gt31 + (float)0;
+}
+#undef G
+
+#define G(v) double v = 0; int v##_n = 0
+static void vanilla_grad_f64(const double* s, const double* t, const double* g, double* gs, double* gt) {
+  const double s00 = s[0], s01 = s[1], s10 = s[2], s11 = s[3], s20 = s[4], s21 = s[5], s30 = s[6], s31 = s[7];
+  const double t00 = t[0], t01 = t[1], t10 = t[2], t11 = t[3], t20 = t[4], t21 = t[5], t30 = t[6], t31 = t[7];
+  /* forward */
+  double M1N1_X = s10 - s00, M1N1_Y = s11 - s01, M1P1_X = s20 - s00, M1P1_Y = s21 - s01;
+  double M1Q1_X = s30 - s00, M1Q1_Y = s31 - s01;
+  double fA1 = M1N1_X * M1P1_Y - M1N1_Y * M1P1_X;
+  double Q3_x = M1P1_Y * M1Q1_X - M1P1_X * M1Q1_Y;
+  double Q3_y = M1N1_X * M1Q1_Y - M1N1_Y * M1Q1_X;
+  double M2N2_X = t10 - t00, M2N2_Y = t11 - t01, M2P2_X = t20 - t00, M2P2_Y = t21 - t01;
+  double M2Q2_X = t30 - t00, M2Q2_Y = t31 - t01;
+  double fA2 = M2N2_X * M2P2_Y - M2N2_Y * M2P2_X;
+  double Q4_x = M2P2_Y * M2Q2_X - M2P2_X * M2Q2_Y;
+  double Q4_y = M2N2_X * M2Q2_Y - M2N2_Y * M2Q2_X;
+  double tt1 = fA1 - Q3_x - Q3_y;
+  double P20 = Q3_y * Q4_x, C11 = P20 * tt1;
+  double P21 = Q3_x * Q4_y, C22 = P21 * tt1;
+  double P22 = Q3_x * Q3_y, E22 = fA2 - Q4_x - Q4_y, C33 = P22 * E22;
+  double C31 = C11 - C33, C32 = C22 - C33;
+  double tt3 = t00 * C33, tt4 = t01 * C33;
+  double H1_11 = t10 * C11 - tt3, H1_12 = t20 * C22 - tt3, H1_21 = t11 * C11 - tt4, H1_22 = t21 * C22 - tt4;
+  double res_0 = H1_11 * M1P1_Y - H1_12 * M1N1_Y;
+  double res_1 = H1_12 * M1N1_X - H1_11 * M1P1_X;
+  double res_3 = H1_21 * M1P1_Y - H1_22 * M1N1_Y;
+  double res_4 = H1_22 * M1N1_X - H1_21 * M1P1_X;
+  double res_6 = C31 * M1P1_Y - C32 * M1N1_Y;
+  double res_7 = C32 * M1N1_X - C31 * M1P1_X;
+  /* backward; acc(x, c): first contribution stored, later ones added */
+  G(gr0); G(gr1); G(gr3); G(gr4); G(gr6); G(gr7);
+  G(gs00); G(gs01); G(gt00); G(gt01);
+  G(gC33); G(gfA1); G(gtt3); G(gtt4); G(gC31); G(gC32); G(gC11); G(gC22);
+  G(gH11); G(gH12); G(gH21); G(gH22);
+  G(gM1PX); G(gM1PY); G(gM1NX); G(gM1NY); G(gM1QX); G(gM1QY);
+  G(gM2PX); G(gM2PY); G(gM2NX); G(gM2NY); G(gM2QX); G(gM2QY);
+  G(gQ3x); G(gQ3y); G(gQ4x); G(gQ4y); G(gtt1); G(gfA2);
+  /* H copies (columns 8..0 deliver first) */
+  ACC(gr7, g[7]); ACC(gr6, g[6]); ACC(gr4, g[4]); ACC(gr3, g[3]); ACC(gr1, g[1]); ACC(gr0, g[0]);
+  double G8 = g[8], G5 = g[5], G2 = g[2];
+  /* 39 */ ACC(gr7, (-G8) * s01); ACC(gs01, (-G8) * res_7); ACC(gr6, (-G8) * s00); ACC(gs00, (-G8) * res_6);
+           ACC(gC33, G8 * fA1); ACC(gfA1, G8 * C33);
+  /* 38 */ ACC(gr4, (-G5) * s01); ACC(gs01, (-G5) * res_4); ACC(gr3, (-G5) * s00); ACC(gs00, (-G5) * res_3);
+           ACC(gtt4, G5 * fA1); ACC(gfA1, G5 * tt4);
+  /* 37 */ ACC(gr1, (-G2) * s01); ACC(gs01, (-G2) * res_1); ACC(gr0, (-G2) * s00); ACC(gs00, (-G2) * res_0);
+           ACC(gtt3, G2 * fA1); ACC(gfA1, G2 * tt3);
+  /* 36 */ { double q = gr7; ACC(gC31, (-q) * M1P1_X); ACC(gM1PX, (-q) * C31); ACC(gC32, q * M1N1_X); ACC(gM1NX, q * C32); }
+  /* 35 */ { double q = gr6; ACC(gC32, (-q) * M1N1_Y); ACC(gM1NY, (-q) * C32); ACC(gC31, q * M1P1_Y); ACC(gM1PY, q * C31); }
+  /* 34 */ { double q = gr4; ACC(gH21, (-q) * M1P1_X); ACC(gM1PX, (-q) * H1_21); ACC(gH22, q * M1N1_X); ACC(gM1NX, q * H1_22); }
+  /* 33 */ { double q = gr3; ACC(gH22, (-q) * M1N1_Y); ACC(gM1NY, (-q) * H1_22); ACC(gH21, q * M1P1_Y); ACC(gM1PY, q * H1_21); }
+  /* 32 */ { double q = gr1; ACC(gH11, (-q) * M1P1_X); ACC(gM1PX, (-q) * H1_11); ACC(gH12, q * M1N1_X); ACC(gM1NX, q * H1_12); }
+  /* 31 */ { double q = gr0; ACC(gH12, (-q) * M1N1_Y); ACC(gM1NY, (-q) * H1_12); ACC(gH11, q * M1P1_Y); ACC(gM1PY, q * H1_11); }
+  double gt10 = 0, gt11 = 0, gt20 = 0, gt21 = 0; int gt10_n = 0, gt11_n = 0, gt20_n = 0, gt21_n = 0;
+  /* 30 */ { double q = gH22; ACC(gtt4, -q); ACC(gt21, q * C22); ACC(gC22, q * t21); }
+  /* 29 */ { double q = gH21; ACC(gtt4, -q); ACC(gt11, q * C11); ACC(gC11, q * t11); }
+  /* 28 */ { double q = gH12; ACC(gtt3, -q); ACC(gt20, q * C22); ACC(gC22, q * t20); }
+  /* 27 */ { double q = gH11; ACC(gtt3, -q); ACC(gt10, q * C11); ACC(gC11, q * t10); }
+  /* 26 */ { double q = gtt4; ACC(gt01, q * C33); ACC(gC33, q * t01); }
+  /* 25 */ { double q = gtt3; ACC(gt00, q * C33); ACC(gC33, q * t00); }
+  /* 24 */ { double q = gC32; ACC(gC22, q); ACC(gC33, -q); }
+  /* 23 */ { double q = gC31; ACC(gC11, q); ACC(gC33, -q); }
+  /* 22 */ { double q = gC33; double gP = q * E22, gE = q * P22;
+             ACC(gQ4y, -gE); ACC(gfA2, gE); ACC(gQ4x, -gE);
+             ACC(gQ3x, gP * Q3_y); ACC(gQ3y, gP * Q3_x); }
+  /* 21 */ { double q = gC22; double gP = q * tt1; ACC(gtt1, q * P21); ACC(gQ3x, gP * Q4_y); ACC(gQ4y, gP * Q3_x); }
+  /* 20 */ { double q = gC11; double gP = q * tt1; ACC(gtt1, q * P20); ACC(gQ3y, gP * Q4_x); ACC(gQ4x, gP * Q3_y); }
+  /* 19 */ { double q = gtt1; ACC(gQ3y, -q); ACC(gfA1, q); ACC(gQ3x, -q); }
+  /* 18 */ { double q = gQ4y; ACC(gM2NY, (-q) * M2Q2_X); ACC(gM2QX, (-q) * M2N2_Y); ACC(gM2NX, q * M2Q2_Y); ACC(gM2QY, q * M2N2_X); }
+  /* 17 */ { double q = gQ4x; ACC(gM2PX, (-q) * M2Q2_Y); ACC(gM2QY, (-q) * M2P2_X); ACC(gM2PY, q * M2Q2_X); ACC(gM2QX, q * M2P2_Y); }
+  /* 16 */ { double q = gfA2; ACC(gM2NY, (-q) * M2P2_X); ACC(gM2PX, (-q) * M2N2_Y); ACC(gM2NX, q * M2P2_Y); ACC(gM2PY, q * M2N2_X); }
+  double gt30 = 0, gt31 = 0; int gt30_n = 0, gt31_n = 0;
+  /* 15 */ ACC(gt31, gM2QY); ACC(gt01, -gM2QY);
+  /* 14 */ ACC(gt30, gM2QX); ACC(gt00, -gM2QX);
+  /* 13 */ ACC(gt21, gM2PY); ACC(gt01, -gM2PY);
+  /* 12 */ ACC(gt20, gM2PX); ACC(gt00, -gM2PX);
+  /* 11 */ ACC(gt11, gM2NY); ACC(gt01, -gM2NY);
+  /* 10 */ ACC(gt10, gM2NX); ACC(gt00, -gM2NX);
+  /* 9 */ { double q = gQ3y; ACC(gM1NY, (-q) * M1Q1_X); ACC(gM1QX, (-q) * M1N1_Y); ACC(gM1NX, q * M1Q1_Y); ACC(gM1QY, q * M1N1_X); }
+  /* 8 */ { double q = gQ3x; ACC(gM1PX, (-q) * M1Q1_Y); ACC(gM1QY, (-q) * M1P1_X); ACC(gM1PY, q * M1Q1_X); ACC(gM1QX, q * M1P1_Y); }
+  /* 7 */ { double q = gfA1; ACC(gM1NY, (-q) * M1P1_X); ACC(gM1PX, (-q) * M1N1_Y); ACC(gM1NX, q * M1P1_Y); ACC(gM1PY, q * M1N1_X); }
+  double gs10 = 0, gs11 = 0, gs20 = 0, gs21 = 0, gs30 = 0, gs31 = 0;
+  int gs10_n = 0, gs11_n = 0, gs20_n = 0, gs21_n = 0, gs30_n = 0, gs31_n = 0;
+  /* 6 */ ACC(gs31, gM1QY); ACC(gs01, -gM1QY);
+  /* 5 */ ACC(gs30, gM1QX); ACC(gs00, -gM1QX);
+  /* 4 */ ACC(gs21, gM1PY); ACC(gs01, -gM1PY);
+  /* 3 */ ACC(gs20, gM1PX); ACC(gs00, -gM1PX);
+  /* 2 */ ACC(gs11, gM1NY); ACC(gs01, -gM1NY);
+  /* 1 */ ACC(gs10, gM1NX); ACC(gs00, -gM1NX);
+  gs[0] = gs00 + (double)0; gs[1] = gs01 + (double)0; gs[2] = gs10 + (double)0; gs[3] = gs11 + (double)0;
+  gs[4] = gs20 + (double)0; gs[5] = gs21 + (double)0; gs[6] = gs30 + (double)0; gs[7] = gs31 + (double)0;
+  gt[0] = gt00 + (double)0; gt[1] = gt01 + (double)0; gt[2] = gt10 + (double)0; gt[3] = gt11 + (double)0;
+  gt[4] = gt20 + (double)0; gt[5] = gt21 + (double)0; gt[6] = gt30 + (double)0; gt[7] = gt31 + (double)0;
+}
+#undef G
+
+#undef ACC
+
+int oracle_aca_vanilla_backward_f32(const float* src, const float* tar, const float* gH, int64_t n,
+                                    float* gsrc, float* gtar) {
+    for (int64_t i = 0; i < n; ++i)
+        vanilla_grad_f32(src + 8 * i, tar + 8 * i, gH + 9 * i, gsrc + 8 * i, gtar + 8 * i);
+    return 0;
+}
+
+int oracle_aca_vanilla_backward_f64(const double* src, const double* tar, const double* gH,
+                                    int64_t n, double* gsrc, double* gtar) {
+    for (int64_t i = 0; i < n; ++i)
+        vanilla_grad_f64(src + 8 * i, tar + 8 * i, gH + 9 * i, gsrc + 8 * i, gtar + 8 * i);
+    return 0;
+}
+
 /* ------------------------------------------------------ RANSAC helpers ----- */
 /* Restates hg_fill_bits_u32 and hg_ransac_score_f32 (csrc/hg_ransac.hip), the
  * SURVEY 8(f).2 extension; the reference has no scorer, so these pin our own

@@ -70,6 +70,8 @@ class Oracle:
                                                             ctypes.c_float, ctypes.c_float,
                                                             _f32p, _f32p, _f32p]
         lib.oracle_tensor_aca_rect_backward_f32.restype = ctypes.c_int
+        lib.oracle_aca_vanilla_backward_f32.argtypes = [_f32p, _f32p, _f32p, _i64, _f32p, _f32p]
+        lib.oracle_aca_vanilla_backward_f64.argtypes = [_f64p, _f64p, _f64p, _i64, _f64p, _f64p]
         lib.oracle_tensor_aca_rect_rows_f32.argtypes = [_f32p, _f32p, _f32p, _i64, _f32p, _f32p]
         lib.oracle_tensor_aca_rect_rows_f32.restype = ctypes.c_int
         lib.oracle_tensor_aca_rect_rows_backward_f32.argtypes = [_f32p, _f32p, _f32p, _i64, _f32p,
@@ -109,6 +111,21 @@ class Oracle:
         self.lib.oracle_tensor_aca_rect_f32(_ptr(src, _f32p), _ptr(tar, _f32p), _ptr(H, _f32p),
                                             B, float(np.float32(scale)), float(np.float32(div)))
         return H
+
+    def aca_vanilla_backward(self, src, tar, gH):
+        """(dL/dsrc, dL/dtar), each (n,8), for ACA_vanilla (.py:322-382) given dL/dH (n,9):
+        ATen autograd's gradients through its statements.  float32 or float64 (src's dtype)."""
+        dt = np.float64 if np.asarray(src).dtype == np.float64 else np.float32
+        fp = _f64p if dt == np.float64 else _f32p
+        n = np.asarray(src).shape[0]
+        src = np.ascontiguousarray(np.asarray(src, dt).reshape(n, 8))
+        tar = np.ascontiguousarray(np.asarray(tar, dt).reshape(n, 8))
+        gH = np.ascontiguousarray(np.asarray(gH, dt).reshape(n, 9))
+        gs, gt = np.empty((n, 8), dt), np.empty((n, 8), dt)
+        fn = (self.lib.oracle_aca_vanilla_backward_f64 if dt == np.float64
+              else self.lib.oracle_aca_vanilla_backward_f32)
+        fn(_ptr(src, fp), _ptr(tar, fp), _ptr(gH, fp), n, _ptr(gs, fp), _ptr(gt, fp))
+        return gs, gt
 
     @staticmethod
     def _rows(x, B):

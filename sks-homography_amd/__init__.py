@@ -17,7 +17,7 @@ from __future__ import annotations
 
 from . import _lib
 from ._lib import HG_FLAG_NORMALIZE, HG_LAYOUT_AOS, HG_LAYOUT_SOA, HipError, lib, version
-from .ops import (aca, fill_uniform, sks, solve, solve_grouped, solve_host, stream_copy, tensor_aca_rect,
+from .ops import (aca, aca_backward, aca_vanilla, fill_uniform, sks, solve, solve_grouped, solve_host, stream_copy, tensor_aca_rect,
                   tensor_aca_rect_autograd, tensor_aca_rect_backward,
                   tensor_aca_offsets, tensor_aca_offsets_backward)
 from .ransac import (RansacResult, fill_bits, gather_solve, get_rand_list, mrg32k3a_state,
@@ -31,7 +31,7 @@ BYTES_PER_PROBLEM = {"f32": 64 + 36, "f64": 128 + 72}   # algorithmic HBM bytes 
 RECT_BYTES_PER_PROBLEM = 48 + 8 + 36                     # tar + src M + H
 
 __all__ = [
-    "aca", "sks", "solve", "solve_grouped", "solve_host", "tensor_aca_rect", "tensor_aca_rect_autograd",
+    "aca", "aca_vanilla", "aca_backward", "sks", "solve", "solve_grouped", "solve_host", "tensor_aca_rect", "tensor_aca_rect_autograd",
     "tensor_aca_rect_backward", "tensor_aca_offsets", "tensor_aca_offsets_backward",
     "fill_uniform", "sample_solve", "sample_solve_seeded", "fill_bits", "ransac", "ransac_score", "RansacResult", "stream_copy",
     "read_points", "rand_mrg32k3a", "get_rand_list", "gather_solve", "rand_gather_solve",

@@ -43,6 +43,8 @@ SIGNATURES = {
                                   _int),
     "hg_tensor_aca_offsets_backward_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
                                            _vp, _vp, _vp], _int),
+    "hg_aca_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
+    "hg_aca_backward_f64": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp], _int),
     "hg_fill_uniform_f32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_float,
                              ctypes.c_float, _vp], _int),
     "hg_fill_bits_u32": ([_vp, _i64, ctypes.c_uint64, ctypes.c_uint64, _vp], _int),

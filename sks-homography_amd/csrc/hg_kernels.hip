@@ -642,6 +642,39 @@ int hg_tensor_aca_offsets_backward_f32(const float* corner, const float* offsets
                       offsets, grad_H, B, width, height, grad_offsets, nullptr);
 }
 
+int hg_aca_backward_f32(const float* src, const float* tar, const float* grad_H, int64_t n,
+                        float* grad_src, float* grad_tar, void* stream) {
+    if (n < 0) return hg::kErrInvalid;
+    if (n == 0) return 0;
+    if (!src || !tar || !grad_H || (!grad_src && !grad_tar)) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    using hg::aligned16;
+    if (aligned16(src) && aligned16(tar) && aligned16(grad_H) &&
+        (!grad_src || aligned16(grad_src)) && (!grad_tar || aligned16(grad_tar))) {
+        const unsigned g = (unsigned)hg::ceil_div(n, hg::kBlock);
+        const bool nt = n * 164 > hg::kMallResidentBytes;
+#define HG_VB(S, T, NT)                                                                        \
+    hg::launch(hg::aca_vanilla_backward_staged<S, T, NT>, g, hg::kBlock, 0, s, src, tar, grad_H, \
+               n, grad_src, grad_tar)
+        if (grad_src && grad_tar) return nt ? HG_VB(true, true, true) : HG_VB(true, true, false);
+        if (grad_src) return nt ? HG_VB(true, false, true) : HG_VB(true, false, false);
+        return nt ? HG_VB(false, true, true) : HG_VB(false, true, false);
+#undef HG_VB
+    }
+    return hg::launch(hg::aca_vanilla_backward_kernel<float>, hg::generic_grid(n), hg::kBlock, 0,
+                      s, src, tar, grad_H, n, grad_src, grad_tar);
+}
+
+int hg_aca_backward_f64(const double* src, const double* tar, const double* grad_H, int64_t n,
+                        double* grad_src, double* grad_tar, void* stream) {
+    if (n < 0) return hg::kErrInvalid;
+    if (n == 0) return 0;
+    if (!src || !tar || !grad_H || (!grad_src && !grad_tar)) return hg::kErrInvalid;
+    return hg::launch(hg::aca_vanilla_backward_kernel<double>, hg::generic_grid(n), hg::kBlock, 0,
+                      reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, n, grad_src,
+                      grad_tar);
+}
+
 int hg_fill_uniform_f32(float* out, int64_t count, uint64_t seed, uint64_t offset, float lo,
                         float hi, void* stream) {
     if (count < 0) return hg::kErrInvalid;

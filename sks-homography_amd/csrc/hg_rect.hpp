@@ -407,4 +407,88 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_staged(
     }
 }
 
+// ---------------------------------------------------------------------------
+// ACA_vanilla backward (aca_vanilla_grad): src, tar (B,4,2), dL/dH (B,3,3) -> dL/dsrc,
+// dL/dtar (B,4,2), either optional.  One lane per problem, grid-stride; 100 B read and up
+// to 64 B written per problem.
+template <typename T>
+__global__ __launch_bounds__(kBlock) void aca_vanilla_backward_kernel(
+    const T* __restrict__ src, const T* __restrict__ tar, const T* __restrict__ gH, int64_t B,
+    T* __restrict__ gsrc, T* __restrict__ gtar) {
+    const int64_t stride = (int64_t)gridDim.x * kBlock;
+    for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
+        T s[8], t[8], g[9], gs[8], gt[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s[k] = src[p * 8 + k];
+            t[k] = tar[p * 8 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+        aca_vanilla_grad(s, t, g, gs, gt);
+        if (gsrc) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) gsrc[p * 8 + k] = gs[k];
+        }
+        if (gtar) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) gtar[p * 8 + k] = gt[k];
+        }
+    }
+}
+
+// Its staged binary32 form (16-B aligned tensors): a wave's 64 problems -- src and tar
+// slabs of 2 KiB, the dL/dH slab of 2304 B -- land in LDS by LDS-DMA, and the gradient rows
+// leave as contiguous 2-KiB slabs (store_rows_staged); a ragged last wave takes the
+// per-lane code.  Same arithmetic, same bits.
+template <bool WANT_SRC, bool WANT_TAR, bool NT>
+__global__ __launch_bounds__(kBlock) void aca_vanilla_backward_staged(
+    const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
+    int64_t B, float* __restrict__ gsrc, float* __restrict__ gtar) {
+    constexpr int kS = kWave * 32, kG = kWave * 36;
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][2 * kS + kG];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    if (base >= B) return;
+    const int64_t p = base + lane;
+    char* lds = smem[wave];
+    float s[8], t[8], g[9], gs[8], gt[8];
+    const bool full = base + kWave <= B;
+    if (full) {
+        dma_slab_issue<kS, NT>(reinterpret_cast<const char*>(src + base * 8), lds, lane);
+        dma_slab_issue<kS, NT>(reinterpret_cast<const char*>(tar + base * 8), lds + kS, lane);
+        dma_slab_issue<kG, NT>(reinterpret_cast<const char*>(gH + base * 9), lds + 2 * kS, lane);
+        dma_wait_sync();
+        __builtin_memcpy(s, lds + lane * 32, 32);
+        __builtin_memcpy(t, lds + kS + lane * 32, 32);
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + 2 * kS)[lane * 9 + k];
+        wave_lds_sync();  // the staging below reuses the input bytes
+    } else {
+        if (p >= B) return;
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+            s[k] = src[p * 8 + k];
+            t[k] = tar[p * 8 + k];
+        }
+#pragma unroll
+        for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
+    }
+    aca_vanilla_grad(s, t, g, gs, gt);
+    if (full) {
+        if constexpr (WANT_SRC) store_rows_staged<8, NT>(reinterpret_cast<char*>(gsrc + base * 8), gs, lds, lane);
+        if constexpr (WANT_TAR) store_rows_staged<8, NT>(reinterpret_cast<char*>(gtar + base * 8), gt, lds, lane);
+        return;
+    }
+    if constexpr (WANT_SRC) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gsrc[p * 8 + k] = gs[k];
+    }
+    if constexpr (WANT_TAR) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) gtar[p * 8 + k] = gt[k];
+    }
+}
+
 }  // namespace hg

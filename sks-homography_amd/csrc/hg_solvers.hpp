@@ -491,6 +491,173 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
     }
 }
 
+// Reverse-mode derivative of ACA_vanilla (Modules_Runtime_Test.py:322-382): the gradients
+// ATen autograd gives through its statements, op for op in the order the autograd engine
+// runs them (restated independently in oracle/hg_oracle.c, pinned by
+// tests/golden/torch_vanilla_grad.npz).  The engine runs the graph's nodes in reverse
+// creation order, so a value used by several statements receives its gradient terms from
+// its LAST use first, and they are summed in that order: H's copies (:373-381) first,
+// then the statements from res_8 (:370) back to M1N1_X (:322).  Each statement's backward is
+// ATen's: a - b gives (g, -g), a * b gives (g*b, g*a), (a*b)*c is two nodes.  The leaves'
+// gradients gather their terms from zero-filled select gradients, hence the final + 0.
+// In: s = src (4,2) = {Mx, My, Nx, Ny, Px, Py, Qx, Qy}, t = tar, g = dL/dH (3x3 row-major).
+// Out: gs = dL/dsrc, gt = dL/dtar (same layout).  Every operation rounds on its own.
+template <typename T>
+__device__ __host__ __forceinline__ void aca_vanilla_grad(const T (&s)[8], const T (&t)[8],
+                                                          const T (&g)[9], T (&gs)[8],
+                                                          T (&gt)[8]) {
+    const T s00 = s[0], s01 = s[1], s10 = s[2], s11 = s[3], s20 = s[4], s21 = s[5], s30 = s[6],
+            s31 = s[7];
+    const T t00 = t[0], t01 = t[1], t10 = t[2], t11 = t[3], t20 = t[4], t21 = t[5], t30 = t[6],
+            t31 = t[7];
+    // the forward's statements (:322-370), every intermediate kept
+    const T M1N1_X = s10 - s00, M1N1_Y = s11 - s01, M1P1_X = s20 - s00, M1P1_Y = s21 - s01;
+    const T M1Q1_X = s30 - s00, M1Q1_Y = s31 - s01;
+    const T fA1 = M1N1_X * M1P1_Y - M1N1_Y * M1P1_X;
+    const T Q3_x = M1P1_Y * M1Q1_X - M1P1_X * M1Q1_Y;
+    const T Q3_y = M1N1_X * M1Q1_Y - M1N1_Y * M1Q1_X;
+    const T M2N2_X = t10 - t00, M2N2_Y = t11 - t01, M2P2_X = t20 - t00, M2P2_Y = t21 - t01;
+    const T M2Q2_X = t30 - t00, M2Q2_Y = t31 - t01;
+    const T fA2 = M2N2_X * M2P2_Y - M2N2_Y * M2P2_X;
+    const T Q4_x = M2P2_Y * M2Q2_X - M2P2_X * M2Q2_Y;
+    const T Q4_y = M2N2_X * M2Q2_Y - M2N2_Y * M2Q2_X;
+    const T tt1 = (fA1 - Q3_x) - Q3_y;
+    const T P20 = Q3_y * Q4_x, C11 = P20 * tt1;
+    const T P21 = Q3_x * Q4_y, C22 = P21 * tt1;
+    const T P22 = Q3_x * Q3_y, E22 = (fA2 - Q4_x) - Q4_y, C33 = P22 * E22;
+    const T C31 = C11 - C33, C32 = C22 - C33;
+    const T tt3 = t00 * C33, tt4 = t01 * C33;
+    const T H1_11 = t10 * C11 - tt3, H1_12 = t20 * C22 - tt3;
+    const T H1_21 = t11 * C11 - tt4, H1_22 = t21 * C22 - tt4;
+    const T res_0 = H1_11 * M1P1_Y - H1_12 * M1N1_Y;
+    const T res_1 = H1_12 * M1N1_X - H1_11 * M1P1_X;
+    const T res_3 = H1_21 * M1P1_Y - H1_22 * M1N1_Y;
+    const T res_4 = H1_22 * M1N1_X - H1_21 * M1P1_X;
+    const T res_6 = C31 * M1P1_Y - C32 * M1N1_Y;
+    const T res_7 = C32 * M1N1_X - C31 * M1P1_X;
+    // res_k: H's copy first, then its use in res_2 / res_5 / res_8 (:368-370)
+    const T G8 = g[8], G5 = g[5], G2 = g[2];
+    const T gr7 = g[7] + (-G8) * s01, gr6 = g[6] + (-G8) * s00;
+    const T gr4 = g[4] + (-G5) * s01, gr3 = g[3] + (-G5) * s00;
+    const T gr1 = g[1] + (-G2) * s01, gr0 = g[0] + (-G2) * s00;
+    // res_8, res_5, res_2 (:370, :369, :368)
+    T gs00 = (-G8) * res_6, gs01 = (-G8) * res_7;
+    T gC33 = G8 * fA1, gfA1 = G8 * C33;
+    gs01 = gs01 + (-G5) * res_4;
+    gs00 = gs00 + (-G5) * res_3;
+    T gtt4 = G5 * fA1;
+    gfA1 = gfA1 + G5 * tt4;
+    gs01 = gs01 + (-G2) * res_1;
+    gs00 = gs00 + (-G2) * res_0;
+    T gtt3 = G2 * fA1;
+    gfA1 = gfA1 + G2 * tt3;
+    // res_7, res_6, res_4, res_3, res_1, res_0 (:367 back to :362)
+    T gC31 = (-gr7) * M1P1_X, gM1PX = (-gr7) * C31, gC32 = gr7 * M1N1_X, gM1NX = gr7 * C32;
+    gC32 = gC32 + (-gr6) * M1N1_Y;
+    T gM1NY = (-gr6) * C32;
+    gC31 = gC31 + gr6 * M1P1_Y;
+    T gM1PY = gr6 * C31;
+    T gH21 = (-gr4) * M1P1_X;
+    gM1PX = gM1PX + (-gr4) * H1_21;
+    T gH22 = gr4 * M1N1_X;
+    gM1NX = gM1NX + gr4 * H1_22;
+    gH22 = gH22 + (-gr3) * M1N1_Y;
+    gM1NY = gM1NY + (-gr3) * H1_22;
+    gH21 = gH21 + gr3 * M1P1_Y;
+    gM1PY = gM1PY + gr3 * H1_21;
+    T gH11 = (-gr1) * M1P1_X;
+    gM1PX = gM1PX + (-gr1) * H1_11;
+    T gH12 = gr1 * M1N1_X;
+    gM1NX = gM1NX + gr1 * H1_12;
+    gH12 = gH12 + (-gr0) * M1N1_Y;
+    gM1NY = gM1NY + (-gr0) * H1_12;
+    gH11 = gH11 + gr0 * M1P1_Y;
+    gM1PY = gM1PY + gr0 * H1_11;
+    // H1_22, H1_21, H1_12, H1_11 (:360 back to :357)
+    gtt4 = gtt4 - gH22;
+    T gt21 = gH22 * C22, gC22 = gH22 * t21;
+    gtt4 = gtt4 - gH21;
+    T gt11 = gH21 * C11, gC11 = gH21 * t11;
+    gtt3 = gtt3 - gH12;
+    T gt20 = gH12 * C22;
+    gC22 = gC22 + gH12 * t20;
+    gtt3 = gtt3 - gH11;
+    T gt10 = gH11 * C11;
+    gC11 = gC11 + gH11 * t10;
+    // tt4, tt3 (:356, :355), C32, C31 (:353, :352)
+    T gt01 = gtt4 * C33;
+    gC33 = gC33 + gtt4 * t01;
+    T gt00 = gtt3 * C33;
+    gC33 = gC33 + gtt3 * t00;
+    gC22 = gC22 + gC32;
+    gC33 = gC33 - gC32;
+    gC11 = gC11 + gC31;
+    gC33 = gC33 - gC31;
+    // C33 = (Q3_x*Q3_y) * ((fA2 - Q4_x) - Q4_y), C22, C11, tt1 (:351 back to :348)
+    const T gP22 = gC33 * E22, gE22 = gC33 * P22;
+    T gQ4y = -gE22, gfA2 = gE22, gQ4x = -gE22;
+    T gQ3x = gP22 * Q3_y, gQ3y = gP22 * Q3_x;
+    const T gP21 = gC22 * tt1;
+    T gtt1 = gC22 * P21;
+    gQ3x = gQ3x + gP21 * Q4_y;
+    gQ4y = gQ4y + gP21 * Q3_x;
+    const T gP20 = gC11 * tt1;
+    gtt1 = gtt1 + gC11 * P20;
+    gQ3y = gQ3y + gP20 * Q4_x;
+    gQ4x = gQ4x + gP20 * Q3_y;
+    gQ3y = gQ3y - gtt1;
+    gfA1 = gfA1 + gtt1;
+    gQ3x = gQ3x - gtt1;
+    // Q4_y, Q4_x, fA2 (:346 back to :344)
+    T gM2NY = (-gQ4y) * M2Q2_X, gM2QX = (-gQ4y) * M2N2_Y, gM2NX = gQ4y * M2Q2_Y;
+    T gM2QY = gQ4y * M2N2_X;
+    T gM2PX = (-gQ4x) * M2Q2_Y;
+    gM2QY = gM2QY + (-gQ4x) * M2P2_X;
+    T gM2PY = gQ4x * M2Q2_X;
+    gM2QX = gM2QX + gQ4x * M2P2_Y;
+    gM2NY = gM2NY + (-gfA2) * M2P2_X;
+    gM2PX = gM2PX + (-gfA2) * M2N2_Y;
+    gM2NX = gM2NX + gfA2 * M2P2_Y;
+    gM2PY = gM2PY + gfA2 * M2N2_X;
+    // the target differences (:342 back to :335)
+    const T gt31 = gM2QY;
+    gt01 = gt01 - gM2QY;
+    const T gt30 = gM2QX;
+    gt00 = gt00 - gM2QX;
+    gt21 = gt21 + gM2PY;
+    gt01 = gt01 - gM2PY;
+    gt20 = gt20 + gM2PX;
+    gt00 = gt00 - gM2PX;
+    gt11 = gt11 + gM2NY;
+    gt01 = gt01 - gM2NY;
+    gt10 = gt10 + gM2NX;
+    gt00 = gt00 - gM2NX;
+    // Q3_y, Q3_x, fA1 (:333 back to :331)
+    gM1NY = gM1NY + (-gQ3y) * M1Q1_X;
+    T gM1QX = (-gQ3y) * M1N1_Y;
+    gM1NX = gM1NX + gQ3y * M1Q1_Y;
+    T gM1QY = gQ3y * M1N1_X;
+    gM1PX = gM1PX + (-gQ3x) * M1Q1_Y;
+    gM1QY = gM1QY + (-gQ3x) * M1P1_X;
+    gM1PY = gM1PY + gQ3x * M1Q1_X;
+    gM1QX = gM1QX + gQ3x * M1P1_Y;
+    gM1NY = gM1NY + (-gfA1) * M1P1_X;
+    gM1PX = gM1PX + (-gfA1) * M1N1_Y;
+    gM1NX = gM1NX + gfA1 * M1P1_Y;
+    gM1PY = gM1PY + gfA1 * M1N1_X;
+    // the source differences (:329 back to :322)
+    gs01 = gs01 - gM1QY;
+    gs00 = gs00 - gM1QX;
+    gs01 = gs01 - gM1PY;
+    gs00 = gs00 - gM1PX;
+    gs01 = gs01 - gM1NY;
+    gs00 = gs00 - gM1NX;
+    gs[0] = gs00 + T(0); gs[1] = gs01 + T(0); gs[2] = gM1NX + T(0); gs[3] = gM1NY + T(0);
+    gs[4] = gM1PX + T(0); gs[5] = gM1PY + T(0); gs[6] = gM1QX + T(0); gs[7] = gM1QY + T(0);
+    gt[0] = gt00 + T(0); gt[1] = gt01 + T(0); gt[2] = gt10 + T(0); gt[3] = gt11 + T(0);
+    gt[4] = gt20 + T(0); gt[5] = gt21 + T(0); gt[6] = gt30 + T(0); gt[7] = gt31 + T(0);
+}
+
 __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,
                                                      float scale, float div, const float (&g)[9],
                                                      float (&gt)[12], float& gmx, float& gmy,

@@ -294,13 +294,68 @@ at::Tensor& quad_out(const at::Tensor& src_, const at::Tensor& tar_, bool normal
     TORCH_CHECK(src_.size(0) == tar_.size(0), "sks_amd::aca/sks: batch sizes differ");
     const int64_t B = tar_.size(0);
     check_out(out, {B, 3, 3}, dev);
+    const auto dt = tar_.scalar_type();
+    TORCH_CHECK((dt == at::kFloat || dt == at::kDouble) && src_.scalar_type() == dt &&
+                    out.scalar_type() == dt,
+                "sks_amd::aca/sks: src/tar/out must all be float32 or all float64");
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
     const c10::DeviceGuard guard(dev);
+    const int flags = normalize ? HG_FLAG_NORMALIZE : 0;
+    if (dt == at::kDouble) {
+        auto fn = ALGO == 0 ? hg_aca_f64 : hg_sks_f64;
+        hip_ok(fn(src.data_ptr<double>(), tar.data_ptr<double>(), out.data_ptr<double>(), B,
+                  HG_LAYOUT_AOS, flags, stream_of(tar)),
+               ALGO == 0 ? "hg_aca_f64" : "hg_sks_f64");
+        return out;
+    }
     auto fn = ALGO == 0 ? hg_aca_f32 : hg_sks_f32;
     hip_ok(fn(src.data_ptr<float>(), tar.data_ptr<float>(), out.data_ptr<float>(), B,
-              HG_LAYOUT_AOS, normalize ? HG_FLAG_NORMALIZE : 0, stream_of(tar)),
+              HG_LAYOUT_AOS, flags, stream_of(tar)),
            ALGO == 0 ? "hg_aca_f32" : "hg_sks_f32");
     return out;
+}
+
+// ACA_vanilla's gradients (.py:312-388 under ATen autograd): dL/dsrc, dL/dtar shaped like
+// src / tar, or (0,) where not needed.
+std::tuple<at::Tensor, at::Tensor> aca_backward(const at::Tensor& src_, const at::Tensor& tar_,
+                                                const at::Tensor& grad_, bool need_src,
+                                                bool need_tar) {
+    const at::Device dev = tar_.device();
+    on_gpu(src_, "src", dev);
+    on_gpu(tar_, "tar", dev);
+    on_gpu(grad_, "grad", dev);
+    for (const auto* p : {&src_, &tar_}) {
+        TORCH_CHECK((p->dim() == 3 && p->size(1) == 4 && p->size(2) == 2) ||
+                        (p->dim() == 2 && p->size(1) == 8),
+                    "sks_amd::aca_backward: src/tar must be (B,4,2) or (B,8), got ", p->sizes());
+    }
+    const int64_t B = tar_.size(0);
+    TORCH_CHECK(src_.size(0) == B, "sks_amd::aca_backward: batch sizes differ");
+    TORCH_CHECK(grad_.numel() == B * 9, "sks_amd::aca_backward: grad must be (B,3,3)");
+    const auto dt = tar_.scalar_type();
+    TORCH_CHECK((dt == at::kFloat || dt == at::kDouble) && src_.scalar_type() == dt &&
+                    grad_.scalar_type() == dt,
+                "sks_amd::aca_backward: src/tar/grad must all be float32 or all float64");
+    const at::Tensor src = src_.contiguous(), tar = tar_.contiguous(), grad = grad_.contiguous();
+    at::Tensor none = at::empty({0}, tar.options());
+    at::Tensor g_src = need_src ? at::empty(src_.sizes(), src.options()) : none;
+    at::Tensor g_tar = need_tar ? at::empty(tar_.sizes(), tar.options()) : none;
+    if (B == 0 || (!need_src && !need_tar)) return {g_src, g_tar};
+    const c10::DeviceGuard guard(dev);
+    if (dt == at::kDouble) {
+        hip_ok(hg_aca_backward_f64(src.data_ptr<double>(), tar.data_ptr<double>(),
+                                   grad.data_ptr<double>(), B,
+                                   need_src ? g_src.data_ptr<double>() : nullptr,
+                                   need_tar ? g_tar.data_ptr<double>() : nullptr, stream_of(tar)),
+               "hg_aca_backward_f64");
+    } else {
+        hip_ok(hg_aca_backward_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                   grad.data_ptr<float>(), B,
+                                   need_src ? g_src.data_ptr<float>() : nullptr,
+                                   need_tar ? g_tar.data_ptr<float>() : nullptr, stream_of(tar)),
+               "hg_aca_backward_f32");
+    }
+    return {g_src, g_tar};
 }
 
 template <int ALGO>
@@ -447,6 +502,54 @@ at::Tensor rect_autograd(const at::Tensor& src, const at::Tensor& tar, const at:
     return RectFunction::apply(src, tar, scale, div);
 }
 
+at::Tensor call_aca(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::aca", "")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&, bool)>();
+    return op.call(src, tar, normalize);
+}
+
+std::tuple<at::Tensor, at::Tensor> call_aca_backward(const at::Tensor& src, const at::Tensor& tar,
+                                                     const at::Tensor& grad, bool need_src,
+                                                     bool need_tar) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::aca_backward", "")
+                         .typed<std::tuple<at::Tensor, at::Tensor>(
+                             const at::Tensor&, const at::Tensor&, const at::Tensor&, bool, bool)>();
+    return op.call(src, tar, grad, need_src, need_tar);
+}
+
+// ACA_vanilla is differentiable in the reference (ATen autograd through its statements,
+// .py:322-382); the normalised form is the C++ API's (ACA_SKS.cpp:94-98), which nothing
+// differentiates, so it is refused rather than given a gradient the reference never defines.
+class AcaFunction : public torch::autograd::Function<AcaFunction> {
+   public:
+    static at::Tensor forward(AutogradContext* ctx, const at::Tensor& src, const at::Tensor& tar) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        ctx->save_for_backward({src, tar});
+        return call_aca(src, tar, false);
+    }
+
+    static variable_list backward(AutogradContext* ctx, variable_list grads) {
+        const auto saved = ctx->get_saved_variables();
+        const bool need_src = ctx->needs_input_grad(0), need_tar = ctx->needs_input_grad(1);
+        auto [g_src, g_tar] =
+            call_aca_backward(saved[0], saved[1], grads[0].contiguous(), need_src, need_tar);
+        at::Tensor none;
+        return {need_src ? g_src : none, need_tar ? g_tar : none};
+    }
+};
+
+at::Tensor aca_autograd(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
+    if (!any_requires_grad({&src, &tar})) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        return call_aca(src, tar, normalize);
+    }
+    TORCH_CHECK(!normalize, "sks_amd::aca: normalize=True (the C++ API's H/H[8], ACA_SKS.cpp:94-98) "
+                "is not differentiable; ACA_vanilla's unnormalised form (normalize=False) is");
+    return AcaFunction::apply(src, tar);
+}
+
 at::Tensor call_offsets(const at::Tensor& corner, const at::Tensor& offsets, double w, double h) {
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::tensor_aca_offsets", "")
@@ -504,6 +607,8 @@ TORCH_LIBRARY(sks_amd, m) {
           "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect_backward(Tensor src, Tensor tar, Tensor grad, Tensor scale, "
           "Tensor div, bool need_src, bool need_scale_div) -> (Tensor, Tensor, Tensor, Tensor)");
+    m.def("aca_backward(Tensor src, Tensor tar, Tensor grad, bool need_src, bool need_tar) -> "
+          "(Tensor, Tensor)");
     m.def("tensor_aca_offsets(Tensor corner, Tensor offsets, float width, float height) -> Tensor");
     m.def("tensor_aca_offsets.out(Tensor corner, Tensor offsets, float width, float height, *, "
           "Tensor(a!) out) -> Tensor(a!)");
@@ -516,6 +621,7 @@ TORCH_LIBRARY_IMPL(sks_amd, CUDA, m) {
     m.impl("solve.out", solve_out);
     m.impl("aca", quad<0>);
     m.impl("aca.out", quad_out<0>);
+    m.impl("aca_backward", aca_backward);
     m.impl("sks", quad<1>);
     m.impl("sks.out", quad_out<1>);
     m.impl("tensor_aca_rect", rect);
@@ -558,6 +664,11 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
                                       need_sd ? at::empty(dv.sizes(), t.options())
                                               : at::empty({0}, t.options()));
            });
+    m.impl("aca_backward", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&,
+                              bool need_src, bool need_tar) {
+        return std::make_tuple(need_src ? at::empty(s.sizes(), s.options()) : at::empty({0}, s.options()),
+                               need_tar ? at::empty(t.sizes(), t.options()) : at::empty({0}, t.options()));
+    });
     m.impl("tensor_aca_offsets_backward",
            [](const at::Tensor& c, const at::Tensor& o, const at::Tensor&, double, double,
               bool need_c) {
@@ -568,6 +679,7 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
 }
 
 TORCH_LIBRARY_IMPL(sks_amd, Autograd, m) {
+    m.impl("aca", aca_autograd);
     m.impl("tensor_aca_rect", rect_autograd);
     m.impl("tensor_aca_offsets", offsets_autograd);
 }

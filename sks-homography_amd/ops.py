@@ -204,6 +204,23 @@ def sks(src, tar, normalize: bool = True, layout: str = "aos", out=None) -> torc
     return solve("sks", src, tar, normalize, layout, out)
 
 
+def aca_vanilla(src: torch.Tensor, tar: torch.Tensor) -> torch.Tensor:
+    """ACA_vanilla's contract (Modules_Runtime_Test.py:312-388): src, tar (B,4,2) or (B,8),
+    float32 or float64 -> the unnormalised (B,3,3) H.  Runs torch.ops.sks_amd.aca, which is
+    differentiable w.r.t. src and tar as the reference's statements are under ATen autograd,
+    with the same gradient bits (hg_aca_backward_*)."""
+    _gpu_only(src)
+    _gpu_only(tar)
+    return _OPS.aca.default(src, tar, False)
+
+
+def aca_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor,
+                 need_src: bool = True, need_tar: bool = True):
+    """Gradients of aca_vanilla: (dL/dsrc, dL/dtar) shaped like src / tar (or empty)."""
+    _gpu_only(tar)
+    return _OPS.aca_backward.default(src, tar, grad, need_src, need_tar)
+
+
 Scalar = Union[float, int, torch.Tensor]
 
 

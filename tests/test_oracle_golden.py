@@ -376,3 +376,37 @@ def test_oracle_rect_backward_equals_reference_autograd(orc, oracle):
             ws, wd = _rect_grad_reduced(gss, gds, gsr, gdr, sc, dv)
             _assert_bits(orc, ws, g[f"{tag}_gscale"], f"grad scale {tag}")
             _assert_bits(orc, wd, g[f"{tag}_gdiv"], f"grad div {tag}")
+
+
+def test_oracle_aca_vanilla_backward_equals_reference_autograd(orc, oracle):
+    """tests/golden/torch_vanilla_grad.npz: ATen autograd through the reference's own
+    ACA_vanilla statements (tools/make_golden.py --torch-vanilla-grad) in binary32 and
+    binary64 -- uniform quads, adjust() batches with signed-zero gradients, point-file subsets,
+    the edge set, special values, random bit patterns.  The oracle's dL/dsrc and dL/dtar
+    equal it bit for bit, and so does its forward (unnormalised ACA)."""
+    g = load_golden("torch_vanilla_grad.npz")
+    for tag in (str(t) for t in g["cases"]):
+        src, tar = g[f"{tag}_src"], g[f"{tag}_tar"]
+        n = src.shape[0]
+        gs, gt = oracle.aca_vanilla_backward(src, tar, g[f"{tag}_gH"])
+        _assert_bits(orc, gs, g[f"{tag}_gsrc"].reshape(n, 8), f"grad src {tag}")
+        _assert_bits(orc, gt, g[f"{tag}_gtar"].reshape(n, 8), f"grad tar {tag}")
+        H = oracle.solve("aca", src.reshape(n, 8), tar.reshape(n, 8), normalize=False)
+        _assert_bits(orc, H, g[f"{tag}_H"].reshape(n, 9), f"H {tag}")
+
+
+def test_vanilla_restatement_builds_the_reference_graph(orc):
+    """bench.torch_aca_vanilla (the composition the GPU tests run under autograd on the box's
+    CPU, and bench times on the GPU) gives the fixture's H and gradients bit for bit: the
+    same graph as the reference's statements."""
+    import torch
+    from bench import torch_aca_vanilla
+    g = load_golden("torch_vanilla_grad.npz")
+    for tag in (str(t) for t in g["cases"]):
+        S = torch.from_numpy(g[f"{tag}_src"].copy()).requires_grad_()
+        T = torch.from_numpy(g[f"{tag}_tar"].copy()).requires_grad_()
+        H = torch_aca_vanilla(S, T)
+        H.backward(torch.from_numpy(g[f"{tag}_gH"]))
+        _assert_bits(orc, H.detach().numpy(), g[f"{tag}_H"], f"H {tag}")
+        _assert_bits(orc, S.grad.numpy(), g[f"{tag}_gsrc"], f"grad src {tag}")
+        _assert_bits(orc, T.grad.numpy(), g[f"{tag}_gtar"], f"grad tar {tag}")

@@ -52,6 +52,8 @@ for step in $STEPS; do
         newtests) run pytest_new 600 python -u -m pytest tests/test_gpu_errors.py tests/test_gpu_kat.py \
                 tests/test_gpu_config5.py tests/test_gpu_host.py tests/test_gpu_cpp_api.py -m gpu -v \
                 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        vanilla_tests) run pytest_vanilla 600 python -u -m pytest tests/test_gpu_vanilla_grad.py tests/test_gpu_parity.py \
+                tests/test_gpu_kat.py -m gpu -v -s -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         rect_tests) run pytest_rect 600 python -u -m pytest tests/test_gpu_rect_grad.py tests/test_gpu_rect_bcast.py \
                 tests/test_gpu_rect_aten_bits.py tests/test_gpu_offsets.py tests/test_gpu_parity.py -m gpu -v -s \
                 -k "rect or offsets or grad" -p no:cacheprovider --timeout 300 --timeout-method thread ;;

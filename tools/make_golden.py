@@ -503,9 +503,77 @@ def torch_rect_grad() -> str:
                                                    ", ".join(names), refused))
 
 
+def torch_vanilla_grad() -> str:
+    """The gradients ATen autograd gives through ACA_vanilla's own statements
+    (Modules_Runtime_Test.py:322-382) on CPU torch: dL/dsrc, dL/dtar for H.backward(gH).
+    binary32: uniform quads, the reference's adjust() batches (seed 0) with integer gH full of
+    signed zeros, 4-subsets of the reference's point file, the edge set, special values and
+    random bit patterns; binary64 (the statements run with float64 as the default dtype, as
+    torch_aca_f64 does): uniform quads, point-file subsets, the edge set.  Writes
+    tests/golden/torch_vanilla_grad.npz; returns its manifest line."""
+    gen = ref_generators()
+    rng = np.random.default_rng(3141)
+    vals = np.array([0.0, -0.0, 1.0, -1.0, 2.0, 0.5, 1024.0, np.inf, -np.inf, np.nan, 1e-45,
+                     -1.2e-40, 3e38], np.float32)
+    n = 512
+    cases = []
+    cases.append(("uniform", rng.uniform(0, 1024, (n, 4, 2)).astype(np.float32),
+                  rng.uniform(0, 1024, (n, 4, 2)).astype(np.float32),
+                  rng.standard_normal((n, 3, 3)).astype(np.float32)))
+    torch.manual_seed(0)
+    s_int, t_int, *_ = gen["adjust"]("cpu", n)
+    g_int = rng.integers(-3, 4, (n, 3, 3)).astype(np.float32)
+    g_int[rng.random((n, 3, 3)) < 0.3] = -0.0
+    cases.append(("int", s_int.numpy().copy(), t_int.numpy().copy(), g_int))
+    ws, wt, _ = wall_problems(n, 31)
+    cases.append(("wall", ws.reshape(n, 4, 2), wt.reshape(n, 4, 2),
+                  rng.standard_normal((n, 3, 3)).astype(np.float32)))
+    es, et = edge_problems()
+    ne = es.shape[0]
+    cases.append(("edge", es.reshape(ne, 4, 2), et.reshape(ne, 4, 2),
+                  rng.standard_normal((ne, 3, 3)).astype(np.float32)))
+    pick = lambda *shape: rng.choice(vals, size=shape).astype(np.float32)  # noqa: E731
+    cases.append(("special", pick(n, 4, 2), pick(n, 4, 2), pick(n, 3, 3)))
+    bits = lambda *shape: rng.integers(0, 2**32 - 1, size=shape, dtype=np.uint32,  # noqa: E731
+                                       endpoint=True).view(np.float32)
+    cases.append(("bits", bits(n, 4, 2), bits(n, 4, 2), bits(n, 3, 3)))
+    f64 = [("f64_uniform", rng.uniform(-512, 512, (n, 4, 2)), rng.uniform(-512, 512, (n, 4, 2)),
+            rng.standard_normal((n, 3, 3))),
+           ("f64_wall", ws.astype(np.float64).reshape(n, 4, 2), wt.astype(np.float64).reshape(n, 4, 2),
+            rng.standard_normal((n, 3, 3))),
+           ("f64_edge", es.astype(np.float64).reshape(ne, 4, 2), et.astype(np.float64).reshape(ne, 4, 2),
+            rng.standard_normal((ne, 3, 3)))]
+    out, names = {}, []
+    prev = torch.get_default_dtype()
+    try:
+        for tag, src, tar, gH in cases + f64:
+            torch.set_default_dtype(torch.float64 if src.dtype == np.float64 else torch.float32)
+            S = torch.from_numpy(src.copy()).requires_grad_(True)
+            T = torch.from_numpy(tar.copy()).requires_grad_(True)
+            H = run_ref_statements("ACA_vanilla", bs=src.shape[0], src=S, tar=T)["H"]
+            assert H.dtype == S.dtype
+            H.backward(torch.from_numpy(gH))
+            names.append(tag)
+            out.update({f"{tag}_src": src, f"{tag}_tar": tar, f"{tag}_gH": gH,
+                        f"{tag}_H": H.detach().numpy().copy(),
+                        f"{tag}_gsrc": S.grad.numpy().copy(), f"{tag}_gtar": T.grad.numpy().copy()})
+    finally:
+        torch.set_default_dtype(prev)
+    out["cases"] = np.array(names)
+    np.savez_compressed(os.path.join(OUT, "torch_vanilla_grad.npz"), **out)
+    return ("torch_vanilla_grad.npz: ATen autograd through the reference's ACA_vanilla statements "
+            "on CPU torch %s (ATen CPU capability %s): H, dL/dsrc, dL/dtar for H.backward(gH) on "
+            "%s" % (torch.__version__, torch.backends.cpu.get_cpu_capability(), ", ".join(names)))
+
+
 if __name__ == "__main__":
     if sys.argv[1:] == ["--torch-bcast"]:  # this fixture alone, appended to the manifest
         line = torch_bcast()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    elif sys.argv[1:] == ["--torch-vanilla-grad"]:  # this fixture alone, appended to the manifest
+        line = torch_vanilla_grad()
         with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
             f.write("- " + line + "\n")
         print(line)
