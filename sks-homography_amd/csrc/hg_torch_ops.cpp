@@ -30,11 +30,14 @@ void hip_ok(int rc, const char* fn) {
     TORCH_CHECK(rc == 0, fn, " failed with hipError_t ", rc);
 }
 
-void on_gpu(const at::Tensor& t, const char* name, const at::Device& dev) {
+// on `dev`; float32 unless `any_float` (the general-quad ops take float64 too and check
+// that their tensors agree)
+void on_gpu(const at::Tensor& t, const char* name, const at::Device& dev, bool any_float = false) {
     TORCH_CHECK(t.is_cuda(), "sks_amd: ", name, " must be a GPU tensor (no CPU path), got ",
                 t.device());
     TORCH_CHECK(t.device() == dev, "sks_amd: ", name, " is on ", t.device(), ", expected ", dev);
-    TORCH_CHECK(t.scalar_type() == at::kFloat, "sks_amd: ", name, " must be float32, got ",
+    TORCH_CHECK(t.scalar_type() == at::kFloat || (any_float && t.scalar_type() == at::kDouble),
+                "sks_amd: ", name, any_float ? " must be float32 or float64, got " : " must be float32, got ",
                 t.scalar_type());
 }
 
@@ -46,8 +49,9 @@ void check_rect(const at::Tensor& src, const at::Tensor& tar) {
     TORCH_CHECK(src.size(0) == tar.size(0), "sks_amd::tensor_aca_rect: batch sizes differ");
 }
 
-void check_out(const at::Tensor& out, at::IntArrayRef shape, const at::Device& dev) {
-    on_gpu(out, "out", dev);
+void check_out(const at::Tensor& out, at::IntArrayRef shape, const at::Device& dev,
+               bool any_float = false) {
+    on_gpu(out, "out", dev, any_float);
     TORCH_CHECK(out.sizes() == shape && out.is_contiguous(), "sks_amd: out must be a contiguous ",
                 shape, " tensor, got ", out.sizes());
 }
@@ -284,8 +288,8 @@ template <int ALGO>
 at::Tensor& quad_out(const at::Tensor& src_, const at::Tensor& tar_, bool normalize,
                      at::Tensor& out) {
     const at::Device dev = tar_.device();
-    on_gpu(src_, "src", dev);
-    on_gpu(tar_, "tar", dev);
+    on_gpu(src_, "src", dev, true);
+    on_gpu(tar_, "tar", dev, true);
     for (const auto* p : {&src_, &tar_}) {
         TORCH_CHECK((p->dim() == 3 && p->size(1) == 4 && p->size(2) == 2) ||
                         (p->dim() == 2 && p->size(1) == 8),
@@ -293,7 +297,7 @@ at::Tensor& quad_out(const at::Tensor& src_, const at::Tensor& tar_, bool normal
     }
     TORCH_CHECK(src_.size(0) == tar_.size(0), "sks_amd::aca/sks: batch sizes differ");
     const int64_t B = tar_.size(0);
-    check_out(out, {B, 3, 3}, dev);
+    check_out(out, {B, 3, 3}, dev, true);
     const auto dt = tar_.scalar_type();
     TORCH_CHECK((dt == at::kFloat || dt == at::kDouble) && src_.scalar_type() == dt &&
                     out.scalar_type() == dt,
@@ -321,9 +325,9 @@ std::tuple<at::Tensor, at::Tensor> aca_backward(const at::Tensor& src_, const at
                                                 const at::Tensor& grad_, bool need_src,
                                                 bool need_tar) {
     const at::Device dev = tar_.device();
-    on_gpu(src_, "src", dev);
-    on_gpu(tar_, "tar", dev);
-    on_gpu(grad_, "grad", dev);
+    on_gpu(src_, "src", dev, true);
+    on_gpu(tar_, "tar", dev, true);
+    on_gpu(grad_, "grad", dev, true);
     for (const auto* p : {&src_, &tar_}) {
         TORCH_CHECK((p->dim() == 3 && p->size(1) == 4 && p->size(2) == 2) ||
                         (p->dim() == 2 && p->size(1) == 8),
