@@ -366,13 +366,18 @@ PMC_TRAFFIC = os.path.join(ROOT, "profiles", "pmc_traffic.json")
 
 def traffic_source() -> dict:
     """Where `roofline.traffic` comes from: the committed rocprofv3 PMC summary, the run it
-    was reduced from, and whether the headline kernel's sources still have the digest they
-    were measured on (a changed kernel makes the committed figure stale: traffic is then
-    reported as null until the PMC passes are re-run)."""
+    was reduced from, and whether the headline kernels' gfx950 machine code in the library
+    loaded now is the code that was measured (build_lib.kernel_code_digest: a changed kernel
+    makes the committed figure stale, and traffic is then reported as null until the PMC
+    passes are re-run).  The source digest of the files around it is reported beside it."""
     sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
     try:
         import build_lib
-        now = build_lib.sources_digest("aos")
+        now_src = build_lib.sources_digest("aos")
+        try:
+            now_code = build_lib.kernel_code_digest()
+        except (OSError, KeyError, RuntimeError, ValueError):
+            now_code = None
     finally:
         sys.path.pop(0)
     try:
@@ -380,17 +385,20 @@ def traffic_source() -> dict:
             prov = json.load(f).get("provenance", {})
     except (OSError, ValueError):
         prov = {}
-    measured = prov.get("sources_aos", {}).get("sha256")
+    measured_src = prov.get("sources_aos", {}).get("sha256")
+    measured_code = prov.get("kernel_code")
     return {"file": os.path.relpath(PMC_TRAFFIC, ROOT), "pmc_run": prov.get("pmc_run"),
-            "sources_sha256_measured": measured, "sources_sha256_now": now["sha256"],
-            "sources_match": measured == now["sha256"]}
+            "kernel_code_measured": measured_code, "kernel_code_now": now_code,
+            "kernel_code_match": bool(measured_code) and measured_code == now_code,
+            "sources_sha256_measured": measured_src, "sources_sha256_now": now_src["sha256"],
+            "sources_match": measured_src == now_src["sha256"]}
 
 
 def pmc_traffic(kernel_key: str):
     """Per-launch HBM bytes of `kernel_key` from the committed rocprofv3 PMC summary
     (profiles/pmc_traffic.json, produced by tools/pmc_traffic.py), or None -- also None when
-    the kernel sources changed since it was measured (traffic_source)."""
-    if not traffic_source()["sources_match"]:
+    the kernel's machine code changed since it was measured (traffic_source)."""
+    if not traffic_source()["kernel_code_match"]:
         return None
     try:
         with open(PMC_TRAFFIC) as f:
@@ -1372,6 +1380,14 @@ def main():
             for _ in range(5):
                 pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb)
             _, ms_b = timed_region(d, lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb), 50)
+            # per-problem (B,1,1) scale / div (the reference composition's broadcast, .py:301-302)
+            psc = torch.full((big, 1, 1), 128.0, device=d.dev) + torch.rand(big, 1, 1, device=d.dev)
+            pdv = torch.ones((big, 1, 1), device=d.dev)
+            f_pp = lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, psc, pdv, out=Hb)  # noqa: E731
+            for _ in range(5):
+                f_pp()
+            _, ms_pp = timed_region(d, f_pp, 50)
+            del psc, pdv
             # compact form (corner + 4 offsets) on the same big batch
             corner = bs_h[:, 0:2, 0].contiguous()
             offs = (bt_h[:, 0:2, :] - bs_h[:, 0:2, :]).transpose(1, 2).contiguous()
@@ -1432,6 +1448,10 @@ def main():
                 "layout_min_bytes_per_problem": RECT_LAYOUT_MIN_BYTES,
                 "large_layout_min_frac": round(
                     big * RECT_LAYOUT_MIN_BYTES / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                # (B,1,1) scale and div: 8 B more per problem
+                "large_per_problem_scale_div_us_per_call": round(ms_pp * 1e3, 2),
+                "large_per_problem_layout_min_frac": round(
+                    big * (RECT_LAYOUT_MIN_BYTES + 8) / (ms_pp * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
             }
             del bs_h, bt_h, Hb
             line["aca_vanilla_autograd"] = vanilla_autograd_section(d, pkg, args.rect_batch)

@@ -53,6 +53,68 @@ def sources_digest(kind: str = "aos") -> dict:
     return {"files": files, "flags": flags, "sha256": whole.hexdigest()[:16]}
 
 
+# The headline kernels whose HBM traffic profiles/pmc_traffic.json records, by the mangled
+# name of their gfx950 entry point (hg::solve_aos<ALGO, true, float, 2, 39>).
+TRAFFIC_KERNELS = {
+    "aca_f32_aos_norm": "_ZN2hg9solve_aosILi0ELb1EfLi2ELi39EEEvPKT1_S3_PS1_l",
+    "sks_f32_aos_norm": "_ZN2hg9solve_aosILi1ELb1EfLi2ELi39EEEvPKT1_S3_PS1_l",
+}
+
+
+def _elf_sections(b: bytes, base: int = 0) -> dict:
+    """{name: (sh_addr, sh_offset, sh_size)} of the little-endian ELF64 image at b[base:]."""
+    import struct
+    shoff = struct.unpack_from("<Q", b, base + 0x28)[0]
+    shentsize, shnum, shstrndx = struct.unpack_from("<HHH", b, base + 0x3A)
+    raw = [struct.unpack_from("<IIQQQQ", b, base + shoff + i * shentsize) for i in range(shnum)]
+    strtab_off = base + raw[shstrndx][4]
+    out = {}
+    for name, _typ, _flags, addr, off, size in raw:
+        end = b.index(b"\0", strtab_off + name)
+        out[b[strtab_off + name:end].decode()] = (addr, base + off, size)
+    return out
+
+
+def kernel_code_digest(lib_path: str = None) -> dict:
+    """sha256 (16 hex digits) of the gfx950 machine code of each TRAFFIC_KERNELS entry point,
+    read from the built library: the HIP fat binary's offload bundles (.hip_fatbin), the gfx950
+    code object in each, that object's symbol table and .text.  What ran is what is hashed, so
+    edits that leave the kernel's code unchanged keep its measured traffic valid."""
+    import hashlib
+    import struct
+    b = open(lib_path or LIB, "rb").read()
+    _, fat_off, fat_size = _elf_sections(b)[".hip_fatbin"]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    found = {}
+    pos = b.find(magic, fat_off, fat_off + fat_size)
+    while pos >= 0:
+        count = struct.unpack_from("<Q", b, pos + 24)[0]
+        q = pos + 32
+        for _ in range(count):
+            off, size, idlen = struct.unpack_from("<QQQ", b, q)
+            ident = b[q + 24:q + 24 + idlen].decode()
+            q += 24 + idlen
+            if ARCH not in ident or size == 0:
+                continue
+            co = pos + off
+            secs = _elf_sections(b, co)
+            sym_addr, sym_off, sym_size = secs[".symtab"]
+            str_off = secs[".strtab"][1]
+            text_addr, text_off, _ = secs[".text"]
+            for k in range(sym_size // 24):
+                st_name, _info, _other, _shndx, value, sz = struct.unpack_from("<IBBHQQ", b, sym_off + 24 * k)
+                name = b[str_off + st_name:b.index(b"\0", str_off + st_name)].decode()
+                for key, mangled in TRAFFIC_KERNELS.items():
+                    if name == mangled and sz:
+                        start = text_off + (value - text_addr)
+                        found[key] = hashlib.sha256(b[start:start + sz]).hexdigest()[:16]
+        pos = b.find(magic, pos + 24, fat_off + fat_size)
+    missing = set(TRAFFIC_KERNELS) - set(found)
+    if missing:
+        raise RuntimeError(f"{lib_path or LIB}: no gfx950 code for {sorted(missing)}")
+    return found
+
+
 def hipcc() -> str:
     for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):

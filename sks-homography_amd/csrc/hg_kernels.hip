@@ -573,8 +573,17 @@ int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, i
     if (B == 0) return 0;
     if (!src || !tar || !H || !scale || !div) return hg::kErrInvalid;
     const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
-    return hg::launch(hg::tensor_aca_rect_bcast_kernel, hg::generic_grid(B), hg::kBlock, 0,
-                      reinterpret_cast<hipStream_t>(stream), src, tar, H, B, a);
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(H)) {
+        const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
+        if (B * 140 > hg::kMallResidentBytes)  // 132 B of (B,3,4) records and H + 8 B of scale / div
+            return hg::launch(hg::tensor_aca_rect_bcast_staged<true>, g, hg::kBlock, 0, s, src, tar,
+                              H, B, a);
+        return hg::launch(hg::tensor_aca_rect_bcast_staged<false>, g, hg::kBlock, 0, s, src, tar, H,
+                          B, a);
+    }
+    return hg::launch(hg::tensor_aca_rect_bcast_kernel, hg::generic_grid(B), hg::kBlock, 0, s, src,
+                      tar, H, B, a);
 }
 
 int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, const float* grad_H,

@@ -146,6 +146,47 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_kernel(
     }
 }
 
+// The same, staged like tensor_aca_rect_kernel<1, true, ...> (16-B aligned src / tar / H): the
+// wave's tar slab by LDS-DMA, M's x and y with two dword loads, scale / div per (problem, row)
+// through RectBcast, H through the staged 16-B store; a ragged last wave takes the per-lane
+// code.  Same arithmetic, same bits.
+template <bool NT>
+__global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
+    const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H, int64_t B,
+    RectBcast a) {
+    constexpr int kSlab = kWave * 48;  // >= the 36-B rows H stages
+    __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kSlab];
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
+    if (base >= B) return;
+    const int64_t p = base + lane;
+    char* lds = smem[wave];
+    float h[1][9], sc[3], dv[3];
+    if (base + kWave <= B) {
+        const float mx = NT ? __builtin_nontemporal_load(src + p * 12 + 0) : src[p * 12 + 0];
+        const float my = NT ? __builtin_nontemporal_load(src + p * 12 + 4) : src[p * 12 + 4];
+        rect_bcast_load(a, p, sc, dv);
+        const char* const g[1] = {reinterpret_cast<const char*>(tar + base * 12)};
+        char* const l[1] = {lds};
+        slabs_to_lds<kSlab, 1, true, NT>(g, l, lane);
+        float tr[12];
+        __builtin_memcpy(tr, lds + lane * 48, 48);
+        tensor_aca_rect_solve_rows(tr, mx, my, sc, dv, h[0]);
+        wave_lds_sync();
+        store_rows9_staged<float, 1, NT>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
+        return;
+    }
+    if (p >= B) return;
+    float tr[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
+    rect_bcast_load(a, p, sc, dv);
+    tensor_aca_rect_solve_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h[0]);
+#pragma unroll
+    for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[0][k];
+}
+
 // Its backward: dL/dtar, optionally dL/dsrc, and per parameter either each row's share
 // ((3,B): gs[r * B + p]) or the problem's three-row sum ((B): gs[p], the uniform kernels'
 // per-problem partial, ((0 + t0) + t1) + t2); the caller reduces them to the parameter's shape.

@@ -321,16 +321,31 @@ def test_read_points_rounds_once_like_sscanf(pkg, tmp_path):
     assert Fraction(tricky[0]) > (lo + hi) / 2 and Fraction(float(got[0])) == hi
 
 
-def test_pmc_traffic_matches_the_kernel_sources():
-    """profiles/pmc_traffic.json's PMC figures were measured on kernel sources whose digest it
-    records; bench.py reports them as `roofline.traffic` only while the tree still has that
-    digest.  A change to the headline kernel's sources fails here until the PMC passes are
-    re-run (tools/gpu_round.sh pmc, tools/pmc_traffic.py) -- the committed figure is never
-    silently reused for a different kernel."""
+def test_pmc_traffic_matches_the_kernel_code():
+    """profiles/pmc_traffic.json's PMC figures were measured on headline kernels whose gfx950
+    machine code digest it records (build_lib.kernel_code_digest, read from the library that
+    ran); bench.py reports them as `roofline.traffic` only while the built library still holds
+    that code.  A change to the headline kernels fails here until the PMC passes are re-run
+    (tools/gpu_round.sh pmc, tools/pmc_traffic.py) -- the committed figure is never silently
+    reused for a different kernel."""
     import bench
     src = bench.traffic_source()
-    assert src["sources_sha256_measured"], "profiles/pmc_traffic.json has no source digest"
-    assert src["sources_match"], (f"kernel sources changed since the PMC run "
-                                  f"({src['sources_sha256_measured']} -> "
-                                  f"{src['sources_sha256_now']}): re-measure the traffic")
+    assert src["kernel_code_measured"], "profiles/pmc_traffic.json has no kernel code digest"
+    assert src["kernel_code_match"], (f"headline kernel code changed since the PMC run "
+                                      f"({src['kernel_code_measured']} -> "
+                                      f"{src['kernel_code_now']}): re-measure the traffic")
     assert bench.pmc_traffic("aca_f32_aos_norm") is not None
+
+
+def test_kernel_code_digest_reads_the_headline_entry_points(pkg):
+    """The digest finds exactly the two headline kernels' code in the gfx950 code objects of
+    the built library, and it is a function of the code alone (stable across reads)."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
+    try:
+        import build_lib as bl
+    finally:
+        sys.path.pop(0)
+    d1, d2 = bl.kernel_code_digest(), bl.kernel_code_digest()
+    assert d1 == d2 and set(d1) == set(bl.TRAFFIC_KERNELS)
+    assert d1["aca_f32_aos_norm"] != d1["sks_f32_aos_norm"]

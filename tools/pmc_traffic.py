@@ -75,14 +75,17 @@ def main():
                                                                       "sks_f32_aos_norm")}
     doc = dict(flat)
     doc["detail"] = res
-    # provenance: which run, and the kernel sources it was measured on (bench.py reports the
-    # figure only while the tree's sources still have this digest; tests/test_capi.py checks)
+    # provenance: which run, and the kernels it was measured on -- the gfx950 machine code of
+    # the headline entry points in the library that ran (reduce right after the run, before
+    # rebuilding); bench.py reports the figure only while the library still holds that code
+    # (tests/test_capi.py checks), the source digest is kept for reference
     sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                                     "sks-homography_amd"))
     import build_lib
     doc["provenance"] = {
         "pmc_run": {"fetch_dir": sys.argv[1], "write_dir": sys.argv[2],
                     "tag": os.environ.get("PMC_TAG", "")},
+        "kernel_code": build_lib.kernel_code_digest(),
         "sources_aos": build_lib.sources_digest("aos"),
     }
     doc["method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE, separate passes, csv; "
