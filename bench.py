@@ -376,7 +376,7 @@ def traffic_source() -> dict:
         now_src = build_lib.sources_digest("aos")
         try:
             now_code = build_lib.kernel_code_digest()
-        except (OSError, KeyError, RuntimeError, ValueError):
+        except Exception:  # noqa: BLE001 -- unreadable library: no code match, traffic null
             now_code = None
     finally:
         sys.path.pop(0)
