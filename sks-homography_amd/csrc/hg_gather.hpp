@@ -42,8 +42,8 @@ __device__ __forceinline__ uint32_t mrg_entry_dot(const uint32_t* e, int t, cons
 // its own l < 256 and writes its positions -- lane-consecutive subsequences, so every store
 // instruction covers 256 contiguous bytes.  Default-policy stores: the words are read again
 // by the gather that follows, from the MALL when they fit.
-// ABL (tune library only, wrong bits): 1 no table jumps (the lane starts from y[j]), 2 no
-// engine steps (the words are the lane's index)
+// ABL (tune library only): 1 no table jumps (the lane starts from y[j]), 2 no engine steps
+// (the words are the lane's index) -- wrong bits, timing only; 4 non-temporal stores (same bits)
 template <int ABL = 0>
 __global__ __launch_bounds__(kBlock) void mrg_words_kernel(uint32_t* __restrict__ out,
                                                            mrg::WordsArgs a) {
@@ -79,13 +79,17 @@ __global__ __launch_bounds__(kBlock) void mrg_words_kernel(uint32_t* __restrict_
         for (; i < left; ++i, o += mrg::kOrder) o[lane] = x + (uint32_t)i;
         return;
     }
+    auto put = [&](uint32_t* p, uint32_t w) {
+        if constexpr ((ABL & 4) != 0) __builtin_nontemporal_store(w, p);
+        else *p = w;
+    };
     for (; i + 3 <= left; i += 3, o += 3 * mrg::kOrder) {  // three steps: the state stays put
-        o[lane] = mrg::step<0>(st);
-        o[mrg::kOrder + lane] = mrg::step<1>(st);
-        o[2 * mrg::kOrder + lane] = mrg::step<2>(st);
+        put(o + lane, mrg::step<0>(st));
+        put(o + mrg::kOrder + lane, mrg::step<1>(st));
+        put(o + 2 * mrg::kOrder + lane, mrg::step<2>(st));
     }
-    if (i < left) o[lane] = mrg::step<0>(st);
-    if (i + 1 < left) o[mrg::kOrder + lane] = mrg::step<1>(st);
+    if (i < left) put(o + lane, mrg::step<0>(st));
+    if (i + 1 < left) put(o + mrg::kOrder + lane, mrg::step<1>(st));
 }
 
 // One lane per hypothesis.  rand_list (4,n) uint32, pool_src / pool_tar (size,2) binary64

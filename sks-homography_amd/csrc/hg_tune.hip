@@ -865,13 +865,17 @@ int hg_tune_rocrand_mrg32k3a_u32(uint32_t* out, int64_t count, uint64_t seed, vo
 
 // The standalone generator with another split threshold (positions per thread).
 // min_chunk >= 2^20 + 1 ... : ablations (wrong bits, timing only) at the shipped split --
-// 2^20 + 1 no table jumps, 2^20 + 2 no engine steps, 2^20 + 3 neither.
+// 2^20 + 1 no table jumps, 2^20 + 2 no engine steps, 2^20 + 3 neither; 2^20 + 4 the shipped
+// kernel with non-temporal stores (same bits); 2^21 + c: non-temporal stores at split c.
 int hg_tune_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t min_chunk,
                       void* stream) {
     if (count <= 0 || !out || min_chunk < 1) return (int)hipErrorInvalidValue;
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (min_chunk > (1 << 21))
+        return hg::launch_mrg_words<4>(out, count, seed, min_chunk - (1 << 21), s);
     const int64_t abl = min_chunk > (1 << 20) ? min_chunk - (1 << 20) : 0;
     switch (abl) {
+        case 4: return hg::launch_mrg_words<4>(out, count, seed, hg::kMrgMinChunk, s);
         case 0: return hg::launch_mrg_words(out, count, seed, min_chunk, s);
         case 1: return hg::launch_mrg_words<1>(out, count, seed, hg::kMrgMinChunk, s);
         case 2: return hg::launch_mrg_words<2>(out, count, seed, hg::kMrgMinChunk, s);
