@@ -579,7 +579,7 @@ def torch_aca_vanilla(src, tar):
     h2 = m0 * det_s - h0 * src[:, 0, 0] - h1 * src[:, 0, 1]
     h5 = m1 * det_s - h3 * src[:, 0, 0] - h4 * src[:, 0, 1]
     h8 = c33 * det_s - h6 * src[:, 0, 0] - h7 * src[:, 0, 1]
-    H = torch.ones((bs, 9), device=src.device, dtype=src.dtype)   # :372-382
+    H = torch.ones((bs, 9), device=src.device)   # :372-382 (torch's default dtype)
     for k, v in enumerate((h0, h1, h2, h3, h4, h5, h6, h7, h8)):
         H[:, k] = v
     return H.reshape(bs, 3, 3)

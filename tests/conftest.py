@@ -48,3 +48,20 @@ def load_golden(name):
         pytest.fail(f"golden fixture {path} missing (run tools/make_golden.py here)")
     with np.load(path, allow_pickle=False) as z:
         return {k: z[k] for k in z.files}
+
+
+class default_dtype:
+    """torch's default dtype set for a block (the reference's statements allocate H with it:
+    torch.zeros / torch.ones without a dtype, Modules_Runtime_Test.py:297, :372)."""
+
+    def __init__(self, dt):
+        import torch
+        self.dt, self.torch = dt, torch
+
+    def __enter__(self):
+        self.prev = self.torch.get_default_dtype()
+        self.torch.set_default_dtype(self.dt)
+
+    def __exit__(self, *exc):
+        self.torch.set_default_dtype(self.prev)
+

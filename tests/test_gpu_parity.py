@@ -82,8 +82,14 @@ def test_golden_aca_f64_unnormalised(orc, pkg, dev, tag):
                          layout="soa").T, want, f"{tag} soa")
     _bits(orc, pkg.solve("aca", s, t, normalize=False), want, f"{tag} aos")
     B = src.shape[0]
-    _bits(orc, pkg.ACA_vanilla(B, _t(g[f"{tag}_src"], dev), _t(g[f"{tag}_tar"], dev)).reshape(B, 9),
-          want, f"{tag} ACA_vanilla f64")
+    from conftest import default_dtype
+    with default_dtype(torch.float64):  # as the fixture's statements ran
+        _bits(orc, pkg.ACA_vanilla(B, _t(g[f"{tag}_src"], dev), _t(g[f"{tag}_tar"], dev)).reshape(B, 9),
+              want, f"{tag} ACA_vanilla f64")
+    # under the float32 default the statements round each binary64 value once into H (.py:372)
+    H32 = pkg.ACA_vanilla(B, _t(g[f"{tag}_src"], dev), _t(g[f"{tag}_tar"], dev))
+    assert H32.dtype is torch.float32
+    _bits(orc, H32.reshape(B, 9), want.astype(np.float32), f"{tag} ACA_vanilla f64 inputs, f32 default")
     if tag == "wall":
         w = load_golden("cpp_wall.npz")
         ps = _t(w["pool_src"].astype(np.float64), dev)

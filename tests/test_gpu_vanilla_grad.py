@@ -23,8 +23,8 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import load_golden
 from bench import torch_aca_vanilla
+from conftest import default_dtype, load_golden
 
 pytestmark = pytest.mark.gpu
 
@@ -56,9 +56,11 @@ def test_backward_equals_reference_autograd_fixture(orc, pkg, dev, gold):
         assert none_t.numel() == 0 and none_s.numel() == 0
         _same(orc, only_s, ws, f"op grad src alone {tag}")
         _same(orc, only_t, wt, f"op grad tar alone {tag}")
-        # torch.autograd through the reference-API mirror, and the (B,8) layout
+        # torch.autograd through the reference-API mirror (with the fixture's default dtype),
+        # and the (B,8) layout
         S, T = src.clone().requires_grad_(), tar.clone().requires_grad_()
-        H = pkg.ACA_vanilla(B, S, T)
+        with default_dtype(src.dtype):
+            H = pkg.ACA_vanilla(B, S, T)
         _same(orc, H, gold[f"{tag}_H"], f"forward {tag}")
         H.backward(gH)
         _same(orc, S.grad, ws, f"autograd src {tag}")
@@ -70,7 +72,9 @@ def test_backward_equals_reference_autograd_fixture(orc, pkg, dev, gold):
         _same(orc, T8.grad, wt.reshape(B, 8), f"autograd (B,8) tar {tag}")
         # tar alone requiring grad (the deep-homography case: a fixed source quad)
         T1 = tar.clone().requires_grad_()
-        pkg.ACA_vanilla(B, src, T1).backward(gH)
+        with default_dtype(src.dtype):
+            H1 = pkg.ACA_vanilla(B, src, T1)
+        H1.backward(gH)
         _same(orc, T1.grad, wt, f"autograd tar alone {tag}")
 
 
@@ -153,8 +157,32 @@ def test_backward_f64_equals_aten_autograd_on_box_cpu(orc, pkg, dev):
     tar = rng.uniform(-512, 512, (n, 4, 2)) * 10.0 ** rng.integers(-6, 7, (n, 1, 1))
     gH = rng.standard_normal((n, 3, 3))
     S, T = torch.from_numpy(src).requires_grad_(), torch.from_numpy(tar).requires_grad_()
-    torch_aca_vanilla(S, T).backward(torch.from_numpy(gH))
+    with default_dtype(torch.float64):
+        H = torch_aca_vanilla(S, T)
+    H.backward(torch.from_numpy(gH))
     g_src, g_tar = pkg.aca_backward(torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev),
                                     torch.from_numpy(gH).to(dev))
     _same(orc, g_src, S.grad.numpy(), "f64 grad src")
     _same(orc, g_tar, T.grad.numpy(), "f64 grad tar")
+
+
+def test_binary64_inputs_under_the_float32_default(orc, pkg, dev, gold):
+    """The reference's statements write into torch.ones((bs, 9)) -- torch's default dtype
+    (.py:372) -- so binary64 inputs under the float32 default give a float32 H (each binary64
+    value rounded once) and binary64 gradients of a float32 upstream gradient.  ACA_vanilla does
+    the same, and its gradients equal ATen autograd's through the statements on the CPU."""
+    tag = "f64_uniform"
+    src, tar = (torch.from_numpy(gold[f"{tag}_{k}"]) for k in ("src", "tar"))
+    B = src.shape[0]
+    g32 = torch.from_numpy(gold[f"{tag}_gH"].astype(np.float32))
+    S, T = src.clone().requires_grad_(), tar.clone().requires_grad_()
+    H = torch_aca_vanilla(S, T)  # the float32 default
+    assert H.dtype is torch.float32
+    H.backward(g32)
+    Sd, Td = src.to(dev).requires_grad_(), tar.to(dev).requires_grad_()
+    Hd = pkg.ACA_vanilla(B, Sd, Td)
+    assert Hd.dtype is torch.float32
+    _same(orc, Hd, H.detach().numpy(), "forward, f32 default")
+    Hd.backward(g32.to(dev))
+    _same(orc, Sd.grad, S.grad.numpy(), "grad src, f32 default")
+    _same(orc, Td.grad, T.grad.numpy(), "grad tar, f32 default")

@@ -401,11 +401,13 @@ def test_vanilla_restatement_builds_the_reference_graph(orc):
     same graph as the reference's statements."""
     import torch
     from bench import torch_aca_vanilla
+    from conftest import default_dtype
     g = load_golden("torch_vanilla_grad.npz")
     for tag in (str(t) for t in g["cases"]):
         S = torch.from_numpy(g[f"{tag}_src"].copy()).requires_grad_()
         T = torch.from_numpy(g[f"{tag}_tar"].copy()).requires_grad_()
-        H = torch_aca_vanilla(S, T)
+        with default_dtype(S.dtype):  # as the fixture was made
+            H = torch_aca_vanilla(S, T)
         H.backward(torch.from_numpy(g[f"{tag}_gH"]))
         _assert_bits(orc, H.detach().numpy(), g[f"{tag}_H"], f"H {tag}")
         _assert_bits(orc, S.grad.numpy(), g[f"{tag}_gsrc"], f"grad src {tag}")
