@@ -150,20 +150,27 @@ def test_backward_equals_aten_autograd_on_box_cpu(orc, pkg, dev, kind):
     _same(orc, g_tar, T.grad.numpy(), f"grad tar {kind}")
 
 
-def test_backward_f64_equals_aten_autograd_on_box_cpu(orc, pkg, dev):
-    rng = np.random.default_rng(64)
+@pytest.mark.parametrize("kind", ["scaled", "random_bits", "special_mixture"])
+def test_backward_f64_equals_aten_autograd_on_box_cpu(orc, pkg, dev, kind):
+    rng = np.random.default_rng(zlib.crc32(("f64" + kind).encode()))
     n = 100_003
-    src = rng.uniform(-512, 512, (n, 4, 2)) * 10.0 ** rng.integers(-6, 7, (n, 1, 1))
-    tar = rng.uniform(-512, 512, (n, 4, 2)) * 10.0 ** rng.integers(-6, 7, (n, 1, 1))
-    gH = rng.standard_normal((n, 3, 3))
+
+    def draw(shape):
+        if kind == "random_bits":
+            return rng.integers(0, 2**64 - 1, size=shape, dtype=np.uint64, endpoint=True).view(np.float64)
+        if kind == "special_mixture":
+            return rng.choice(SPECIALS.astype(np.float64), size=shape, p=WEIGHTS / WEIGHTS.sum())
+        return rng.uniform(-512, 512, shape) * 10.0 ** rng.integers(-6, 7, (shape[0],) + (1,) * (len(shape) - 1))
+
+    src, tar, gH = draw((n, 4, 2)), draw((n, 4, 2)), draw((n, 3, 3))
     S, T = torch.from_numpy(src).requires_grad_(), torch.from_numpy(tar).requires_grad_()
     with default_dtype(torch.float64):
         H = torch_aca_vanilla(S, T)
     H.backward(torch.from_numpy(gH))
     g_src, g_tar = pkg.aca_backward(torch.from_numpy(src).to(dev), torch.from_numpy(tar).to(dev),
                                     torch.from_numpy(gH).to(dev))
-    _same(orc, g_src, S.grad.numpy(), "f64 grad src")
-    _same(orc, g_tar, T.grad.numpy(), "f64 grad tar")
+    _same(orc, g_src, S.grad.numpy(), f"f64 grad src {kind}")
+    _same(orc, g_tar, T.grad.numpy(), f"f64 grad tar {kind}")
 
 
 def test_binary64_inputs_under_the_float32_default(orc, pkg, dev, gold):
