@@ -127,6 +127,13 @@ def test_native_ops_pass_torch_opcheck(pkg, dev):
     q = torch.rand(B, 4, 2, device=dev) * 100
     torch.library.opcheck(ops.aca.default, (q, q + 1.5, True),
                           test_utils=("test_schema", "test_faketensor"))
+    # ACA_vanilla's differentiable form (normalize=False), float32 and float64
+    for dt in (torch.float32, torch.float64):
+        qg = q.to(dt).clone().requires_grad_(True)
+        torch.library.opcheck(ops.aca.default, (qg, (q + 1.5).to(dt), False), test_utils=tests)
+        torch.library.opcheck(ops.aca_backward.default,
+                              (q.to(dt), (q + 1.5).to(dt), torch.randn(B, 3, 3, device=dev, dtype=dt),
+                               True, True), test_utils=("test_schema", "test_faketensor"))
     torch.library.opcheck(ops.sks.default, (q, q + 1.5, False),
                           test_utils=("test_schema", "test_faketensor"))
 
