@@ -52,7 +52,7 @@ def load_golden(name):
 
 class default_dtype:
     """torch's default dtype set for a block (the reference's statements allocate H with it:
-    torch.zeros / torch.ones without a dtype, Modules_Runtime_Test.py:297, :372)."""
+    torch.zeros / torch.ones without a dtype, Modules_Runtime_Test.py:296, :372)."""
 
     def __init__(self, dt):
         import torch
