@@ -111,6 +111,7 @@ for step in $STEPS; do
         kbench_mrg) run kbench_mrg 300 python tools/kbench_mrg.py ;;
         kbench_mrg_words) run kbench_mrg_words 300 python tools/kbench_mrg_words.py ;;
         t8_order) run t8_order 300 python tools/t8_order_probe.py ;;
+        single_call) run single_call 120 tools/_build/single_call_probe ;;
         kbench_gather_st) KB_ROUNDS=11 KB_GATHER_VARIANTS=0,7,3 run kbench_gather_st 300 python tools/kbench_gather.py ;;
         kbench_stp)  # the seeded sampler's H stores under other cache policies, ACA then SKS
             KB_ROUNDS=11 KB_SEEDED_ONLY=1 KB_SEEDED_VARIANTS=0,22,23,24,25,26,27 run kbench_stp 300 \
