@@ -116,3 +116,34 @@ def test_backward_equals_aten_autograd_on_box_cpu(orc, pkg, dev, kind, per_probl
     if per_problem:
         _same(orc, g_sc, s_.grad.numpy(), f"grad scale {kind}")
         _same(orc, g_dv, d_.grad.numpy(), f"grad div {kind}")
+
+
+def test_offsets_gradient_equals_aten_autograd_through_the_reference_construction(orc, pkg, dev):
+    """The compact deep-homography form against what a reference user writes: the source
+    rectangle built as getInput builds it, tar = src + offsets as getTar does (.py:9-21), the
+    homogeneous tensors as adjust makes them (.py:24-37), then TensorACA_rect's statements
+    under autograd on this box's CPU -- the offsets' gradient equals the op's bit for bit."""
+    if not orc.cpu_has_avx512():
+        pytest.skip("ATen's CPU cross takes its AVX-512 FMA path only on an AVX-512 host")
+    import bench
+    n = 100_003
+    rng = np.random.default_rng(2718)
+    corner = rng.integers(10, 30, (n, 2)).astype(np.float32)
+    offs = (rng.random((n, 4, 2)) * 32).astype(np.float32)
+    gH = rng.standard_normal((n, 3, 3)).astype(np.float32)
+    rect = torch.tensor([[0.0, 0.0], [128.0, 0.0], [0.0, 128.0], [128.0, 128.0]])
+    src = torch.from_numpy(corner)[:, None, :] + rect[None]
+    off_t = torch.from_numpy(offs).requires_grad_()
+    tar = src + off_t
+    ones = torch.ones((n, 1, 4))
+    src_h = torch.cat((src.transpose(1, 2), ones), dim=1)
+    tar_h = torch.cat((tar.transpose(1, 2), ones), dim=1)
+    H = bench.torch_tensor_aca_rect(src_h, tar_h, torch.tensor([128.0]), torch.tensor([1.0]))
+    H.backward(torch.from_numpy(gH))
+    g_off, _ = pkg.tensor_aca_offsets_backward(torch.from_numpy(corner).to(dev),
+                                               torch.from_numpy(offs).to(dev),
+                                               torch.from_numpy(gH).to(dev), 128.0, 128.0, False)
+    _same(orc, H.detach().numpy(), pkg.tensor_aca_offsets(torch.from_numpy(corner).to(dev),
+                                                           torch.from_numpy(offs).to(dev),
+                                                           128.0, 128.0).cpu().numpy(), "forward")
+    _same(orc, g_off, off_t.grad.numpy(), "grad offsets")
