@@ -193,3 +193,23 @@ def test_binary64_inputs_under_the_float32_default(orc, pkg, dev, gold):
     Hd.backward(g32.to(dev))
     _same(orc, Sd.grad, S.grad.numpy(), "grad src, f32 default")
     _same(orc, Td.grad, T.grad.numpy(), "grad tar, f32 default")
+
+
+@pytest.mark.parametrize("kind", ["random_bits", "special_mixture", "scaled"])
+def test_equals_the_reference_statements_run_on_this_gpu(orc, pkg, dev, kind):
+    """The reference runs its statements with device='cuda' (.py:393): ACA_vanilla's are
+    element-wise products and differences only, so ROCm's ATen evaluates them exactly as the
+    CPU does, and autograd sums the same terms in the same order -- forward and both gradients
+    equal the op's bit for bit on the GPU itself (unlike TensorACA_rect, whose torch.sum order
+    differs on ROCm: tests/test_gpu_parity.py)."""
+    rng = np.random.default_rng(zlib.crc32(("gpu" + kind).encode()))
+    src, tar, gH = (torch.from_numpy(_inputs(kind, rng, sh)).to(dev) for sh in ((B, 4, 2), (B, 4, 2), (B, 3, 3)))
+    S, T = src.clone().requires_grad_(), tar.clone().requires_grad_()
+    H = torch_aca_vanilla(S, T)
+    H.backward(gH)
+    S2, T2 = src.clone().requires_grad_(), tar.clone().requires_grad_()
+    H2 = pkg.ACA_vanilla(B, S2, T2)
+    H2.backward(gH)
+    _same(orc, H2, H.detach().cpu().numpy(), f"forward {kind}")
+    _same(orc, S2.grad, S.grad.cpu().numpy(), f"grad src {kind}")
+    _same(orc, T2.grad, T.grad.cpu().numpy(), f"grad tar {kind}")
