@@ -211,7 +211,10 @@ def test_rect_close_to_torch_composed_on_gpu(pkg, dev, B):
     path (bit-exact) and cannot hold against the GPU composition for any CPU-exact
     implementation; the bar here is that spread: per H (normwise) and per row, the op is no
     farther from the GPU composition than the reference on the CPU is.  The measured maxima,
-    and how far torch.cross alone moves between the devices, are printed."""
+    and how far torch.cross alone moves between the devices, are printed.  And the whole
+    spread is the sum's order: ROCm's ATen adds the three cross terms as (c0 + c2) + c1
+    (tools/rocm_sum_probe.py), and the statements with that one order changed, run on the
+    CPU, equal the GPU composition exactly (asserted)."""
     import bench
     torch.manual_seed(0)
     _, _, sh, th, sc, dv = pkg.adjust(dev, B)
@@ -240,6 +243,20 @@ def test_rect_close_to_torch_composed_on_gpu(pkg, dev, B):
               f"{srow:.3e}; torch.cross CPU vs GPU: {cross_diff} of {cc.numel()} elements differ, "
               f"torch.sum of the cross terms: {sum_diff} of {B}")
         assert mat <= max(1e-6, smat) and row <= max(1e-6, srow), (tag, mat, row, smat, srow)
+        # the whole gap is the sum's order: ROCm's ATen adds the three cross terms as
+        # (c0 + c2) + c1 (profiles/r03/rocm_sum_probe.json); the statements restated on the CPU
+        # with that one order changed give the GPU composition bit for bit
+        sc_c, dv_c, s_c, t_c = sc.cpu(), dv.cpu(), sh.cpu(), t.cpu()
+        dd = t_c[:, :, 1:] - t_c[:, :, 0:1]
+        q = torch.cross(dd[:, 1:2, :], dd[:, 0:1, :], dim=2)
+        qs = (q[:, :, 0:1] + q[:, :, 2:3]) + q[:, :, 1:2]
+        ht = qs * t_c[:, :, 0:1]
+        H = torch.zeros((B, 3, 3))
+        H[:, :, 0:1] = t_c[:, :, 1:2] * q[:, :, 0:1] - ht
+        H[:, :, 1:2] = torch.mul(dv_c, t_c[:, :, 2:3] * q[:, :, 1:2] - ht)
+        H[:, :, 2:3] = sc_c * ht - s_c[:, 0:1, 0:1] * H[:, :, 0:1] - s_c[:, 1:2, 0:1] * H[:, :, 1:2]
+        assert torch.equal(H, bench.torch_tensor_aca_rect(sh, t, sc, dv).cpu()), \
+            f"{tag}: the GPU composition is not the CPU statements with ROCm's sum order"
 
 
 # -------------------------------------------------------------- other entries
