@@ -70,6 +70,58 @@ def parse():
     return ap.parse_args()
 
 
+def launch_plan(gpus: int, env) -> tuple[str, str]:
+    """What ``--gpus N`` means for this process, decided before anything touches a GPU:
+    ("self", "") -- run as this rank: N = 1 alone, or a torch.distributed.run rank whose
+    WORLD_SIZE equals N; ("spawn", why) -- N > 1 and no WORLD_SIZE: start N ranks under
+    torch.distributed.run as a child process; ("refuse", why) -- WORLD_SIZE is set and is not
+    N, or N < 1 (a job that would report a GPU count it did not run on)."""
+    if gpus < 1:
+        return "refuse", f"--gpus {gpus}: at least one GPU"
+    ws = env.get("WORLD_SIZE")
+    if ws is None or ws == "":
+        if gpus == 1:
+            return "self", ""
+        return "spawn", f"--gpus {gpus} without WORLD_SIZE: starting {gpus} ranks"
+    try:
+        world = int(ws)
+    except ValueError:
+        return "refuse", f"WORLD_SIZE={ws!r} is not an integer"
+    if world != gpus:
+        return "refuse", f"WORLD_SIZE={world} but --gpus {gpus}: the line would misreport n_gpus"
+    return "self", ""
+
+
+def _free_port() -> int:
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def torchrun_cmd(gpus: int, argv, port: int) -> list:
+    """The child command of launch_plan's "spawn": one process per GPU on this node, the
+    rendezvous on the loopback address (the container's hostname may not resolve)."""
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+            f"--nproc-per-node={gpus}", "--master-addr=127.0.0.1", f"--master-port={port}",
+            os.path.abspath(__file__), *argv]
+
+
+def spawn_ranks(gpus: int, argv) -> int:
+    """Runs torch.distributed.run as a CHILD (never exec: see the process rules in DESIGN
+    §7) and passes its stdout through line by line -- rank 0's JSON line among it -- then
+    returns its exit status.  No GPU call happens in this process."""
+    import subprocess
+    cmd = torchrun_cmd(gpus, argv, _free_port())
+    print(f"bench.py: {' '.join(cmd[1:5])} ... (--gpus {gpus}, no WORLD_SIZE)", file=sys.stderr,
+          flush=True)
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    for text in proc.stdout:
+        sys.stdout.write(text)
+        sys.stdout.flush()
+    return proc.wait()
+
+
 def _kfd_gpu_bdfs(base: str = "/sys/class/kfd/kfd/topology/nodes"):
     """PCI addresses of the node's GPUs in KFD topology order (the order the HIP runtime
     numbers them), read from /sys without touching the GPU."""
@@ -1166,6 +1218,14 @@ def rank_block_inputs(pkg, dev, n: int, n_total: int, rank: int):
 
 def main():
     args = parse()
+    # --gpus N is authoritative: a bare `bench.py --gpus 8` starts the 8 ranks itself, and a
+    # rank whose WORLD_SIZE disagrees with --gpus refuses to run (before any GPU call)
+    plan, why = launch_plan(args.gpus, os.environ)
+    if plan == "refuse":
+        print(f"bench.py: {why}", file=sys.stderr, flush=True)
+        sys.exit(2)
+    if plan == "spawn":
+        sys.exit(spawn_ranks(args.gpus, sys.argv[1:]))
     # before anything touches the GPU: this rank's CPUs and first-touch pages on its GPU's
     # NUMA node (the device index is LOCAL_RANK, as Dist picks it)
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1174,6 +1234,7 @@ def main():
     else:  # gloo rehearsal: ranks share the devices (device_count does not initialise HIP here)
         numa = bind_numa(local % max(torch.cuda.device_count(), 1))
     d = Dist(args.dist_backend)
+    assert d.world == args.gpus, f"n_gpus {d.world} != --gpus {args.gpus}"
     numa["rank"] = d.rank
     try:  # the device HIP gave this rank is the one bound to
         pr = torch.cuda.get_device_properties(d.dev)
