@@ -98,9 +98,11 @@ int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float*
 /* Backward of hg_tensor_aca_rect_f32 (the gradients ATen autograd gives the
  * reference's composed TensorACA_rect, Modules_Runtime_Test.py:294-302).  grad_H:
  * (B,3,3) dL/dH.  Writes grad_tar (B,3,4); grad_src (B,3,4, only [0][0] and [1][0]
- * non-zero) when non-NULL; grad_scale_div (2,B) per-problem partials -- row 0 of
- * dL/dscale, row 1 of dL/ddiv -- when non-NULL (the caller sums each row).  scale, div:
- * device pointers. */
+ * non-zero) when non-NULL; grad_scale_div (2,B,3) when non-NULL: [0] the (problem, row)
+ * terms of dL/dscale, [1] those of dL/ddiv, each in the order of the (B,3,1) tensor ATen
+ * autograd sums to the (1,) parameter -- reduce each half with hg_sum_aten_f32 (rows 1,
+ * m 3B) for the reference's bits.  scale, div: device pointers.  (Until round 3 this
+ * array was (2,B) per-problem sums.) */
 int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
                                     int64_t B, const float* scale, const float* div,
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
@@ -118,10 +120,12 @@ int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, i
                                  const float* div, int64_t div_sb, int64_t div_sr, void* stream);
 
 /* Its backward: grad_tar (B,3,4), grad_src (B,3,4) when non-NULL, and per parameter, when
- * its pointer is non-NULL, either each row's share of dL/dparam(b, r) ((3,B), row r at
- * [r * B], when *_rows != 0) or each problem's three-row sum ((B), the per-problem partial
- * of hg_tensor_aca_rect_backward_f32).  The caller sums them over the parameter's broadcast
- * dimensions (hg_sum_rows_f32). */
+ * its pointer is non-NULL and by its *_rows mode: 0 -- each problem's three-row sum ((B):
+ * ATen's reduction to a (B,1,1) parameter, final); 1 -- each row's share of dL/dparam(b, r)
+ * as (3,B) rows, row r at [r * B]; 2 -- the same terms as (B,3), [3 b + r] (the order ATen
+ * sums them to a batch-uniform parameter).  The caller sums modes 1 / 2 over the
+ * parameter's broadcast dimensions in ATen's order (hg_sum_aten_f32: mode 1 rows 3,
+ * lanes 1 for a (3,1) parameter; mode 2 rows 1 for a one-value parameter). */
 int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, const float* grad_H,
                                           int64_t B, const float* scale, int64_t scale_sb,
                                           int64_t scale_sr, const float* div, int64_t div_sb,
@@ -302,6 +306,18 @@ int hg_solve_grouped_f64(int algo, const double* const* src, const double* const
  * not depend on timing.  x is OVERWRITTEN (used as the scratch for the chunk sums).
  * rows <= 65535.  Reduces hg_tensor_aca_rect_backward_f32's (2,B) partials. */
 int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stream);
+
+/* Sums in ATen-CPU's float32 order (SumKernel.cpp cascade_sum under TensorIterator's
+ * two-pass reduction; restated in oracle/aten_sum.py, pinned against torch.sum): row r of x
+ * is x[r * row_stride + e * elem_stride], e < m, and out[r] receives the bits torch.sum of
+ * that run gives on ATen-CPU with Vectorized<float>::size() == lanes (8: ATen's sum kernel
+ * runs its 8-lane build on AVX2 and AVX-512 hosts alike) and at::get_num_threads() ==
+ * threads.  lanes 1, threads 1 give the order of a strided column reduced to (C,1) (the
+ * (3,1) parameter case).  1 <= lanes <= 16, 1 <= threads <= 1024, lanes >= 4 when
+ * threads > 1; rows * min(threads, ceil(m / 32768)) <= 65535.  x is OVERWRITTEN (scratch).
+ * Reduces the gradient terms of hg_tensor_aca_rect_backward_f32 and *_bcast_*. */
+int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
+                    int lanes, int threads, float* out, void* stream);
 
 /* Device-to-device streaming copy (float4) used by bench.py as the measured
  * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */

@@ -212,6 +212,23 @@ class Oracle:
                                         _ptr(H, _f32p), src.shape[0], threads, reps)
 
 
+def rect_grad_batch(o: "Oracle", B: int, seed: int):
+    """A deterministic TensorACA batch for the large gradient fixtures (no stored arrays):
+    128 x 128 rectangles at corners in [10, 30), targets offset by [0, 32), dL/dH in [-1, 1),
+    all drawn from fill_uniform's counter streams and assembled with float32 additions.
+    Returns (src_h, tar_h, gH): (B,3,4), (B,3,4), (B,3,3) float32."""
+    corner = o.fill_uniform(2 * B, seed, 0, 10.0, 30.0).reshape(B, 2)
+    off = o.fill_uniform(8 * B, seed, 2 * B, 0.0, 32.0).reshape(B, 4, 2)
+    gH = o.fill_uniform(9 * B, seed, 10 * B, -1.0, 1.0).reshape(B, 3, 3)
+    rect = np.array([[0, 0], [128, 0], [0, 128], [128, 128]], np.float32)
+    src = corner[:, None, :] + rect[None]
+    tar = src + off
+    ones = np.ones((B, 1, 4), np.float32)
+    src_h = np.ascontiguousarray(np.concatenate([src.transpose(0, 2, 1), ones], 1))
+    tar_h = np.ascontiguousarray(np.concatenate([tar.transpose(0, 2, 1), ones], 1))
+    return src_h, tar_h, np.ascontiguousarray(gH)
+
+
 class RefOracle:
     """The reference's own solver bodies (oracle/_ref/libsks_ref.so)."""
 

@@ -66,6 +66,7 @@ SIGNATURES = {
     "hg_solve_grouped_f32": ([_int, _vp, _vp, _vp, _vp, _int, _int, _int, _vp], _int),
     "hg_solve_grouped_f64": ([_int, _vp, _vp, _vp, _vp, _int, _int, _int, _vp], _int),
     "hg_sum_rows_f32": ([_vp, _i64, _i64, _vp, _vp], _int),
+    "hg_sum_aten_f32": ([_vp, _i64, _i64, _i64, _i64, _int, _int, _vp, _vp], _int),
     "hg_stream_copy": ([_vp, _vp, _i64, _vp], _int),
     "hg_version": ([], ctypes.c_char_p),
 }

@@ -20,6 +20,7 @@
 #include "hg_aos.hpp"
 #include "hg_launch.hpp"
 #include "hg_rect.hpp"
+#include "hg_reduce.hpp"
 #include "hg_soa.hpp"
 #include "hg_solvers.hpp"
 #include "sks_homography.h"
@@ -595,10 +596,11 @@ int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, co
     if (B < 0) return hg::kErrInvalid;
     if (B == 0) return 0;
     if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
+    if (scale_rows < 0 || scale_rows > 2 || div_rows < 0 || div_rows > 2) return hg::kErrInvalid;
     const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
     return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel, hg::generic_grid(B), hg::kBlock,
                       0, reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, B, a, grad_src,
-                      grad_tar, grad_scale, scale_rows ? 1 : 0, grad_div, div_rows ? 1 : 0);
+                      grad_tar, grad_scale, scale_rows, grad_div, div_rows);
 }
 
 int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,
@@ -728,6 +730,37 @@ int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stre
         if (rc) return rc;
     }
     return hg::launch(hg::sum_rows_pass2, (unsigned)rows, hg::kBlock, 0, s, x, cols, chunks, out);
+}
+
+int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
+                    int lanes, int threads, float* out, void* stream) {
+    if (rows < 0 || m < 0 || lanes < 1 || lanes > hg::kAtenMaxLanes || threads < 1 ||
+        threads > hg::kAtenMaxThreads || (threads > 1 && lanes < 4))
+        return hg::kErrInvalid;
+    if (rows == 0) return 0;
+    if (!out || (m > 0 && !x)) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int64_t want = hg::ceil_div(m, hg::kAtenGrain);
+    const int64_t chunks = threads > 1 && m >= hg::kAtenGrain ? (want < threads ? want : threads) : 1;
+    const int64_t runs = rows * chunks;
+    if (runs > 65535) return hg::kErrInvalid;
+    const hg::AtenSum a{x, row_stride, elem_stride, m, chunks > 1 ? hg::ceil_div(m, chunks) : m,
+                        (int)chunks, lanes};
+    const hg::AtenRun r0(a, 0);  // the longest run sizes the grids
+    if (r0.nb > 0) {
+        const int64_t bx = hg::ceil_div((r0.g1 + 1) * r0.S, (int64_t)256);
+        if (bx > 0x7fffffffLL) return hg::kErrInvalid;
+        const int rc = hg::launch(hg::aten_sum_l1, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
+        if (rc) return rc;
+    }
+    if (r0.g1 > 0) {
+        const int64_t bx = hg::ceil_div((r0.g2 + 1) * r0.S, (int64_t)256);
+        const int rc = hg::launch(hg::aten_sum_l2, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
+        if (rc) return rc;
+    }
+    const int rc = hg::launch(hg::aten_sum_l3, (unsigned)runs, 64, 0, s, a, out);
+    if (rc || chunks == 1) return rc;
+    return hg::launch(hg::aten_sum_l4, (unsigned)rows, 64, 0, s, a, threads, lanes, out);
 }
 
 const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }

@@ -78,8 +78,17 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
 // ---------------------------------------------------------------------------
 // TensorACA rect backward: one lane per problem, grid-stride.  Writes dL/dtar
 // (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and the
-// per-problem dL/dscale and dL/ddiv partials as the rows of a (2,B) array the caller
-// reduces.
+// (problem, row) terms of dL/dscale and dL/ddiv as a (2,B,3) array -- each half in the
+// order of the (B,3,1) tensor ATen autograd sums to the (1,) parameter (hg_sum_aten_f32).
+__device__ __forceinline__ void store_sd_terms(float* __restrict__ gsd, int64_t B, int64_t p,
+                                               const float (&gsr)[3], const float (&gdr)[3]) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+        gsd[3 * p + r] = gsr[r];
+        gsd[3 * B + 3 * p + r] = gdr[r];
+    }
+}
+
 template <bool WANT_SRC, bool WANT_SD>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
@@ -93,19 +102,16 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
         for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
-        float gmx, gmy, gscale, gdiv;
-        tensor_aca_rect_grad(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx, gmy,
-                             gscale, gdiv);
+        float gmx, gmy, gsr[3], gdr[3];
+        tensor_aca_rect_grad_terms(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx,
+                                   gmy, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
-        if constexpr (WANT_SD) {
-            gsd[p] = gscale;      // (2,B): each row reduces as one contiguous run
-            gsd[B + p] = gdiv;
-        }
+        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
     }
 }
 
@@ -187,9 +193,11 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
     for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[0][k];
 }
 
-// Its backward: dL/dtar, optionally dL/dsrc, and per parameter either each row's share
-// ((3,B): gs[r * B + p]) or the problem's three-row sum ((B): gs[p], the uniform kernels'
-// per-problem partial, ((0 + t0) + t1) + t2); the caller reduces them to the parameter's shape.
+// Its backward: dL/dtar, optionally dL/dsrc, and per parameter (mode *_rows) the problem's
+// three-row sum ((B): gs[p] = ((0 + t0) + t1) + t2, ATen's reduction to a (B,1,1) shape; mode
+// 0), each row's share as (3,B) rows (gs[r * B + p]; mode 1) or as the (B,3) terms in the
+// order ATen sums them to a batch-uniform shape (gs[3 p + r]; mode 2); the caller reduces
+// them to the parameter's shape.
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, RectBcast a, float* __restrict__ gsrc, float* __restrict__ gtar,
@@ -212,17 +220,23 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_backward_kernel(
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
         if (gsc) {
-            if (sc_rows) {
+            if (sc_rows == 1) {
 #pragma unroll
                 for (int r = 0; r < 3; ++r) gsc[r * B + p] = gsr[r];
+            } else if (sc_rows == 2) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) gsc[3 * p + r] = gsr[r];
             } else {
                 gsc[p] = gscale;
             }
         }
         if (gdv) {
-            if (dv_rows) {
+            if (dv_rows == 1) {
 #pragma unroll
                 for (int r = 0; r < 3; ++r) gdv[r * B + p] = gdr[r];
+            } else if (dv_rows == 2) {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) gdv[3 * p + r] = gdr[r];
             } else {
                 gdv[p] = gdiv;
             }
@@ -343,8 +357,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
         __builtin_memcpy(tr, lds + lane * 48, 48);
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
-        float gmx, gmy, gscale, gdiv;
-        tensor_aca_rect_grad(tr, mx, my, scale, div, g, gt, gmx, gmy, gscale, gdiv);
+        float gmx, gmy, gsr[3], gdr[3];
+        tensor_aca_rect_grad_terms(tr, mx, my, scale, div, g, gt, gmx, gmy, gsr, gdr);
         wave_lds_sync();  // the staging below reuses the input bytes
         store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
         if constexpr (WANT_SRC) {
@@ -353,10 +367,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
             for (int k = 0; k < 12; ++k) gs[k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
             store_rows_staged<12, NT>(reinterpret_cast<char*>(gsrc + base * 12), gs, lds, lane);
         }
-        if constexpr (WANT_SD) {
-            gsd[p] = gscale;
-            gsd[B + p] = gdiv;
-        }
+        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
         return;
     }
     if (p < B) {
@@ -365,19 +376,16 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
         for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
-        float gmx, gmy, gscale, gdiv;
-        tensor_aca_rect_grad(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx, gmy,
-                             gscale, gdiv);
+        float gmx, gmy, gsr[3], gdr[3];
+        tensor_aca_rect_grad_terms(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx,
+                                   gmy, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
-        if constexpr (WANT_SD) {
-            gsd[p] = gscale;
-            gsd[B + p] = gdiv;
-        }
+        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
     }
 }
 

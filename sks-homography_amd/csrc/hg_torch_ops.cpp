@@ -8,6 +8,7 @@
 // launch, which is what bounds the reference's B = 64 K case (Modules_Runtime_Test.py:
 // 286-309 is launch-bound).  There is no CPU kernel: CPU tensors raise.
 #include <ATen/ATen.h>
+#include <ATen/Parallel.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
 #include <torch/autograd.h>
@@ -155,17 +156,42 @@ at::Tensor rect_scalar(const at::Tensor& src, const at::Tensor& tar, double scal
     return out;
 }
 
-// A parameter's gradient from the kernel's partials: summed over the dimensions it was
-// broadcast along, in hg_sum_rows_f32's fixed order, and shaped like the parameter.
+// ATen autograd reduces a broadcast parameter's (B,3,1) gradient terms with ATen-CPU's sum
+// (the reference runs its statements under .backward(), Modules_Runtime_Test.py:301-302):
+// its order depends on the vector width of the sum kernel -- 8 lanes on every x86 capability
+// (its AVX-512 build is not used for sums; measured, tests/test_aten_sum_order.py) -- and,
+// for a batch-uniform parameter of >= 32768 terms, on at::get_num_threads().  The op takes
+// the caller's thread count, so its gradient equals the one ATen-CPU autograd gives in the
+// calling process; aten_threads > 0 names another (a fixture made elsewhere).
+constexpr int kAtenLanes = 8;
+
+int aten_threads_of(int64_t requested) {
+    const int64_t t = requested > 0 ? requested : at::get_num_threads();
+    return (int)(t < 1 ? 1 : (t > 1024 ? 1024 : t));
+}
+
+// How the kernel writes a parameter's terms (hg_tensor_aca_rect_bcast_backward_f32's modes):
+// per problem (final for (B,1,1)), (3,B) rows, or (B,3) in ATen's full-reduction order.
+int terms_mode(const Bcast& b) {
+    if (b.over_b) return b.over_r ? 1 : 0;
+    return b.over_r ? 1 : 2;
+}
+
+// A parameter's gradient from the kernel's terms: summed over the dimensions it was
+// broadcast along in ATen-CPU's order, and shaped like the parameter.
 at::Tensor reduce_param_grad(at::Tensor part, const Bcast& b, const at::Tensor& param, int64_t B,
-                             void* stream) {
+                             int threads, void* stream) {
     if (b.over_b && b.over_r)  // (3,B) -> (B,3)
         return part.view({3, B}).t().contiguous().reshape(param.sizes());
-    if (b.over_b) return part.reshape(param.sizes());  // (B): one value per problem
-    const int64_t rows = b.over_r ? 3 : 1;              // (3,B) or (B): summed over b
-    at::Tensor g = at::empty({rows}, part.options());
-    hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), rows, B, g.data_ptr<float>(), stream),
-           "hg_sum_rows_f32");
+    if (b.over_b) return part.reshape(param.sizes());  // (B): ATen's per-problem three-row sums
+    at::Tensor g = at::empty({b.over_r ? 3 : 1}, part.options());
+    // (3,1): each (3,B) row as ATen sums a strided column (one lane, no threads); one value:
+    // the (B,3) terms as one run
+    const int rc = b.over_r ? hg_sum_aten_f32(part.data_ptr<float>(), 3, B, B, 1, 1, 1,
+                                              g.data_ptr<float>(), stream)
+                            : hg_sum_aten_f32(part.data_ptr<float>(), 1, 3 * B, 0, 1, kAtenLanes,
+                                              threads, g.data_ptr<float>(), stream);
+    hip_ok(rc, "hg_sum_aten_f32");
     return g.reshape(param.sizes());
 }
 
@@ -173,7 +199,8 @@ at::Tensor reduce_param_grad(at::Tensor part, const Bcast& b, const at::Tensor& 
 // or (0,) when not needed)
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& grad_,
-    const at::Tensor& scale_, const at::Tensor& div_, bool need_src, bool need_scale_div) {
+    const at::Tensor& scale_, const at::Tensor& div_, bool need_src, bool need_scale_div,
+    int64_t aten_threads) {
     const at::Device dev = tar_.device();
     on_gpu(src_, "src", dev);
     on_gpu(tar_, "tar", dev);
@@ -191,8 +218,9 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     at::Tensor none = at::empty({0}, tar.options());
     const c10::DeviceGuard guard(dev);
     void* st = stream_of(tar);
+    const int threads = aten_threads_of(aten_threads);
     if (one_value(scale_) && one_value(div_)) {
-        at::Tensor part = need_scale_div ? at::empty({2, B}, tar.options()) : none;
+        at::Tensor part = need_scale_div ? at::empty({2, 3 * B}, tar.options()) : none;
         hip_ok(hg_tensor_aca_rect_backward_f32(
                    src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
                    scale_.data_ptr<float>(), div_.data_ptr<float>(),
@@ -200,27 +228,28 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
                    need_scale_div && B ? part.data_ptr<float>() : nullptr, st),
                "hg_tensor_aca_rect_backward_f32");
         if (!need_scale_div) return {g_src, g_tar, none, none};
-        // per-problem partials summed on the device in a fixed order (hg_sum_rows_f32)
+        // each half's (B,3) terms summed in ATen-CPU's order (two rows of one call)
         at::Tensor g_sd = at::empty({2}, tar.options());
-        hip_ok(hg_sum_rows_f32(part.data_ptr<float>(), 2, B, g_sd.data_ptr<float>(), st),
-               "hg_sum_rows_f32");
+        hip_ok(hg_sum_aten_f32(part.data_ptr<float>(), 2, 3 * B, 3 * B, 1, kAtenLanes, threads,
+                               g_sd.data_ptr<float>(), st),
+               "hg_sum_aten_f32");
         return {g_src, g_tar, g_sd.slice(0, 0, 1).reshape(scale_.sizes()),
                 g_sd.slice(0, 1, 2).reshape(div_.sizes())};
     }
-    // each parameter's partials: one per (row, problem) where it varies over rows, else the
-    // problem's three-row sum
-    at::Tensor ps = need_scale_div ? at::empty({sb.over_r ? 3 * B : B}, tar.options()) : none;
-    at::Tensor pd = need_scale_div ? at::empty({db.over_r ? 3 * B : B}, tar.options()) : none;
+    // each parameter's terms in the layout its reduction reads (terms_mode)
+    const int ms = terms_mode(sb), md = terms_mode(db);
+    at::Tensor ps = need_scale_div ? at::empty({ms ? 3 * B : B}, tar.options()) : none;
+    at::Tensor pd = need_scale_div ? at::empty({md ? 3 * B : B}, tar.options()) : none;
     hip_ok(hg_tensor_aca_rect_bcast_backward_f32(
                src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
                scale_.data_ptr<float>(), sb.sb, sb.sr, div_.data_ptr<float>(), db.sb, db.sr,
                need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
-               need_scale_div && B ? ps.data_ptr<float>() : nullptr, sb.over_r ? 1 : 0,
-               need_scale_div && B ? pd.data_ptr<float>() : nullptr, db.over_r ? 1 : 0, st),
+               need_scale_div && B ? ps.data_ptr<float>() : nullptr, ms,
+               need_scale_div && B ? pd.data_ptr<float>() : nullptr, md, st),
            "hg_tensor_aca_rect_bcast_backward_f32");
     if (!need_scale_div) return {g_src, g_tar, none, none};
-    return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, st),
-            reduce_param_grad(pd, db, div_, B, st)};
+    return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, threads, st),
+            reduce_param_grad(pd, db, div_, B, threads, st)};
 }
 
 // ------------------------------------------------------------------ compact offsets form
@@ -447,13 +476,13 @@ at::Tensor call_rect(const at::Tensor& src, const at::Tensor& tar, const at::Ten
 // AOT autograd) sees their Meta kernels instead of a raw launch.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> call_rect_backward(
     const at::Tensor& src, const at::Tensor& tar, const at::Tensor& grad, const at::Tensor& scale,
-    const at::Tensor& div, bool need_src, bool need_sd) {
+    const at::Tensor& div, bool need_src, bool need_sd, int64_t threads) {
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::tensor_aca_rect_backward", "")
                          .typed<std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>(
                              const at::Tensor&, const at::Tensor&, const at::Tensor&,
-                             const at::Tensor&, const at::Tensor&, bool, bool)>();
-    return op.call(src, tar, grad, scale, div, need_src, need_sd);
+                             const at::Tensor&, const at::Tensor&, bool, bool, int64_t)>();
+    return op.call(src, tar, grad, scale, div, need_src, need_sd, threads);
 }
 
 std::tuple<at::Tensor, at::Tensor> call_offsets_backward(const at::Tensor& corner,
@@ -474,6 +503,8 @@ class RectFunction : public torch::autograd::Function<RectFunction> {
                               const at::Tensor& scale, const at::Tensor& div) {
         at::AutoDispatchBelowADInplaceOrView below;
         ctx->save_for_backward({src, tar, scale, div});
+        // the caller's ATen thread count: the backward may run on an autograd device thread
+        ctx->saved_data["threads"] = (int64_t)at::get_num_threads();
         return call_rect(src, tar, scale, div);
     }
 
@@ -483,7 +514,8 @@ class RectFunction : public torch::autograd::Function<RectFunction> {
         const bool need_src = ctx->needs_input_grad(0);
         const bool need_sd = ctx->needs_input_grad(2) || ctx->needs_input_grad(3);
         auto [g_src, g_tar, g_scale, g_div] =
-            call_rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd);
+            call_rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd,
+                               ctx->saved_data["threads"].toInt());
         at::Tensor none;
         return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none,
                 ctx->needs_input_grad(2) ? g_scale : none, ctx->needs_input_grad(3) ? g_div : none};
@@ -504,6 +536,49 @@ at::Tensor rect_autograd(const at::Tensor& src, const at::Tensor& tar, const at:
         return call_rect(src, tar, scale, div);
     }
     return RectFunction::apply(src, tar, scale, div);
+}
+
+at::Tensor call_rect_scalar(const at::Tensor& src, const at::Tensor& tar, double scale, double div) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::tensor_aca_rect", "scalar")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&, double, double)>();
+    return op.call(src, tar, scale, div);
+}
+
+// tensor_aca_rect.scalar: scale / div are constants, so src and tar are the only inputs with a
+// gradient -- the tensor overload's backward with the two values as (1,) device tensors
+// (the same float32 values the forward's host-scalar kernel uses).
+class RectScalarFunction : public torch::autograd::Function<RectScalarFunction> {
+   public:
+    static at::Tensor forward(AutogradContext* ctx, const at::Tensor& src, const at::Tensor& tar,
+                              double scale, double div) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        ctx->save_for_backward({src, tar});
+        ctx->saved_data["scale"] = scale;
+        ctx->saved_data["div"] = div;
+        return call_rect_scalar(src, tar, scale, div);
+    }
+
+    static variable_list backward(AutogradContext* ctx, variable_list grads) {
+        const auto saved = ctx->get_saved_variables();
+        const auto opts = saved[1].options();
+        const at::Tensor sc = at::full({1}, (float)ctx->saved_data["scale"].toDouble(), opts);
+        const at::Tensor dv = at::full({1}, (float)ctx->saved_data["div"].toDouble(), opts);
+        const bool need_src = ctx->needs_input_grad(0);
+        auto [g_src, g_tar, g_sc, g_dv] =
+            call_rect_backward(saved[0], saved[1], grads[0].contiguous(), sc, dv, need_src, false, 0);
+        at::Tensor none;
+        return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none, none, none};
+    }
+};
+
+at::Tensor rect_scalar_autograd(const at::Tensor& src, const at::Tensor& tar, double scale,
+                                double div) {
+    if (!any_requires_grad({&src, &tar})) {
+        at::AutoDispatchBelowADInplaceOrView below;
+        return call_rect_scalar(src, tar, scale, div);
+    }
+    return RectScalarFunction::apply(src, tar, scale, div);
 }
 
 at::Tensor call_aca(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
@@ -545,13 +620,50 @@ class AcaFunction : public torch::autograd::Function<AcaFunction> {
 };
 
 at::Tensor aca_autograd(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
-    if (!any_requires_grad({&src, &tar})) {
+    if (!any_requires_grad({&src, &tar}) || normalize) {
+        if (normalize && any_requires_grad({&src, &tar}))
+            TORCH_WARN_ONCE("sks_amd::aca: normalize=True (the C++ API's H/H[8], ACA_SKS.cpp:94-98) "
+                            "has no gradient in the reference; H is returned without one -- "
+                            "ACA_vanilla's unnormalised form (normalize=False) is differentiable");
         at::AutoDispatchBelowADInplaceOrView below;
         return call_aca(src, tar, normalize);
     }
-    TORCH_CHECK(!normalize, "sks_amd::aca: normalize=True (the C++ API's H/H[8], ACA_SKS.cpp:94-98) "
-                "is not differentiable; ACA_vanilla's unnormalised form (normalize=False) is");
     return AcaFunction::apply(src, tar);
+}
+
+// sks_amd::solve is the C++ API's batch mirror (sks::runKernel_*, normalised by default):
+// nothing differentiates it in the reference, so it runs below autograd and says so once.
+at::Tensor solve_autograd(const at::Tensor& src, const at::Tensor& tar, int64_t algo,
+                          bool normalize, int64_t layout) {
+    if (any_requires_grad({&src, &tar}))
+        TORCH_WARN_ONCE("sks_amd::solve has no gradient (the C++ API it mirrors, ACA_SKS.cpp, is "
+                        "not differentiated by the reference); its output carries none -- "
+                        "sks_amd::aca (normalize=False, ACA_vanilla's form) is differentiable");
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::solve", "")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&, int64_t, bool,
+                                           int64_t)>();
+    at::AutoDispatchBelowADInplaceOrView below;
+    return op.call(src, tar, algo, normalize, layout);
+}
+
+at::Tensor call_sks(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
+    static auto op = c10::Dispatcher::singleton()
+                         .findSchemaOrThrow("sks_amd::sks", "")
+                         .typed<at::Tensor(const at::Tensor&, const at::Tensor&, bool)>();
+    return op.call(src, tar, normalize);
+}
+
+// The reference has no differentiable SKS (its PyTorch file composes ACA only, .py:286-388),
+// so an input that requires grad is refused here instead of reaching autograd's
+// not-implemented fallback (a warning now, an error at .backward()).
+at::Tensor sks_autograd(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
+    TORCH_CHECK(!any_requires_grad({&src, &tar}),
+                "sks_amd::sks has no backward (the reference differentiates ACA only: "
+                "Modules_Runtime_Test.py:286-388); call it on detached inputs or under "
+                "torch.no_grad(), or use sks_amd::aca (normalize=False) for gradients");
+    at::AutoDispatchBelowADInplaceOrView below;
+    return call_sks(src, tar, normalize);
 }
 
 at::Tensor call_offsets(const at::Tensor& corner, const at::Tensor& offsets, double w, double h) {
@@ -610,7 +722,8 @@ TORCH_LIBRARY(sks_amd, m) {
     m.def("tensor_aca_rect.scalar_out(Tensor src, Tensor tar, float scale, float div, *, "
           "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect_backward(Tensor src, Tensor tar, Tensor grad, Tensor scale, "
-          "Tensor div, bool need_src, bool need_scale_div) -> (Tensor, Tensor, Tensor, Tensor)");
+          "Tensor div, bool need_src, bool need_scale_div, int aten_threads=0) -> "
+          "(Tensor, Tensor, Tensor, Tensor)");
     m.def("aca_backward(Tensor src, Tensor tar, Tensor grad, bool need_src, bool need_tar) -> "
           "(Tensor, Tensor)");
     m.def("tensor_aca_offsets(Tensor corner, Tensor offsets, float width, float height) -> Tensor");
@@ -658,7 +771,7 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
     });
     m.impl("tensor_aca_rect_backward",
            [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&, const at::Tensor& sc,
-              const at::Tensor& dv, bool need_src, bool need_sd) {
+              const at::Tensor& dv, bool need_src, bool need_sd, int64_t) {
                const int64_t B = t.size(0);
                return std::make_tuple(need_src ? at::empty({B, 3, 4}, t.options())
                                                : at::empty({0}, t.options()),
@@ -684,6 +797,9 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
 
 TORCH_LIBRARY_IMPL(sks_amd, Autograd, m) {
     m.impl("aca", aca_autograd);
+    m.impl("sks", sks_autograd);
+    m.impl("solve", solve_autograd);
     m.impl("tensor_aca_rect", rect_autograd);
+    m.impl("tensor_aca_rect.scalar", rect_scalar_autograd);
     m.impl("tensor_aca_offsets", offsets_autograd);
 }

@@ -274,15 +274,18 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
 
 def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor,
                              scale: Scalar, div: Scalar, need_src: bool = True,
-                             need_scale_div: bool = True):
+                             need_scale_div: bool = True, aten_threads: int = 0):
     """Gradients of tensor_aca_rect: (dL/dsrc (B,3,4) or empty, dL/dtar (B,3,4), dL/dscale,
-    dL/ddiv shaped like scale and div, or empty).  The kernel's per-problem (or per-row)
-    partials are summed over the dimensions scale / div were broadcast along, on the device
-    (deterministically, in float32)."""
+    dL/ddiv shaped like scale and div, or empty).  The kernel's (problem, row) terms are
+    summed over the dimensions scale / div were broadcast along, on the device, in the
+    float32 order ATen-CPU's autograd sums them through the reference's statements
+    (hg_sum_aten_f32): for a batch-uniform scale / div of >= 32768 terms that order depends
+    on ATen's thread count -- this process's (torch.get_num_threads()) unless
+    ``aten_threads`` names another."""
     _gpu_only(tar)
     return _OPS.tensor_aca_rect_backward.default(
         src, tar, grad, _dev_scalar(scale, tar.device), _dev_scalar(div, tar.device),
-        need_src, need_scale_div)
+        need_src, need_scale_div, aten_threads)
 
 
 def tensor_aca_offsets(corner: torch.Tensor, offsets: torch.Tensor, width: float, height: float,

@@ -146,6 +146,13 @@ def test_other_entry_validation(pkg):
     assert lib.hg_sum_rows_f32(None, 0, 5, None, None) == 0                       # nothing to do
     assert lib.hg_sum_rows_f32(None, 2, 5, None, None) == 1                       # NULL x / out
     assert lib.hg_sum_rows_f32(None, 70000, 5, None, None) == 1                   # rows > 65535
+    assert lib.hg_sum_aten_f32(None, 0, 5, 5, 1, 8, 1, None, None) == 0           # no rows
+    assert lib.hg_sum_aten_f32(None, 1, 5, 5, 1, 8, 1, None, None) == 1           # NULL x / out
+    assert lib.hg_sum_aten_f32(None, 1, 5, 5, 1, 0, 1, None, None) == 1           # lanes 0
+    assert lib.hg_sum_aten_f32(None, 1, 5, 5, 1, 17, 1, None, None) == 1          # lanes > 16
+    assert lib.hg_sum_aten_f32(None, 1, 5, 5, 1, 8, 1025, None, None) == 1        # threads
+    assert lib.hg_sum_aten_f32(None, 1, 5, 5, 1, 1, 2, None, None) == 1           # chunked 1 lane
+    assert lib.hg_sum_aten_f32(None, 70000, 5, 5, 1, 8, 1, None, None) == 1       # runs > 65535
     assert lib.hg_sample_solve_f32(None, None, 0, None, None, 5, 0, 1, None) == 1  # npool 0
     assert lib.hg_sample_solve_f32(None, None, 9, None, None, 5, 7, 1, None) == 1  # algo 7
     assert lib.hg_ransac_score_f32(None, -1, None, None, 9, 1.0, None, None) == 1

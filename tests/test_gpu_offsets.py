@@ -5,6 +5,8 @@ import numpy as np
 import pytest
 import torch
 
+from test_gpu_parity import _bits
+
 pytestmark = pytest.mark.gpu
 
 
@@ -135,7 +137,45 @@ def test_native_ops_pass_torch_opcheck(pkg, dev):
                               (q.to(dt), (q + 1.5).to(dt), torch.randn(B, 3, 3, device=dev, dtype=dt),
                                True, True), test_utils=("test_schema", "test_faketensor"))
     torch.library.opcheck(ops.sks.default, (q, q + 1.5, False),
-                          test_utils=("test_schema", "test_faketensor"))
+                          test_utils=("test_schema", "test_faketensor", "test_autograd_registration"))
+    # the host-scalar overload: differentiable in src and tar (scale / div are constants)
+    tar_s = tar.clone().requires_grad_(True)
+    torch.library.opcheck(ops.tensor_aca_rect.scalar, (src, tar_s, 128.0, 1.0), test_utils=tests)
+
+
+def test_autograd_refusals_and_constants(orc, pkg, dev):
+    """Every native op answers inputs that require grad explicitly: sks_amd::sks (no
+    differentiable SKS in the reference) raises naming the missing backward; aca with
+    normalize=True and solve (the C++ API's forms) return H without a graph; the scalar
+    TensorACA overload gives src / tar the tensor overload's gradients bit for bit."""
+    import warnings
+    ops = torch.ops.sks_amd
+    q = (torch.rand(64, 4, 2, device=dev) * 100).requires_grad_(True)
+    t = q.detach() + 1.5
+    with pytest.raises(RuntimeError, match="sks_amd::sks has no backward"):
+        ops.sks.default(q, t, False)
+    with torch.no_grad():
+        assert ops.sks.default(q, t, False).shape == (64, 3, 3)
+    assert ops.sks.default(q.detach(), t, True).grad_fn is None
+    with warnings.catch_warnings():
+        warnings.simplefilter("ignore")
+        H = ops.aca.default(q, t, True)
+        Hs = ops.solve.default(q.view(64, 8), t.view(64, 8), 1, True, 0)
+    assert H.grad_fn is None and not H.requires_grad
+    assert Hs.grad_fn is None and not Hs.requires_grad
+    _bits(orc, H, ops.aca.default(q.detach(), t, True).cpu().numpy(), "aca normalize=True, grad inputs")
+    B = 777
+    torch.manual_seed(1)
+    _, _, sh, th, sc, dv = pkg.adjust(dev, B)
+    th = th + torch.rand_like(th)
+    gH = torch.randn(B, 3, 3, device=dev)
+    t1, t2 = th.clone().requires_grad_(True), th.clone().requires_grad_(True)
+    s1, s2 = sh.clone().requires_grad_(True), sh.clone().requires_grad_(True)
+    ops.tensor_aca_rect.scalar(s1, t1, 128.0, 1.0).backward(gH)
+    ops.tensor_aca_rect.default(s2, t2, torch.tensor([128.0], device=dev),
+                                torch.tensor([1.0], device=dev)).backward(gH)
+    _bits(orc, t1.grad, t2.grad.cpu().numpy(), "scalar overload dL/dtar")
+    _bits(orc, s1.grad, s2.grad.cpu().numpy(), "scalar overload dL/dsrc")
 
 
 def test_fit_offsets_example(pkg, dev):

@@ -434,13 +434,18 @@ def test_rect_backward_kernel_vs_oracle(orc, oracle, pkg, dev):
                                                           gH.cpu().numpy(), scale, div)
             _bits(orc, g_tar, wt, f"grad_tar B={B}")
             _bits(orc, g_src, ws, f"grad_src B={B}")
-            # per-problem partials, via the raw C ABI
-            part = torch.empty(2, B, device=dev)
+            # the (problem, row) terms of dL/dscale, dL/ddiv, via the raw C ABI: (2,B,3)
+            part = torch.empty(2, B, 3, device=dev)
             gt2 = torch.empty(B, 3, 4, device=dev)
             pkg._lib.call("hg_tensor_aca_rect_backward_f32", sh.data_ptr(), th.data_ptr(),
                           gH.data_ptr(), B, s_t.data_ptr(), d_t.data_ptr(), None, gt2.data_ptr(),
                           part.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
-            _bits(orc, part.T, wsd, f"scale/div partials B={B}")
+            *_, gsr, gdr, gss, gds = oracle.tensor_aca_rect_rows_backward(
+                sh.cpu().numpy(), th.cpu().numpy(), gH.cpu().numpy(),
+                np.array([scale], np.float32), np.array([div], np.float32))
+            _bits(orc, part[0], gsr, f"scale terms B={B}")
+            _bits(orc, part[1], gdr, f"div terms B={B}")
+            _bits(orc, np.stack([gss, gds], 1), wsd, f"oracle per-problem sums B={B}")
             _bits(orc, gt2, wt, f"grad_tar (no src) B={B}")
 
 

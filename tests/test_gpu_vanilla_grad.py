@@ -111,13 +111,19 @@ def test_backward_c_abi_misaligned_and_ragged(orc, oracle, pkg, dev):
                       x.data_ptr(), None, None)
 
 
-def test_normalised_form_is_not_differentiable(pkg, dev):
+def test_normalised_form_returns_H_without_a_graph(pkg, dev):
+    """normalize=True (the C++ API's H / H[8], ACA_SKS.cpp:94-98) has no gradient in the
+    reference: with inputs that require grad the op still returns H -- the same bits as
+    without grad -- carrying no graph, and warns once (inference callers need not detach)."""
+    import warnings
     src = torch.rand(8, 4, 2, device=dev, requires_grad=True)
     tar = torch.rand(8, 4, 2, device=dev)
-    with pytest.raises(RuntimeError, match="not differentiable"):
-        torch.ops.sks_amd.aca(src, tar, True)
-    with torch.no_grad():  # inference is fine
-        assert torch.ops.sks_amd.aca(src, tar, True).shape == (8, 3, 3)
+    with warnings.catch_warnings(record=True):
+        warnings.simplefilter("always")
+        H = torch.ops.sks_amd.aca(src, tar, True)
+    assert H.shape == (8, 3, 3) and H.grad_fn is None and not H.requires_grad
+    with torch.no_grad():
+        assert torch.equal(torch.ops.sks_amd.aca(src, tar, True), H)
 
 
 B = 200_003

@@ -503,6 +503,58 @@ def torch_rect_grad() -> str:
                                                    ", ".join(names), refused))
 
 
+RECT_GRAD_LARGE_B = (65536, 1048576)
+RECT_GRAD_LARGE_THREADS = (1, 4, 8, 16)
+RECT_GRAD_LARGE_SEED = 2026
+
+
+def torch_rect_grad_large() -> str:
+    """ATen autograd's batch-uniform scale / div gradients through TensorACA_rect's own
+    statements (Modules_Runtime_Test.py:294-302) on CPU torch at B = 64 K (BASELINE configs[3])
+    and 1 M -- sums of 3B float32 terms whose order depends on at::get_num_threads(), so each
+    is recorded for several thread counts (torch.set_num_threads).  Inputs are regenerated
+    from oracle.rect_grad_batch (fill_uniform counter streams), not stored; dL/dtar is kept
+    as a SHA-256 of its bytes.  A (3,1) per-row scale / div case (column sums, independent of
+    the thread count) rides along.  Writes tests/golden/torch_rect_grad_large.npz."""
+    import hashlib
+    from oracle import Oracle, rect_grad_batch
+    o = Oracle()
+    out = {"B": np.array(RECT_GRAD_LARGE_B), "threads": np.array(RECT_GRAD_LARGE_THREADS),
+           "seed": np.array(RECT_GRAD_LARGE_SEED)}
+    prev = torch.get_num_threads()
+    try:
+        for B in RECT_GRAD_LARGE_B:
+            sh, th, gH = rect_grad_batch(o, B, RECT_GRAD_LARGE_SEED + B)
+            cases = [("uniform", np.array([128.0], np.float32), np.array([1.0], np.float32), RECT_GRAD_LARGE_THREADS),
+                     ("frac", np.array([50.0], np.float32), np.array([1.25], np.float32), RECT_GRAD_LARGE_THREADS),
+                     ("per_row", o.fill_uniform(3, 7, 0, 64.0, 128.0).reshape(3, 1),
+                      o.fill_uniform(3, 7, 3, 0.5, 1.5).reshape(3, 1), (1, 8))]
+            for tag, scale, div, threads in cases:
+                for T in threads:
+                    torch.set_num_threads(T)
+                    tr = torch.from_numpy(th.copy()).requires_grad_(True)
+                    sc = torch.from_numpy(scale.copy()).requires_grad_(True)
+                    dv = torch.from_numpy(div.copy()).requires_grad_(True)
+                    H = run_ref_statements("TensorACA_rect", bs=B, src=torch.from_numpy(sh),
+                                           tar=tr, scale=sc, div=dv)["H"]
+                    H.backward(torch.from_numpy(gH))
+                    key = f"B{B}_{tag}"
+                    out[f"{key}_scale"], out[f"{key}_div"] = scale, div
+                    out[f"{key}_T{T}_gscale"] = sc.grad.numpy().copy()
+                    out[f"{key}_T{T}_gdiv"] = dv.grad.numpy().copy()
+                    out[f"{key}_T{T}_gtar_sha256"] = np.array(
+                        hashlib.sha256(np.ascontiguousarray(tr.grad.numpy()).tobytes()).hexdigest())
+    finally:
+        torch.set_num_threads(prev)
+    np.savez_compressed(os.path.join(OUT, "torch_rect_grad_large.npz"), **out)
+    return ("torch_rect_grad_large.npz: ATen autograd through the reference's TensorACA_rect "
+            "statements on CPU torch %s (ATen CPU capability %s; sum kernel 8 lanes): dL/dscale, "
+            "dL/ddiv (batch-uniform (1,), and (3,1) per row) and SHA-256 of dL/dtar at B = %s, "
+            "for at::get_num_threads() in %s; inputs regenerated by oracle.rect_grad_batch"
+            % (torch.__version__, torch.backends.cpu.get_cpu_capability(),
+               ", ".join(map(str, RECT_GRAD_LARGE_B)), RECT_GRAD_LARGE_THREADS))
+
+
 def torch_vanilla_grad() -> str:
     """The gradients ATen autograd gives through ACA_vanilla's own statements
     (Modules_Runtime_Test.py:322-382) on CPU torch: dL/dsrc, dL/dtar for H.backward(gH).
@@ -579,6 +631,11 @@ if __name__ == "__main__":
         print(line)
     elif sys.argv[1:] == ["--torch-grad"]:  # this fixture alone, appended to the manifest
         line = torch_rect_grad()
+        with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
+            f.write("- " + line + "\n")
+        print(line)
+    elif sys.argv[1:] == ["--torch-grad-large"]:  # this fixture alone, appended to the manifest
+        line = torch_rect_grad_large()
         with open(os.path.join(OUT, "MANIFEST.txt"), "a") as f:
             f.write("- " + line + "\n")
         print(line)
