@@ -460,6 +460,41 @@ def pmc_traffic(kernel_key: str):
         return None
 
 
+_FAMILY_CODE = {}
+
+
+def pmc_detail(key: str, note: str = None) -> dict:
+    """The committed PMC figure (profiles/pmc_traffic.json "detail") for one kernel family,
+    reported beside the section's `frac`: HBM bytes per launch and their ratio to the
+    section's algorithmic bytes, while the library loaded now holds the machine code that
+    was measured (build_lib.kernel_family_digest); otherwise traffic null with the reason.
+    The PMC workload (tools/pmc_run.py) runs each kernel at the bench's own size."""
+    try:
+        with open(PMC_TRAFFIC) as f:
+            rec = json.load(f)["detail"][key]
+    except (OSError, KeyError, ValueError):
+        return {"traffic_bytes": None, "reason": f"no PMC record for {key}"}
+    prefix = rec.get("prefix")
+    if prefix not in _FAMILY_CODE:
+        sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
+        try:
+            import build_lib
+            _FAMILY_CODE[prefix] = build_lib.kernel_family_digest(prefix) if prefix else None
+        except Exception:  # noqa: BLE001 -- unreadable library or no demangler: no match
+            _FAMILY_CODE[prefix] = None
+        finally:
+            sys.path.pop(0)
+    if not rec.get("code") or _FAMILY_CODE[prefix] != rec["code"]:
+        return {"traffic_bytes": None,
+                "reason": "the kernel's machine code changed since the PMC run (tools/gpu_round.sh pmc)"}
+    out = {"traffic_bytes": int(rec["hbm_bytes"]), "pmc_key": key}
+    if rec.get("traffic_over_algorithmic") is not None:
+        out["traffic_over_algorithmic"] = rec["traffic_over_algorithmic"]
+    if note:
+        out["note"] = note
+    return out
+
+
 # Table 5 (imgs/CPU-runtime.png, BASELINE.md): one 4-point set solved 10 M times on one core,
 # MSVC /O2, us per H (main.cpp:87-114)
 TABLE5_US = {"aca": 0.0145, "sks": 0.0252, "aca_f64": 0.0171, "sks_f64": 0.0256}
@@ -695,8 +730,10 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
     """ACA_vanilla as a differentiable loss term (deep homography with general quads):
     forward + backward of the reference's ATen composition (torch_aca_vanilla: the same
     graph, so the same gradient bits) against ours (torch.ops.sks_amd.aca + one
-    hg_aca_backward_f32 launch) at the config-4 batch, eager; and the backward kernel alone
-    at 16 M problems against its 164 B per problem (32 + 32 + 36 in, 32 + 32 out)."""
+    hg_aca_backward_f32 launch) at the config-4 batch -- eager (against autograd's own floor
+    for a one-element op on this host) and 100 steps per HIP graph; the same for
+    TensorACA_rect with tar requiring grad; and the backward kernel alone at 16 M problems
+    against its 164 B per problem (32 + 32 + 36 in, 32 + 32 out)."""
     torch.manual_seed(0)
     src, tar, *_ = pkg.adjust(d.dev, batch)
     tar = (tar + torch.rand_like(tar)).contiguous()
@@ -721,7 +758,46 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
         f_torch()
     _, ms_o = timed_region(d, f_ours, 200)
     _, ms_t = timed_region(d, f_torch, 200)
-    del S, T, src, tar, gH
+    # autograd's own per-step floor on this host: a one-element mul and its .backward()
+    x1 = torch.ones(1, device=d.dev, requires_grad=True)
+    g1 = torch.ones(1, device=d.dev)
+
+    def f_floor():
+        x1.grad = None
+        (x1 * 2.0).backward(g1)
+
+    for _ in range(20):
+        f_floor()
+    _, ms_floor = timed_region(d, f_floor, 200)
+    # 100 fwd + bwd steps (torch.autograd.grad: no .grad accumulation) in one HIP graph
+    ops = torch.ops.sks_amd
+    g_o = graph_of(d, lambda: torch.autograd.grad(ops.aca.default(S, T, False), (S, T), gH), 100)
+    g_t = graph_of(d, lambda: torch.autograd.grad(torch_aca_vanilla(S, T), (S, T), gH), 100)
+    _, ms_go = timed_region(d, g_o.replay, 10)
+    _, ms_gt = timed_region(d, g_t.replay, 3)
+    del g_o, g_t
+    # the same for TensorACA_rect with tar requiring grad (deep-homography training)
+    _, _, sh, th, sc, dv = pkg.adjust(d.dev, batch)
+    Th = th.clone().requires_grad_()
+
+    def r_ours():
+        Th.grad = None
+        pkg.TensorACA_rect(batch, sh, Th, sc, dv).backward(gH)
+
+    def r_torch():
+        Th.grad = None
+        torch_tensor_aca_rect(sh, Th, sc, dv).backward(gH)
+
+    for _ in range(20):
+        r_ours()
+        r_torch()
+    _, ms_ro = timed_region(d, r_ours, 200)
+    _, ms_rt = timed_region(d, r_torch, 200)
+    g_ro = graph_of(d, lambda: torch.autograd.grad(ops.tensor_aca_rect.default(sh, Th, sc, dv), (Th,), gH), 100)
+    g_rt = graph_of(d, lambda: torch.autograd.grad(torch_tensor_aca_rect(sh, Th, sc, dv), (Th,), gH), 100)
+    _, ms_gro = timed_region(d, g_ro.replay, 10)
+    _, ms_grt = timed_region(d, g_rt.replay, 3)
+    del g_ro, g_rt, S, T, src, tar, gH, sh, th, Th
     n = big
     s = torch.rand(n, 8, device=d.dev) * 1024
     t = torch.rand(n, 8, device=d.dev) * 1024
@@ -738,9 +814,18 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
     return {"batch": batch, "fwd_bwd_us_per_call": round(ms_o * 1e3, 2),
             "torch_composed_fwd_bwd_us_per_call": round(ms_t * 1e3, 2),
             "speedup_vs_torch": round(ms_t / ms_o, 2),
+            "autograd_floor_us_per_call": round(ms_floor * 1e3, 2),
+            "above_floor_us_per_call": round((ms_o - ms_floor) * 1e3, 2),
+            "graph_fwd_bwd_us_per_call": round(ms_go * 1e3 / 100, 2),
+            "torch_composed_graph_fwd_bwd_us_per_call": round(ms_gt * 1e3 / 100, 2),
+            "rect_fwd_bwd_us_per_call": round(ms_ro * 1e3, 2),
+            "rect_torch_composed_fwd_bwd_us_per_call": round(ms_rt * 1e3, 2),
+            "rect_graph_fwd_bwd_us_per_call": round(ms_gro * 1e3 / 100, 2),
+            "rect_torch_composed_graph_fwd_bwd_us_per_call": round(ms_grt * 1e3 / 100, 2),
             "gradients_bit_identical_to_torch_composed_on_gpu": same,
             "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
             "backward_large_gbps": round(gbps, 1), "backward_large_frac": round(gbps / HBM_PEAK_GBPS, 4),
+            "backward_large_traffic": pmc_detail("aca_vanilla_backward"),
             "backward_bytes_per_problem": 164}
 
 
@@ -815,7 +900,10 @@ def reference_layout(d: Dist, pkg):
             bpp = 200
             rec = {"us_per_launch": round(ms * 1e3, 2), "launches": loops,
                    "achieved_gbps": round(n * bpp / (ms * 1e-3) / 1e9, 1),
+                   "frac": round(n * bpp / (ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                    "G_homographies_per_s": round(n / (ms * 1e-3) / 1e9, 2)}
+            if n == 10_000_000:
+                rec["traffic"] = pmc_detail(f"{algo}_f64_soa")
             if n == 1_000_000:
                 rec["table8_us"] = TABLE8_US[algo]
                 rec["speedup_vs_table8"] = round(TABLE8_US[algo] / (ms * 1e3), 2)
@@ -867,6 +955,7 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
                      "gbps_written": round(4 * n * 4 / (ms_draw * 1e-3) / 1e9, 1),
                      "write_only_stream_us": round(ms_wsmall * 1e3, 2),
                      "frac_of_write_only_stream": round(ms_wsmall / ms_draw, 4),
+                     "traffic": pmc_detail("mrg_words", "PMC at 40 M words (10 x this launch)"),
                      "rocrand_generate_us": round(ms_roc * 1e3, 1),
                      "speedup_vs_rocrand": round(ms_roc / ms_draw, 1),
                      "bit_identical_to_rocrand": bool(torch.equal(words, ref_words))}}
@@ -940,6 +1029,7 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
             "G_hyp_per_s": round(big / (ms_one * 1e-3) / 1e9, 2),
             "gbps_H": round(big * 72 / (ms_one * 1e-3) / 1e9, 1),
             "frac": round(big * 72 / (ms_one * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_detail(f"rand_gather_solve_f64_{algo}"),
             "write_only_stream_gbps": round(big * 72 / (ms_write * 1e-3) / 1e9, 1),
             "frac_of_write_only_stream": round(ms_write / ms_one, 4),
             "draws_then_gather_solve_us": round(ms_two * 1e3, 2)}
@@ -1129,12 +1219,14 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
         "sample_solve_large": {"hypotheses": big, "us": round(ms_big * 1e3, 2),
                                "G_hyp_per_s": round(big / (ms_big * 1e-3) / 1e9, 2),
                                "achieved_gbps": round(big * 52 / (ms_big * 1e-3) / 1e9, 1),
-                               "frac": round(big * 52 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
+                               "frac": round(big * 52 / (ms_big * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                               "traffic": pmc_detail("sample_solve_indexed")},
         "sample_solve_seeded_large": {
             "hypotheses": big, "us": round(ms_seed * 1e3, 2),
             "G_hyp_per_s": round(big / (ms_seed * 1e-3) / 1e9, 2),
             "achieved_gbps": round(big * 36 / (ms_seed * 1e-3) / 1e9, 1),
             "frac": round(big * 36 / (ms_seed * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+            "traffic": pmc_detail("sample_solve_seeded"),
             "write_only_stream_gbps": round(big * 36 / (ms_write * 1e-3) / 1e9, 1),
             "frac_of_write_only_stream": round(ms_write / ms_seed, 4),
             "draws_then_indexed_us": round(ms_two * 1e3, 2),
@@ -1393,7 +1485,7 @@ def main():
                 "achieved_gbps": round(n * bpp / (ms_s * 1e-3) / 1e9, 1),
                 "frac": round(n * bpp / (ms_s * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "sks_over_aca_time": round(ms_s / ms_aca, 3),
-                "traffic": pmc_traffic("sks_f32_aos_norm") if n == 10_000_000 else None,
+                "traffic": pmc_detail("sks_f32_aos_norm") if n == 10_000_000 else None,
             }
             # the reference's RHO-GE comparison baseline on the same inputs
             for _ in range(args.warmup):
@@ -1449,6 +1541,25 @@ def main():
                 f_pp()
             _, ms_pp = timed_region(d, f_pp, 50)
             del psc, pdv
+            gHb = torch.randn(big, 3, 3, device=d.dev)
+            f_bt = lambda: pkg.tensor_aca_rect_backward(bs_h, bt_h, gHb, bsc, bdv, False, False)  # noqa
+            f_ba = lambda: pkg.tensor_aca_rect_backward(bs_h, bt_h, gHb, bsc, bdv, True, True)  # noqa
+            for _ in range(5):
+                f_bt()
+                f_ba()
+            _, ms_bt = timed_region(d, f_bt, 20)
+            _, ms_ba = timed_region(d, f_ba, 20)
+            del gHb
+            rect_backward_large = {
+                "large_backward_tar_us": round(ms_bt * 1e3, 2),
+                "large_backward_tar_frac": round(big * 140 / (ms_bt * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_tar_traffic": pmc_detail("rect_backward_tar"),
+                "large_backward_all_us": round(ms_ba * 1e3, 2),
+                "large_backward_all_frac": round(big * 212 / (ms_ba * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_all_traffic": pmc_detail(
+                    "rect_backward_all", "the backward kernel alone; the scale / div sum "
+                    "(hg_sum_aten_f32) is in large_backward_all_us"),
+            }
             # compact form (corner + 4 offsets) on the same big batch
             corner = bs_h[:, 0:2, 0].contiguous()
             offs = (bt_h[:, 0:2, :] - bs_h[:, 0:2, :]).transpose(1, 2).contiguous()
@@ -1492,6 +1603,7 @@ def main():
                 "large_batch": big, "large_us_per_call": round(ms_ob * 1e3, 2),
                 "large_achieved_gbps": round(big * 76 / (ms_ob * 1e-3) / 1e9, 1),
                 "large_frac": round(big * 76 / (ms_ob * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_traffic": pmc_detail("tensor_aca_offsets"),
                 "bytes_per_problem": 76,
             }
             line["tensor_aca_rect"] = {
@@ -1504,6 +1616,7 @@ def main():
                 "large_batch": big, "large_us_per_call": round(ms_b * 1e3, 2),
                 "large_achieved_gbps": round(big * rb / (ms_b * 1e-3) / 1e9, 1),
                 "large_frac": round(big * rb / (ms_b * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_traffic": pmc_detail("tensor_aca_rect"),
                 # the (B,3,4) contract's floor: the 2 src floats used sit 16 B apart in every
                 # 48-B record, so every 32-B sector of src is fetched (PMC: 1.0x of this count)
                 "layout_min_bytes_per_problem": RECT_LAYOUT_MIN_BYTES,
@@ -1513,6 +1626,10 @@ def main():
                 "large_per_problem_scale_div_us_per_call": round(ms_pp * 1e3, 2),
                 "large_per_problem_layout_min_frac": round(
                     big * (RECT_LAYOUT_MIN_BYTES + 8) / (ms_pp * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_per_problem_traffic": pmc_detail("tensor_aca_rect_bcast"),
+                # the backward at 16 M: dL/dtar alone (140 B per problem) and everything
+                # (dL/dsrc, dL/dtar, the (1,) scale / div through hg_sum_aten_f32: 212 B)
+                **rect_backward_large,
             }
             del bs_h, bt_h, Hb
             line["aca_vanilla_autograd"] = vanilla_autograd_section(d, pkg, args.rect_batch)
@@ -1531,7 +1648,10 @@ def main():
             _, ms64 = timed_region(d, f64, 50)
             line["aca_f64_aos"] = {"us_per_launch": round(ms64 * 1e3, 2),
                                    "G_homographies_per_s": round(n / (ms64 * 1e-3) / 1e9, 2),
-                                   "achieved_gbps": round(n * 200 / (ms64 * 1e-3) / 1e9, 1)}
+                                   "achieved_gbps": round(n * 200 / (ms64 * 1e-3) / 1e9, 1),
+                                   "frac": round(n * 200 / (ms64 * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                                   "traffic": pmc_detail("aca_f64_aos_norm") if n == 10_000_000
+                                   else {"traffic_bytes": None, "reason": "PMC measured at 10 M"}}
             del s64, t64, H64
             if not args.no_host_shard:
                 run("aca")()  # H = this rank's device result again (the f64 step used other buffers)

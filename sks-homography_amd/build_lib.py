@@ -115,6 +115,72 @@ def kernel_code_digest(lib_path: str = None) -> dict:
     return found
 
 
+def device_code_digests(lib_path: str = None) -> dict:
+    """{mangled kernel name: sha256 (16 hex digits) of its gfx950 machine code} for every
+    function symbol in the library's gfx950 code objects (kernel_code_digest's walk, all
+    symbols whose address lies in .text)."""
+    import hashlib
+    import struct
+    b = open(lib_path or LIB, "rb").read()
+    _, fat_off, fat_size = _elf_sections(b)[".hip_fatbin"]
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    found = {}
+    pos = b.find(magic, fat_off, fat_off + fat_size)
+    while pos >= 0:
+        count = struct.unpack_from("<Q", b, pos + 24)[0]
+        q = pos + 32
+        for _ in range(count):
+            off, size, idlen = struct.unpack_from("<QQQ", b, q)
+            ident = b[q + 24:q + 24 + idlen].decode()
+            q += 24 + idlen
+            if ARCH not in ident or size == 0:
+                continue
+            co = pos + off
+            secs = _elf_sections(b, co)
+            _, sym_off, sym_size = secs[".symtab"]
+            str_off = secs[".strtab"][1]
+            text_addr, text_off, text_size = secs[".text"]
+            for k in range(sym_size // 24):
+                st_name, _info, _other, _shndx, value, sz = struct.unpack_from("<IBBHQQ", b, sym_off + 24 * k)
+                if not sz or not (text_addr <= value < text_addr + text_size):
+                    continue
+                name = b[str_off + st_name:b.index(b"\0", str_off + st_name)].decode()
+                start = text_off + (value - text_addr)
+                found[name] = hashlib.sha256(b[start:start + sz]).hexdigest()[:16]
+        pos = b.find(magic, pos + 24, fat_off + fat_size)
+    return found
+
+
+def demangle(names) -> dict:
+    """{mangled: demangled} through binutils' c++filt (on this image and the GPU box)."""
+    names = list(names)
+    tool = shutil.which("c++filt") or shutil.which("llvm-cxxfilt") or "/usr/bin/c++filt"
+    out = subprocess.run([tool], input="\n".join(names), capture_output=True, text=True,
+                         check=True).stdout.splitlines()
+    return dict(zip(names, out))
+
+
+def kernel_family_digest(prefix: str, lib_path: str = None) -> str:
+    """One digest over the machine code of every kernel whose demangled name contains
+    `prefix` (the PMC reducer's match): a changed kernel changes it."""
+    import hashlib
+    codes = device_code_digests(lib_path)
+    names = demangle(codes)
+    hit = sorted(codes[m] for m, d in names.items() if prefix in d)
+    return hashlib.sha256(",".join(hit).encode()).hexdigest()[:16] if hit else ""
+
+
+def compiler_id() -> str:
+    """The first line of `hipcc --version` (the machine code depends on it, not only on the
+    source): recorded beside every machine-code digest."""
+    try:
+        out = subprocess.run([hipcc(), "--version"], capture_output=True, text=True, timeout=60)
+        lines = (out.stdout or out.stderr).strip().splitlines()
+        return "; ".join([lines[0]] + [x.strip() for x in lines if "clang version" in x][:1])
+    except Exception as e:  # noqa: BLE001
+        return f"unknown ({type(e).__name__})"
+
+
 def hipcc() -> str:
     for cand in (shutil.which("hipcc"), "/opt/rocm/bin/hipcc"):
         if cand and os.path.exists(cand):

@@ -537,7 +537,7 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
     const bool ws = grad_src != nullptr, wd = grad_scale_div != nullptr;
     using hg::aligned16;
     if (aligned16(src) && aligned16(tar) && aligned16(grad_H) && aligned16(grad_tar) &&
-        (!ws || aligned16(grad_src))) {
+        (!ws || aligned16(grad_src)) && (!wd || aligned16(grad_scale_div))) {
         // staged form (tools/kbench_bwd.py); cache policy by size as the forward
         const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
         const bool nt = B * 232 > hg::kMallResidentBytes;
@@ -747,10 +747,12 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
     const hg::AtenSum a{x, row_stride, elem_stride, m, chunks > 1 ? hg::ceil_div(m, chunks) : m,
                         (int)chunks, lanes};
     const hg::AtenRun r0(a, 0);  // the longest run sizes the grids
+    if (r0.step > hg::kAtenMaxStep) return hg::kErrInvalid;  // runs beyond 2^24 rows per stream
     if (r0.nb > 0) {
-        const int64_t bx = hg::ceil_div((r0.g1 + 1) * r0.S, (int64_t)256);
+        const int64_t bx = r0.g1 + 1;  // one block per super-block (the last may be partial)
         if (bx > 0x7fffffffLL) return hg::kErrInvalid;
-        const int rc = hg::launch(hg::aten_sum_l1, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
+        const int rc = hg::launch(hg::aten_sum_l1, dim3((unsigned)bx, (unsigned)runs),
+                                  hg::kAtenL1Threads, 0, s, a);
         if (rc) return rc;
     }
     if (r0.g1 > 0) {

@@ -89,6 +89,19 @@ __device__ __forceinline__ void store_sd_terms(float* __restrict__ gsd, int64_t 
     }
 }
 
+// A wave's 64 rows of 3 floats (lane l's v) as ONE contiguous 768-B run at `out` (16-B
+// aligned): ds_write_b32 at an odd dword stride (conflict-free), then lanes 0..47 store 16 B.
+template <bool NT>
+__device__ __forceinline__ void store_terms3_staged(char* __restrict__ out, const float (&v)[3],
+                                                    char* lds, int lane) {
+    float* st = reinterpret_cast<float*>(lds);
+#pragma unroll
+    for (int r = 0; r < 3; ++r) st[lane * 3 + r] = v[r];
+    wave_lds_sync();
+    if (lane < 48) st16<NT>(out + 16 * lane, *reinterpret_cast<const u32x4*>(lds + 16 * lane));
+    wave_lds_sync();
+}
+
 template <bool WANT_SRC, bool WANT_SD>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
@@ -367,7 +380,19 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
             for (int k = 0; k < 12; ++k) gs[k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
             store_rows_staged<12, NT>(reinterpret_cast<char*>(gsrc + base * 12), gs, lds, lane);
         }
-        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
+        if constexpr (WANT_SD) {
+            // the wave's 64 x 3 terms of each parameter are one contiguous 768-B run:
+            // staged, then 48 lanes store 16 B each (the second run is 16-B aligned when 3B
+            // is a multiple of 4)
+            store_terms3_staged<NT>(reinterpret_cast<char*>(gsd + 3 * base), gsr, lds, lane);
+            if (((3 * B) & 3) == 0) {
+                store_terms3_staged<NT>(reinterpret_cast<char*>(gsd + 3 * B + 3 * base), gdr, lds,
+                                        lane);
+            } else {
+#pragma unroll
+                for (int r = 0; r < 3; ++r) gsd[3 * B + 3 * p + r] = gdr[r];
+            }
+        }
         return;
     }
     if (p < B) {

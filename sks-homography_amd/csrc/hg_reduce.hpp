@@ -15,8 +15,9 @@
 //     those flushed every step super-blocks, the last level never; then the leftover vectors
 //     join column 0, the columns fold into column 0, and the scalar tail and the W lanes add
 //     into a 0-initialised float; the stored value is 0 + that.
-// On the device the cascade's levels become launches: L1 sums each super-block of each stream
-// (one thread each), L2 each group of `step` super-block sums, L3 one block per run finishes
+// On the device the cascade's levels become launches: L1 sums each super-block of every stream
+// (one block per super-block, one thread per block of a stream), L2 each group of `step`
+// super-block sums, L3 one block per run finishes
 // the streams and folds them (thread 0), L4 sums the chunk buffer.  Partial results are
 // written in place over elements their own thread has finished reading: x is scratch.
 #pragma once
@@ -89,30 +90,40 @@ struct AtenRun {
     __device__ __forceinline__ float* flat(int64_t e) const { return base + e * es; }
 };
 
-// L1: thread (g, s) sums super-block g of stream s -- each of its blocks from 0, the block
-// sums from 0 -- and writes the sum over the super-block's row 0; g == g1 is the partial
-// super-block's r1 blocks (acc1 when the cascade stops), written over its row 0 too.
-__global__ __launch_bounds__(256) void aten_sum_l1(AtenSum a) {
+// L1: block (g, run) sums super-block g of every stream of the run: thread task (b, s) --
+// block b of stream s, `step` rows from 0, all loads issued together -- lands in LDS, then
+// thread s adds the super-block's block sums from 0 and writes the sum over the super-block's
+// row 0; g == g1 is the partial super-block's r1 blocks (acc1 when the cascade stops),
+// written over its row 0 too.  A wave's load touches 128-B runs (32 streams x 4 B).
+constexpr int kAtenL1Threads = 256;
+constexpr int kAtenMaxStep = 64;  // lp <= 6: runs up to 2^27 rows of each stream
+
+__global__ __launch_bounds__(kAtenL1Threads) void aten_sum_l1(AtenSum a) {
+    __shared__ float bs[kAtenMaxStep * 4 * kAtenMaxLanes];
     const AtenRun R(a, blockIdx.y);
-    const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-    const int s = (int)(idx % R.S);
-    const int64_t g = idx / R.S;
-    if (g > R.g1 || (g == R.g1 && R.r1 == 0)) return;
-    const int64_t blocks = g < R.g1 ? R.step : R.r1;
+    const int64_t g = blockIdx.x;
+    if (g > R.g1 || (g == R.g1 && R.r1 == 0)) return;  // block-uniform
+    const int blocks = (int)(g < R.g1 ? R.step : R.r1);
     const int64_t i0 = g * R.step * R.step;
-    float acc1 = 0.f;
-    for (int64_t b = 0; b < blocks; ++b) {
+    const int step = (int)R.step;
+    for (int task = threadIdx.x; task < blocks * R.S; task += kAtenL1Threads) {
+        const int b = task / R.S, s = task - b * R.S;
+        const int64_t ib = i0 + (int64_t)b * step;
         float acc0 = 0.f;
-        const int64_t ib = i0 + b * R.step;
-        for (int64_t j = 0; j < R.step; j += 16) {  // step is a multiple of 16
+        for (int j = 0; j < step; j += 16) {  // step is a multiple of 16
             float v[16];
 #pragma unroll
             for (int u = 0; u < 16; ++u) v[u] = *R.at(ib + j + u, s);
 #pragma unroll
             for (int u = 0; u < 16; ++u) acc0 = acc0 + v[u];
         }
-        acc1 = acc1 + acc0;
+        bs[b * R.S + s] = acc0;
     }
+    __syncthreads();
+    if (threadIdx.x >= R.S) return;
+    const int s = threadIdx.x;
+    float acc1 = 0.f;
+    for (int b = 0; b < blocks; ++b) acc1 = acc1 + bs[b * R.S + s];
     *R.at(i0, s) = acc1;
 }
 

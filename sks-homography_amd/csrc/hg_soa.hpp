@@ -193,6 +193,94 @@ __global__ __launch_bounds__(kBlock) void solve_soa_narrow(const T* __restrict__
     }
 }
 
+// Block-contiguous row segments: a block of WAVES waves owns a tile of
+// SEG bytes of EVERY component row (SEG / sizeof(T) consecutive problems).  The tile's 16
+// input-row segments land in LDS by LDS-DMA -- the waves share the 1-KiB pieces -- behind
+// one wait and one barrier; each thread then solves SEG / sizeof(T) / (64 WAVES) problems
+// (problem j = thread + k * 64 WAVES) reading its components from LDS, and every H row
+// segment leaves as SEG contiguous bytes (lane-consecutive stores).  So each row is touched
+// in SEG-byte runs instead of the narrow kernel's 512-B wave accesses.  XCD: the blocks one
+// XCD runs (the hardware deals block b to XCD b % 8) take one contiguous range of tiles.
+// NOSOLVE: the same traffic with H = a copy of the inputs (the pattern's own ceiling).
+// One tile per block; 16-B aligned bases; the ragged last tile goes per thread.
+template <int ALGO, bool NORM, typename T, int SEG, int WAVES, bool XCD, bool NOSOLVE,
+          bool NT = true>
+__global__ __launch_bounds__(64 * WAVES) void solve_soa_seg(const T* __restrict__ src,
+                                                            const T* __restrict__ tar,
+                                                            T* __restrict__ H, int64_t n) {
+    constexpr int kThreads = kWave * WAVES;
+    constexpr int kTile = SEG / (int)sizeof(T);
+    constexpr int kPer = kTile / kThreads;
+    constexpr int kPieces = SEG / (16 * kWave);
+    static_assert(kTile % kThreads == 0 && SEG % (16 * kWave) == 0, "whole pieces, whole problems");
+    __shared__ __attribute__((aligned(16))) char lds[16 * SEG];
+    int64_t b = blockIdx.x;
+    if constexpr (XCD) {
+        const uint32_t G = gridDim.x, per = G / 8, rem = G % 8;
+        const uint32_t x = blockIdx.x % 8, k = blockIdx.x / 8;
+        b = (int64_t)(x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + k;
+    }
+    const int64_t base = b * kTile;
+    if (base >= n) return;
+    if (base + kTile > n) {  // the ragged last tile: per thread, straight from HBM
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+            const int64_t p = base + threadIdx.x + k * kThreads;
+            if (p >= n) continue;
+            T s[8], t[8], h[9];
+#pragma unroll
+            for (int r = 0; r < 8; ++r) {
+                s[r] = src[(int64_t)r * n + p];
+                t[r] = tar[(int64_t)r * n + p];
+            }
+            if constexpr (NOSOLVE) {
+#pragma unroll
+                for (int r = 0; r < 8; ++r) h[r] = s[r] + t[r];
+                h[8] = t[0];
+            } else {
+                solve<ALGO, NORM>(s, t, h);
+            }
+#pragma unroll
+            for (int r = 0; r < 9; ++r) H[(int64_t)r * n + p] = h[r];
+        }
+        return;
+    }
+    const int lane = threadIdx.x & (kWave - 1), wave = threadIdx.x / kWave;
+#pragma unroll
+    for (int p = wave; p < 16 * kPieces; p += WAVES) {
+        const int r = p / kPieces, c = p % kPieces;
+        const T* row = (r < 8 ? src + (int64_t)r * n : tar + (int64_t)(r - 8) * n) + base;
+        __builtin_amdgcn_global_load_lds(
+            (gbl_ptr_t)(reinterpret_cast<const char*>(row) + 16 * (c * kWave + lane)),
+            (lds_ptr_t)(lds + r * SEG + 16 * c * kWave), 16, 0, NT ? 2 : 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+        const int j = threadIdx.x + k * kThreads;
+        T s[8], t[8], h[9];
+#pragma unroll
+        for (int r = 0; r < 8; ++r) {
+            s[r] = reinterpret_cast<const T*>(lds + r * SEG)[j];
+            t[r] = reinterpret_cast<const T*>(lds + (8 + r) * SEG)[j];
+        }
+        if constexpr (NOSOLVE) {
+#pragma unroll
+            for (int r = 0; r < 8; ++r) h[r] = s[r] + t[r];
+            h[8] = t[0];
+        } else {
+            solve<ALGO, NORM>(s, t, h);
+        }
+#pragma unroll
+        for (int r = 0; r < 9; ++r) {
+            T* dst = H + (int64_t)r * n + base + j;
+            if constexpr (NT) __builtin_nontemporal_store(h[r], dst);
+            else *dst = h[r];
+        }
+    }
+}
+
 template <int G, bool PERSIST>
 inline int64_t soa_grid(int64_t groups, int per_cu = 8) {
     const int64_t chunks = (groups + (int64_t)kBlock * G - 1) / ((int64_t)kBlock * G);

@@ -370,9 +370,9 @@ std::tuple<at::Tensor, at::Tensor> aca_backward(const at::Tensor& src_, const at
                     grad_.scalar_type() == dt,
                 "sks_amd::aca_backward: src/tar/grad must all be float32 or all float64");
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous(), grad = grad_.contiguous();
-    at::Tensor none = at::empty({0}, tar.options());
-    at::Tensor g_src = need_src ? at::empty(src_.sizes(), src.options()) : none;
-    at::Tensor g_tar = need_tar ? at::empty(tar_.sizes(), tar.options()) : none;
+    // (0,) placeholders only where a gradient is not wanted (one allocation less per step)
+    at::Tensor g_src = at::empty(need_src ? src_.sizes() : at::IntArrayRef{0}, src.options());
+    at::Tensor g_tar = at::empty(need_tar ? tar_.sizes() : at::IntArrayRef{0}, tar.options());
     if (B == 0 || (!need_src && !need_tar)) return {g_src, g_tar};
     const c10::DeviceGuard guard(dev);
     if (dt == at::kDouble) {

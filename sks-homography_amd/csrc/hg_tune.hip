@@ -173,6 +173,19 @@ int launch_soa_narrow(int algo, const void* s, const void* t, void* H, int64_t n
     return (int)hipGetLastError();
 }
 
+template <typename T, int SEG, int WAVES, bool XCD, bool NOSOLVE>
+int launch_soa_seg(int algo, const void* s, const void* t, void* H, int64_t n, int,
+                   hipStream_t st) {
+    constexpr int64_t kTile = SEG / (int)sizeof(T);
+    const unsigned g = (unsigned)((n + kTile - 1) / kTile);
+    const T* a = (const T*)s;
+    const T* b = (const T*)t;
+    T* h = (T*)H;
+    if (algo == 0) solve_soa_seg<kACA, false, T, SEG, WAVES, XCD, NOSOLVE><<<g, 64 * WAVES, 0, st>>>(a, b, h, n);
+    else solve_soa_seg<kSKS, false, T, SEG, WAVES, XCD, NOSOLVE><<<g, 64 * WAVES, 0, st>>>(a, b, h, n);
+    return (int)hipGetLastError();
+}
+
 struct SoaVariant {
     const char* name;
     int (*launch)(int, const void*, const void*, void*, int64_t, int, hipStream_t);
@@ -195,6 +208,25 @@ const SoaVariant kSoaVariants[] = {
     {"f64 narrow W8 (1 problem per lane)", launch_soa_narrow<double, 8>},
     {"f64 narrow W8 plain (cached) ld/st", launch_soa_narrow<double, 8, false>},
     {"f32 narrow W4 plain (cached) ld/st", launch_soa_narrow<float, 4, false>},
+    // block-contiguous row segments (solve_soa_seg): SEG bytes of every row per block
+    {"f64 seg 2K w1", launch_soa_seg<double, 2048, 1, false, false>},
+    {"f64 seg 2K w2", launch_soa_seg<double, 2048, 2, false, false>},
+    {"f64 seg 4K w1", launch_soa_seg<double, 4096, 1, false, false>},
+    {"f64 seg 4K w2", launch_soa_seg<double, 4096, 2, false, false>},
+    {"f64 seg 4K w4", launch_soa_seg<double, 4096, 4, false, false>},
+    {"f64 seg 8K w2", launch_soa_seg<double, 8192, 2, false, false>},
+    {"f64 seg 8K w4", launch_soa_seg<double, 8192, 4, false, false>},
+    {"f64 seg 2K w1 xcd", launch_soa_seg<double, 2048, 1, true, false>},
+    {"f64 seg 4K w2 xcd", launch_soa_seg<double, 4096, 2, true, false>},
+    {"f64 seg 4K w4 xcd", launch_soa_seg<double, 4096, 4, true, false>},
+    {"f64 seg 8K w4 xcd", launch_soa_seg<double, 8192, 4, true, false>},
+    {"f64 seg 2K w1 nosolve", launch_soa_seg<double, 2048, 1, false, true>},
+    {"f64 seg 4K w2 nosolve", launch_soa_seg<double, 4096, 2, false, true>},
+    {"f64 seg 4K w4 nosolve", launch_soa_seg<double, 4096, 4, false, true>},
+    {"f64 seg 8K w4 nosolve", launch_soa_seg<double, 8192, 4, false, true>},
+    {"f64 seg 4K w4 xcd nosolve", launch_soa_seg<double, 4096, 4, true, true>},
+    {"f32 seg 4K w2", launch_soa_seg<float, 4096, 2, false, false>},
+    {"f32 seg 4K w4 xcd", launch_soa_seg<float, 4096, 4, true, false>},
 };
 
 // The HBM ceilings either side of a copy: read-only (every 16-B load folded into a

@@ -57,6 +57,12 @@ for step in $STEPS; do
         rect_tests) run pytest_rect 600 python -u -m pytest tests/test_gpu_rect_grad.py tests/test_gpu_rect_bcast.py \
                 tests/test_gpu_rect_aten_bits.py tests/test_gpu_offsets.py tests/test_gpu_parity.py -m gpu -v -s \
                 -k "rect or offsets or grad" -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        autograd_cost) run autograd_cost 300 python -u tools/autograd_cost.py ;;
+        prof_rect_bwd) run prof_rect_bwd 300 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/prof_rect_bwd_$TAG" -o run -- python3 tools/prof_rect_bwd.py ;;
+        aten_tests) run pytest_aten 600 python -u -m pytest tests/test_gpu_aten_sum.py tests/test_gpu_rect_grad.py \
+                tests/test_gpu_rect_bcast.py tests/test_gpu_offsets.py tests/test_gpu_vanilla_grad.py -m gpu -v \
+                -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         bench) run bench 600 python bench.py ;;
         prof)

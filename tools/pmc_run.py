@@ -36,19 +36,47 @@ def main():
     for algo in ("aca", "sks"):
         for _ in range(REPS):
             pkg.solve(algo, s64, t64, normalize=False, layout="soa", out=H64)
-    del s64, t64, H64, src, tar, H
+    del s64, t64, H64
+    # binary64 AoS, normalised (sks::runKernel_ACA_double semantics; bench aca_f64_aos)
+    sd, td = src.double(), tar.double()
+    Hd = torch.empty((n, 9), dtype=torch.float64, device=dev)
+    for _ in range(REPS):
+        pkg.solve("aca", sd, td, normalize=True, out=Hd)
+    del sd, td, Hd, src, tar, H
     big = 16 * 1024 * 1024
+    # ACA_vanilla's backward alone at 16 M (bench aca_vanilla_autograd.backward_large)
+    vs = torch.rand(big, 8, device=dev) * 1024
+    vt = torch.rand(big, 8, device=dev) * 1024
+    vg = torch.randn(big, 9, device=dev)
+    for _ in range(REPS):
+        pkg.aca_backward(vs, vt, vg)
+    del vs, vt, vg
     torch.manual_seed(0)
     _, _, bs, bt, sc, dv = pkg.adjust(dev, big)
     Hb = torch.empty((big, 3, 3), device=dev)
     for _ in range(REPS):
         pkg.ops.tensor_aca_rect(bs, bt, sc, dv, out=Hb)
+    # per-problem (B,1,1) scale / div: the staged broadcast kernel
+    psc = torch.full((big, 1, 1), 128.0, device=dev) + torch.rand(big, 1, 1, device=dev)
+    pdv = torch.ones((big, 1, 1), device=dev)
+    for _ in range(REPS):
+        pkg.ops.tensor_aca_rect(bs, bt, psc, pdv, out=Hb)
+    del psc, pdv
+    # the rect backward: dL/dtar alone (deep-homography training), then everything (src,
+    # tar, and the batch-uniform scale / div through hg_sum_aten_f32)
+    gHb = torch.randn(big, 3, 3, device=dev)
+    for _ in range(REPS):
+        pkg.tensor_aca_rect_backward(bs, bt, gHb, sc, dv, False, False)
+    for _ in range(REPS):
+        pkg.tensor_aca_rect_backward(bs, bt, gHb, sc, dv, True, True, aten_threads=16)
     corner = bs[:, 0:2, 0].contiguous()
     offs = (bt[:, 0:2, :] - bs[:, 0:2, :]).transpose(1, 2).contiguous()
     del bs, bt
     for _ in range(REPS):
         pkg.ops.tensor_aca_offsets(corner, offs, 128.0, 128.0, out=Hb)
-    del corner, offs, Hb
+    for _ in range(REPS):
+        pkg.tensor_aca_offsets_backward(corner, offs, gHb, 128.0, 128.0, False)
+    del corner, offs, Hb, gHb
     g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
     ps = torch.from_numpy(g["pool_src"]).to(dev)
     pt = torch.from_numpy(g["pool_tar"]).to(dev)
@@ -56,6 +84,8 @@ def main():
     for _ in range(REPS):
         pkg.sample_solve(ps, pt, idx)
     del idx
+    for _ in range(REPS):
+        pkg.sample_solve_seeded(ps, pt, big, 11, 0)
     # the fused binary64 gather + cal_Homo_ACA in the reference's formats (hg_gather.hpp),
     # 10 M hypotheses on the wall file: 16 B of words in, 72 B of H out per hypothesis
     rl = pkg.rand_mrg32k3a(4 * n, 11, dev).view(4, n)
@@ -67,8 +97,9 @@ def main():
     for _ in range(REPS):
         pkg.rand_mrg32k3a(4 * n, 11, dev)
     del rl
-    for _ in range(REPS):
-        pkg.rand_gather_solve(ps64, pt64, n, 11, "aca")
+    for algo in ("aca", "sks"):
+        for _ in range(REPS):
+            pkg.rand_gather_solve(ps64, pt64, n, 11, algo)
     torch.cuda.synchronize()
     print("pmc workload done")
 
