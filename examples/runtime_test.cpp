@@ -126,7 +126,10 @@ int main(int argc, char** argv) {
             std::printf("%s N=%-8lld %10.3f us per launch  %8.2f G H/s\n", c.name, (long long)n,
                         us, n / us * 1e-3);
         }
-        // ACA (unnormalised) against GE (H[8] = 1) after normalising: same homography
+        // ACA (unnormalised) against GE (H[8] = 1) after normalising: same homography.  The
+        // C ABI is asynchronous (hg_rand_mrg32k3a_u32 included, since round 3): wait for the
+        // stream before any host-side read
+        CHECK(hipStreamSynchronize(nullptr));
         std::vector<double> ha(9 * n), hg(9 * n);
         CHECK(hipMemcpy(ha.data(), dh, 9 * n * sizeof(double), hipMemcpyDeviceToHost));
         CHECK(hipMemcpy(hg.data(), dg, 9 * n * sizeof(double), hipMemcpyDeviceToHost));

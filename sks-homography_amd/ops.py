@@ -260,6 +260,13 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     per row, (B,3,1); taken as float32 on tar's device.  Returns (B,3,3).
     Runs torch.ops.sks_amd.tensor_aca_rect (native, csrc/hg_torch_ops.cpp); with tensor
     scale/div and no ``out`` it is differentiable in all four inputs.
+
+    Which bits: the reference's statements as ATen-CPU evaluates them (FMA-contracted cross,
+    the three cross terms summed ((c0 + c1) + c2) + 0), bit for bit.  The same statements on
+    a ROCm GPU sum the terms as (c0 + c2) + c1 (profiles/r03/rocm_sum_probe.json), so against
+    the reference's device='cuda' run H agrees to ~1e-5 relative on fractional inputs (exactly
+    on the reference's integer batches) -- the spread the reference itself shows between its
+    CPU and GPU runs (tests/test_gpu_parity.py::test_rect_close_to_torch_composed_on_gpu).
     """
     _gpu_only(tar)  # the op checks that src (and out) share tar's device
     if isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):

@@ -139,8 +139,11 @@ _ALGO_IDS = {"aca": 0, "sks": 1, "ge": 2, "gpt": 3}
 
 def rand_mrg32k3a(count: int, seed: int = 11, device="cuda") -> torch.Tensor:
     """``count`` MRG32K3A words, as curandGenerate fills the reference's index list
-    (.cu:1443-1446, seed 11): the hand-written generator, rocRAND's host-API words;
-    uint32 values in an int32 tensor."""
+    (.cu:1443-1446, seed 11): the hand-written generator, uint32 values in an int32 tensor.
+    The words equal rocRAND's host-API MRG32K3A words on gfx950 bit for bit (their order is
+    rocRAND's gfx950 launch layout, hg_mrg32k3a.hpp kOrderLog2); equality with cuRAND's
+    words, which the reference's CUDA harness draws, is unpinned (no cuRAND here).
+    Asynchronous on the current stream, like every op here."""
     if count < 0:
         raise ValueError(f"count must be >= 0, got {count}")
     dev = _gpu_device(device)
