@@ -13,6 +13,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_amd.so")
 TORCH_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_torch.so")
 TUNE_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_tune.so")
+MULTI_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_multi.so")
 
 HG_LAYOUT_AOS = 0
 HG_LAYOUT_SOA = 1
@@ -116,6 +117,39 @@ def tune() -> ctypes.CDLL:
             raise ImportError(f"{TUNE_LIB_PATH} not built: run build()")
         _tune = ctypes.CDLL(TUNE_LIB_PATH)
     return _tune
+
+
+class DeviceBatch(ctypes.Structure):
+    """hg_device_batch (include/sks_homography_multi.h)."""
+    _fields_ = [("device", ctypes.c_int), ("src", ctypes.c_void_p), ("tar", ctypes.c_void_p),
+                ("H", ctypes.c_void_p), ("n", ctypes.c_int64), ("stream", ctypes.c_void_p)]
+
+
+MULTI_SIGNATURES = {
+    "hg_shard_range": ([_i64, _int, _int, ctypes.POINTER(_i64), ctypes.POINTER(_i64)], _int),
+    "hg_solve_multi": ([_int, _int, ctypes.POINTER(DeviceBatch), _int, _int, _int], _int),
+    "hg_sync_multi": ([ctypes.POINTER(DeviceBatch), _int], _int),
+    "hg_comm_init_all": ([_int, ctypes.POINTER(_int), ctypes.POINTER(_vp)], _int),
+    "hg_comm_destroy": ([_int, ctypes.POINTER(_vp)], _int),
+    "hg_gather_multi": ([ctypes.POINTER(DeviceBatch), _int, _int, _int, _vp, ctypes.POINTER(_vp)],
+                        _int),
+}
+_multi = None
+
+
+def multi() -> ctypes.CDLL:
+    """The multi-GPU C ABI (include/sks_homography_multi.h; links librccl)."""
+    global _multi
+    if _multi is None:
+        lib()  # the product library first (the multi library links it)
+        if not os.path.exists(MULTI_LIB_PATH):
+            raise ImportError(f"{MULTI_LIB_PATH} not built: run build()")
+        m = ctypes.CDLL(MULTI_LIB_PATH)
+        for name, (args, res) in MULTI_SIGNATURES.items():
+            fn = getattr(m, name)
+            fn.argtypes, fn.restype = args, res
+        _multi = m
+    return _multi
 
 
 def call(name: str, *args) -> None:

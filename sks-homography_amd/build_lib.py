@@ -22,6 +22,7 @@ LIB_DIR = os.path.join(HERE, "lib")
 LIB = os.path.join(LIB_DIR, "libsks_homography_amd.so")
 TORCH_LIB = os.path.join(LIB_DIR, "libsks_homography_torch.so")
 TUNE_LIB = os.path.join(LIB_DIR, "libsks_homography_tune.so")
+MULTI_LIB = os.path.join(LIB_DIR, "libsks_homography_multi.so")
 ARCH = os.environ.get("SKS_AMD_ARCH", "gfx950")
 
 SOURCES = ["hg_kernels.hip", "hg_ransac.hip", "hg_table8.hip", "hg_sks_api.cpp", "hg_host.cpp"]
@@ -238,7 +239,25 @@ def build(verbose: bool = False, force: bool = False) -> str:
             print(" ".join(cmd))
         subprocess.run(cmd, check=True)
     build_torch_ops(verbose, force, headers)
+    build_multi(verbose, force, headers)
     return LIB
+
+
+def build_multi(verbose: bool = False, force: bool = False, headers=()) -> str:
+    """lib/libsks_homography_multi.so: the multi-GPU C ABI (csrc/hg_multi.cpp,
+    include/sks_homography_multi.h), host C++ over the product library and librccl -- kept
+    apart so the product library has no RCCL dependency."""
+    src = os.path.join(CSRC, "hg_multi.cpp")
+    if not force and not _stale(MULTI_LIB, [src, LIB, *headers]):
+        return MULTI_LIB
+    cmd = ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-o", MULTI_LIB, src,
+           "-D__HIP_PLATFORM_AMD__=1", f"-I{os.path.join(ROOT, 'include')}", "-I/opt/rocm/include",
+           f"-L{LIB_DIR}", "-lsks_homography_amd", "-L/opt/rocm/lib", "-lamdhip64", "-lrccl",
+           "-Wl,-rpath,$ORIGIN", "-Wl,-rpath,/opt/rocm/lib"]
+    if verbose:
+        print(" ".join(cmd))
+    subprocess.run(cmd, check=True)
+    return MULTI_LIB
 
 
 def build_torch_ops(verbose: bool = False, force: bool = False, headers=()) -> str:

@@ -58,6 +58,13 @@ for step in $STEPS; do
                 tests/test_gpu_rect_aten_bits.py tests/test_gpu_offsets.py tests/test_gpu_parity.py -m gpu -v -s \
                 -k "rect or offsets or grad" -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         autograd_cost) run autograd_cost 300 python -u tools/autograd_cost.py ;;
+        multi_tests) run pytest_multi 300 python -u -m pytest tests/test_gpu_multi.py tests/test_multi_capi.py -v \
+                -p no:cacheprovider --timeout 120 --timeout-method thread ;;
+        gpus2_bare)
+            # the driver-shaped bare command with --gpus 2 and no torchrun: bench.py starts the
+            # two ranks itself (gloo: they share the one GPU here) and prints n_gpus 2
+            run gpus2_bare 400 python bench.py --gpus 2 --steps 20 --warmup 2 --no-extras \
+                --dist-backend gloo ;;
         prof_rect_bwd) run prof_rect_bwd 300 rocprofv3 --kernel-trace --stats --output-format csv \
                 -d "$OUT/prof_rect_bwd_$TAG" -o run -- python3 tools/prof_rect_bwd.py ;;
         aten_tests) run pytest_aten 600 python -u -m pytest tests/test_gpu_aten_sum.py tests/test_gpu_rect_grad.py \
