@@ -88,6 +88,12 @@ for step in $STEPS; do
                 -d "$OUT/pmc_fetch_$TAG" -o run -- python3 tools/pmc_run.py
             run pmc_write 600 rocprofv3 --pmc WRITE_SIZE --output-format csv \
                 -d "$OUT/pmc_write_$TAG" -o run -- python3 tools/pmc_run.py ;;
+        pmc_reduce)
+            # reduce the passes on the box itself (same tree, same library) so the bench that
+            # follows in this call reads the fresh figures; the summary comes back in gpurun_out
+            PMC_TAG="$TAG" python3 tools/pmc_traffic.py "$OUT/pmc_fetch_$TAG" "$OUT/pmc_write_$TAG" \
+                profiles/pmc_traffic.json > "$OUT/pmc_reduce.log" 2>&1 \
+                && cp profiles/pmc_traffic.json "$OUT/pmc_traffic_$TAG.json" ;;
         pmc_score)
             run pmc_score 300 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES \
                 SQ_WAVE_CYCLES SQ_INSTS_VALU_FLOPS_FP32 GRBM_GUI_ACTIVE --kernel-trace \
