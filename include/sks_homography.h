@@ -133,6 +133,31 @@ int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, co
                                           float* grad_scale, int scale_rows, float* grad_div,
                                           int div_rows, void* stream);
 
+/* Whose evaluation of the reference's TensorACA_rect statements to reproduce, bit for bit.
+ * HG_ORDER_ATEN_CPU: ATen on the CPU (what the fixtures pin, and what every other TensorACA
+ * entry point follows).  HG_ORDER_ATEN_ROCM: torch-ROCm on the GPU -- the reference's default
+ * run (Modules_Runtime_Test.py:393, device='cuda') -- which sums every 3-term reduction as
+ * ((0 + t0) + t2) + t1 (the forward's torch.sum and the backward's sum_to_size over three
+ * elements); cross products and element-wise ops are the same bits on both. */
+#define HG_ORDER_ATEN_CPU 0
+#define HG_ORDER_ATEN_ROCM 1
+
+/* hg_tensor_aca_rect_bcast_f32 / its backward with the evaluation order `order`
+ * (HG_ORDER_*); strides 0 / 0 give the batch-uniform (1,) scale / div.  HG_ORDER_ATEN_CPU
+ * is exactly the bcast entry points.  The backward's per-parameter modes are theirs, and
+ * modes 1 / 2 leave the batch sums to the caller (hg_sum_aten_f32 is ATen-CPU's order; the
+ * GPU run's batch sums follow ROCm's reduction tree, which is not restated here). */
+int hg_tensor_aca_rect_order_f32(const float* src, const float* tar, float* H, int64_t B,
+                                 const float* scale, int64_t scale_sb, int64_t scale_sr,
+                                 const float* div, int64_t div_sb, int64_t div_sr, int order,
+                                 void* stream);
+int hg_tensor_aca_rect_backward_order_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, int64_t scale_sb,
+                                          int64_t scale_sr, const float* div, int64_t div_sb,
+                                          int64_t div_sr, float* grad_src, float* grad_tar,
+                                          float* grad_scale, int scale_rows, float* grad_div,
+                                          int div_rows, int order, void* stream);
+
 /* Compact TensorACA for deep-homography nets: the source is the
  * axis-aligned width x height rectangle with top-left corner (B,2) -- getInput's shape,
  * Modules_Runtime_Test.py:9-16 -- and the target is source + offsets (B,4,2), the

@@ -40,6 +40,11 @@ SIGNATURES = {
                                      _int),
     "hg_tensor_aca_rect_bcast_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,
                                                _i64, _vp, _vp, _vp, _int, _vp, _int, _vp], _int),
+    "hg_tensor_aca_rect_order_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _int,
+                                      _vp], _int),
+    "hg_tensor_aca_rect_backward_order_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,
+                                               _i64, _vp, _vp, _vp, _int, _vp, _int, _int, _vp],
+                                              _int),
     "hg_tensor_aca_offsets_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
                                   _int),
     "hg_tensor_aca_offsets_backward_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,

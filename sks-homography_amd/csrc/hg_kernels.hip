@@ -583,7 +583,7 @@ int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, i
         return hg::launch(hg::tensor_aca_rect_bcast_staged<false>, g, hg::kBlock, 0, s, src, tar, H,
                           B, a);
     }
-    return hg::launch(hg::tensor_aca_rect_bcast_kernel, hg::generic_grid(B), hg::kBlock, 0, s, src,
+    return hg::launch(hg::tensor_aca_rect_bcast_kernel<hg::kAtenCpu>, hg::generic_grid(B), hg::kBlock, 0, s, src,
                       tar, H, B, a);
 }
 
@@ -598,9 +598,54 @@ int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, co
     if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
     if (scale_rows < 0 || scale_rows > 2 || div_rows < 0 || div_rows > 2) return hg::kErrInvalid;
     const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
-    return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel, hg::generic_grid(B), hg::kBlock,
+    return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel<hg::kAtenCpu>, hg::generic_grid(B), hg::kBlock,
                       0, reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, B, a, grad_src,
                       grad_tar, grad_scale, scale_rows, grad_div, div_rows);
+}
+
+int hg_tensor_aca_rect_order_f32(const float* src, const float* tar, float* H, int64_t B,
+                                 const float* scale, int64_t scale_sb, int64_t scale_sr,
+                                 const float* div, int64_t div_sb, int64_t div_sr, int order,
+                                 void* stream) {
+    if (order == HG_ORDER_ATEN_CPU)
+        return hg_tensor_aca_rect_bcast_f32(src, tar, H, B, scale, scale_sb, scale_sr, div, div_sb,
+                                            div_sr, stream);
+    if (order != HG_ORDER_ATEN_ROCM || B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !H || !scale || !div) return hg::kErrInvalid;
+    const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(H)) {
+        const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
+        if (B * 140 > hg::kMallResidentBytes)
+            return hg::launch(hg::tensor_aca_rect_bcast_staged<true, hg::kAtenRocm>, g, hg::kBlock, 0,
+                              s, src, tar, H, B, a);
+        return hg::launch(hg::tensor_aca_rect_bcast_staged<false, hg::kAtenRocm>, g, hg::kBlock, 0, s,
+                          src, tar, H, B, a);
+    }
+    return hg::launch(hg::tensor_aca_rect_bcast_kernel<hg::kAtenRocm>, hg::generic_grid(B), hg::kBlock,
+                      0, s, src, tar, H, B, a);
+}
+
+int hg_tensor_aca_rect_backward_order_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, int64_t scale_sb,
+                                          int64_t scale_sr, const float* div, int64_t div_sb,
+                                          int64_t div_sr, float* grad_src, float* grad_tar,
+                                          float* grad_scale, int scale_rows, float* grad_div,
+                                          int div_rows, int order, void* stream) {
+    if (order == HG_ORDER_ATEN_CPU)
+        return hg_tensor_aca_rect_bcast_backward_f32(src, tar, grad_H, B, scale, scale_sb, scale_sr,
+                                                     div, div_sb, div_sr, grad_src, grad_tar,
+                                                     grad_scale, scale_rows, grad_div, div_rows,
+                                                     stream);
+    if (order != HG_ORDER_ATEN_ROCM || B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
+    if (scale_rows < 0 || scale_rows > 2 || div_rows < 0 || div_rows > 2) return hg::kErrInvalid;
+    const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
+    return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel<hg::kAtenRocm>, hg::generic_grid(B),
+                      hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, B, a,
+                      grad_src, grad_tar, grad_scale, scale_rows, grad_div, div_rows);
 }
 
 int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,

@@ -20,7 +20,8 @@ namespace hg {
 // loads per lane (offsets 0 and 16 of the 48-B src record) issued before the DMA
 // wait.  H is written through the LDS-staged 16-B store.  Ragged/unaligned tiles
 // use per-lane loads and stores.
-template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false, bool NT = true>
+// ORDER: kAtenCpu or kAtenRocm, whose evaluation of the statements to follow (hg_solvers.hpp).
+template <int P, bool VEC, bool SCALAR_ARGS, bool SQUARE = false, bool NT = true, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -55,7 +56,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
         for (int j = 0; j < P; ++j) {
             float tr[12];
             __builtin_memcpy(tr, lds + (j * kWave + lane) * 48, 48);
-            tensor_aca_rect_solve<SQUARE>(tr, mx[j], my[j], scale, div, h[j]);
+            tensor_aca_rect_solve<SQUARE, ORDER>(tr, mx[j], my[j], scale, div, h[j]);
         }
         wave_lds_sync();
         store_rows9_staged<float, P, NT>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
@@ -68,7 +69,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
             float tr[12];
 #pragma unroll
             for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
-            tensor_aca_rect_solve<SQUARE>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
+            tensor_aca_rect_solve<SQUARE, ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, h[j]);
 #pragma unroll
             for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[j][k];
         }
@@ -102,7 +103,7 @@ __device__ __forceinline__ void store_terms3_staged(char* __restrict__ out, cons
     wave_lds_sync();
 }
 
-template <bool WANT_SRC, bool WANT_SD>
+template <bool WANT_SRC, bool WANT_SD, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -116,8 +117,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
         float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx,
-                                   gmy, gsr, gdr);
+        tensor_aca_rect_grad_terms<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt,
+                                          gmx, gmy, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {
@@ -150,6 +151,7 @@ __device__ __forceinline__ void rect_bcast_load(const RectBcast& a, int64_t p, f
     }
 }
 
+template <int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H, int64_t B,
     RectBcast a) {
@@ -159,7 +161,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_kernel(
 #pragma unroll
         for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
         rect_bcast_load(a, p, sc, dv);
-        tensor_aca_rect_solve_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h);
+        tensor_aca_rect_solve_rows<false, ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h);
 #pragma unroll
         for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[k];
     }
@@ -169,7 +171,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_kernel(
 // wave's tar slab by LDS-DMA, M's x and y with two dword loads, scale / div per (problem, row)
 // through RectBcast, H through the staged 16-B store; a ragged last wave takes the per-lane
 // code.  Same arithmetic, same bits.
-template <bool NT>
+template <bool NT, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
     const float* __restrict__ src, const float* __restrict__ tar, float* __restrict__ H, int64_t B,
     RectBcast a) {
@@ -191,7 +193,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
         slabs_to_lds<kSlab, 1, true, NT>(g, l, lane);
         float tr[12];
         __builtin_memcpy(tr, lds + lane * 48, 48);
-        tensor_aca_rect_solve_rows(tr, mx, my, sc, dv, h[0]);
+        tensor_aca_rect_solve_rows<false, ORDER>(tr, mx, my, sc, dv, h[0]);
         wave_lds_sync();
         store_rows9_staged<float, 1, NT>(reinterpret_cast<char*>(H + base * 9), h, lds, lane);
         return;
@@ -201,7 +203,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
 #pragma unroll
     for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
     rect_bcast_load(a, p, sc, dv);
-    tensor_aca_rect_solve_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h[0]);
+    tensor_aca_rect_solve_rows<false, ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, h[0]);
 #pragma unroll
     for (int k = 0; k < 9; ++k) H[p * 9 + k] = h[0][k];
 }
@@ -211,6 +213,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_staged(
 // 0), each row's share as (3,B) rows (gs[r * B + p]; mode 1) or as the (B,3) terms in the
 // order ATen sums them to a batch-uniform shape (gs[3 p + r]; mode 2); the caller reduces
 // them to the parameter's shape.
+template <int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, RectBcast a, float* __restrict__ gsrc, float* __restrict__ gtar,
@@ -224,7 +227,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_bcast_backward_kernel(
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
         rect_bcast_load(a, p, sc, dv);
         float gmx, gmy, gscale, gdiv;
-        tensor_aca_rect_grad_rows(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, g, gt, gmx, gmy,
+        tensor_aca_rect_grad_rows<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, g, gt, gmx, gmy,
                                   gscale, gdiv, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
@@ -346,7 +349,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
 // there, and the gradient rows leave as contiguous slabs (store_rows_staged) instead
 // of 48-B / 32-B per-lane strided accesses.  The ragged tail takes the per-lane code.
 // Same arithmetic (tensor_aca_rect_grad), same bits.
-template <bool WANT_SRC, bool WANT_SD, bool NT>
+template <bool WANT_SRC, bool WANT_SD, bool NT, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -371,7 +374,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
         float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms(tr, mx, my, scale, div, g, gt, gmx, gmy, gsr, gdr);
+        tensor_aca_rect_grad_terms<ORDER>(tr, mx, my, scale, div, g, gt, gmx, gmy, gsr, gdr);
         wave_lds_sync();  // the staging below reuses the input bytes
         store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
         if constexpr (WANT_SRC) {
@@ -402,8 +405,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
         float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt, gmx,
-                                   gmy, gsr, gdr);
+        tensor_aca_rect_grad_terms<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt,
+                                          gmx, gmy, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {

@@ -368,7 +368,40 @@ __device__ __forceinline__ void solve(const T (&s)[8], const T (&t)[8], T (&h)[9
 // Row forms: scale and div per row r of H -- the reference composition broadcasts them
 // against the (B,3,1) columns (.py:301-302), so a (B,1,1) tensor gives per-problem values
 // and a (B,3,1) one per-row values; the batch-uniform forms below pass one value thrice.
-template <bool SQUARE = false>
+//
+// ORDER: whose evaluation of the statements to follow.  kAtenCpu (0): ATen-CPU's, above.
+// kAtenRocm (1): torch-ROCm's on the GPU -- the reference's default run (.py:393,
+// device='cuda') -- which differs only in its 3-term reductions: the forward's torch.sum and,
+// in the backward, every sum_to_size over three elements run ((0 + t0) + t2) + t1 (measured:
+// tools/rocm_grad_probe*.py, profiles/r04/rocm_grad_probe*.json); the cross products and the
+// element-wise ops are the same bits on both devices.
+constexpr int kAtenCpu = 0, kAtenRocm = 1;
+
+// +0 + t as a real add.  With t = -x the IR holds fsub +0, x, and the gfx950 instruction
+// selector folds that into a negate source modifier of the next add -- -0 for x = +0 where
+// the subtraction gives +0 (seen as v_sub_f32 v, -x, y in tensor_aca_rect_grad_rows' sneg;
+// tests/test_gpu_rect_rocm_order.py, tests/test_gpu_rect_bcast.py's signed-zero case).  The
+// empty asm makes t opaque to that fold; it emits no instruction.
+__device__ __forceinline__ float zero_plus(float t) {
+    asm volatile("" : "+v"(t));
+    return 0.f + t;
+}
+
+template <int ORDER>
+__device__ __forceinline__ float sum3(float t0, float t1, float t2) {
+    if constexpr (ORDER == kAtenRocm) return (zero_plus(t0) + t2) + t1;
+    else return ((t0 + t1) + t2) + 0.f;  // left to right from ATen's +0 accumulator
+}
+
+// A (B,1,1) operand's three-row sum (sum_to_size): from +0 in the device's order (CPU:
+// ((0 + t0) + t1) + t2, which the running sums from 0 gave until r03).
+template <int ORDER>
+__device__ __forceinline__ float rows3(float t0, float t1, float t2) {
+    if constexpr (ORDER == kAtenRocm) return sum3<ORDER>(t0, t1, t2);
+    else return (zero_plus(t0) + t1) + t2;
+}
+
+template <bool SQUARE = false, int ORDER = kAtenCpu>
 __device__ __forceinline__ void tensor_aca_rect_solve_rows(const float (&tr)[12], float mx,
                                                            float my, const float (&scale)[3],
                                                            const float (&div)[3], float (&h)[9]) {
@@ -377,7 +410,7 @@ __device__ __forceinline__ void tensor_aca_rect_solve_rows(const float (&tr)[12]
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
     const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
     const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
-    const float sum = ((c0 + c1) + c2) + 0.f;  // torch.sum starts from +0
+    const float sum = sum3<ORDER>(c0, c1, c2);  // torch.sum starts from +0
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const float b = sum * tr[4 * r];
@@ -389,11 +422,11 @@ __device__ __forceinline__ void tensor_aca_rect_solve_rows(const float (&tr)[12]
     }
 }
 
-template <bool SQUARE = false>
+template <bool SQUARE = false, int ORDER = kAtenCpu>
 __device__ __forceinline__ void tensor_aca_rect_solve(const float (&tr)[12], float mx, float my,
                                                       float scale, float div, float (&h)[9]) {
     const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
-    tensor_aca_rect_solve_rows<SQUARE>(tr, mx, my, sc, dv, h);
+    tensor_aca_rect_solve_rows<SQUARE, ORDER>(tr, mx, my, sc, dv, h);
 }
 
 // Compact deep-homography form: the source is the axis-aligned
@@ -435,6 +468,8 @@ __device__ __forceinline__ void rect_target_from_offsets(float mx, float my, flo
 // dL/ddiv (three-row sums from +0, as sum_to_size gives a (B,1,1) parameter).
 // Row form: per-row scale / div (as tensor_aca_rect_solve_rows), and each row's own share of
 // dL/dscale[r], dL/ddiv[r] in gsr / gdr beside the per-problem sums gscale / gdiv.
+// ORDER (see tensor_aca_rect_solve_rows): kAtenRocm runs every 3-term reduction the GPU's way.
+template <int ORDER = kAtenCpu>
 __device__ __forceinline__ void tensor_aca_rect_grad_rows(
     const float (&tr)[12], float mx, float my, const float (&scale)[3], const float (&div)[3],
     const float (&g)[9], float (&gt)[12], float& gmx, float& gmy, float& gscale, float& gdiv,
@@ -444,9 +479,8 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
     const float c0 = __builtin_fmaf(ay, bz, -(az * by));
     const float c1 = __builtin_fmaf(az, bx, -(ax * bz));
     const float c2 = __builtin_fmaf(ax, by, -(ay * bx));
-    const float sum = ((c0 + c1) + c2) + 0.f;  // torch.sum starts from +0
-    float gh0[3], gy[3], ght[3];
-    gmx = 0.f; gmy = 0.f; gscale = 0.f; gdiv = 0.f;
+    const float sum = sum3<ORDER>(c0, c1, c2);  // torch.sum starts from +0
+    float gh0[3], gy[3], ght[3], pmx[3], pmy[3];
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
         const float b = sum * tr[4 * r];
@@ -456,19 +490,22 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
         const float g2 = g[3 * r + 2];
         gh0[r] = (g[3 * r + 0] - mx * g2) + 0.f;
         const float gh1 = (g[3 * r + 1] - my * g2) + 0.f;
-        gmx = gmx - g2 * h0;
-        gmy = gmy - g2 * h1;
+        pmx[r] = -(g2 * h0);
+        pmy[r] = -(g2 * h1);
         gsr[r] = g2 * b;
-        gscale = gscale + gsr[r];
         gy[r] = div[r] * gh1;
         gdr[r] = gh1 * x;
-        gdiv = gdiv + gdr[r];
         ght[r] = (scale[r] * g2 - gy[r]) - gh0[r];
     }
+    // the per-problem sums over the rows (sum_to_size to (B,1,1))
+    gmx = rows3<ORDER>(pmx[0], pmx[1], pmx[2]);
+    gmy = rows3<ORDER>(pmy[0], pmy[1], pmy[2]);
+    gscale = rows3<ORDER>(gsr[0], gsr[1], gsr[2]);
+    gdiv = rows3<ORDER>(gdr[0], gdr[1], gdr[2]);
     // dL/dsum, dL/dQ4[0], dL/dQ4[1]: sums over the rows to the (B,1,1) shapes
-    const float gS = ((ght[0] * tr[0] + ght[1] * tr[4]) + ght[2] * tr[8]) + 0.f;
-    const float s0 = ((gh0[0] * tr[1] + gh0[1] * tr[5]) + gh0[2] * tr[9]) + 0.f;
-    const float s1 = ((gy[0] * tr[2] + gy[1] * tr[6]) + gy[2] * tr[10]) + 0.f;
+    const float gS = sum3<ORDER>(ght[0] * tr[0], ght[1] * tr[4], ght[2] * tr[8]);
+    const float s0 = sum3<ORDER>(gh0[0] * tr[1], gh0[1] * tr[5], gh0[2] * tr[9]);
+    const float s1 = sum3<ORDER>(gy[0] * tr[2], gy[1] * tr[6], gy[2] * tr[10]);
     const float gc0 = (gS + s0) + 0.f, gc1 = (gS + s1) + 0.f, gc2 = gS + 0.f;
     // Q4 = a x b (a = D's y row, b = its x row): dL/da = b x gc, dL/db = gc x a
     float d[2][3];
@@ -483,7 +520,7 @@ __device__ __forceinline__ void tensor_aca_rect_grad_rows(
         // D = tar[:, :, 1:] - tar[:, :, 0:1]; D's w row has no gradient (+0)
         const float d0 = r < 2 ? d[r][0] : 0.f, d1 = r < 2 ? d[r][1] : 0.f;
         const float d2 = r < 2 ? d[r][2] : 0.f;
-        const float sneg = (((-d0) + (-d1)) + (-d2)) + 0.f;
+        const float sneg = sum3<ORDER>(-d0, -d1, -d2);
         gt[4 * r + 0] = (ght[r] * sum + sneg) + 0.f;
         gt[4 * r + 1] = (d0 + gh0[r] * c0) + 0.f;
         gt[4 * r + 2] = (d1 + gy[r] * c1) + 0.f;
@@ -658,17 +695,19 @@ __device__ __host__ __forceinline__ void aca_vanilla_grad(const T (&s)[8], const
     gt[4] = gt20 + T(0); gt[5] = gt21 + T(0); gt[6] = gt30 + T(0); gt[7] = gt31 + T(0);
 }
 
+template <int ORDER = kAtenCpu>
 __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], float mx, float my,
                                                      float scale, float div, const float (&g)[9],
                                                      float (&gt)[12], float& gmx, float& gmy,
                                                      float& gscale, float& gdiv) {
     const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
     float gsr[3], gdr[3];
-    tensor_aca_rect_grad_rows(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
+    tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
 }
 
 // The same with each row's share of dL/dscale, dL/ddiv (the (B,3,1) terms ATen autograd sums
 // to a (1,) parameter's shape) instead of the per-problem sums.
+template <int ORDER = kAtenCpu>
 __device__ __forceinline__ void tensor_aca_rect_grad_terms(const float (&tr)[12], float mx,
                                                            float my, float scale, float div,
                                                            const float (&g)[9], float (&gt)[12],
@@ -676,7 +715,7 @@ __device__ __forceinline__ void tensor_aca_rect_grad_terms(const float (&tr)[12]
                                                            float (&gdr)[3]) {
     const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
     float gscale, gdiv;
-    tensor_aca_rect_grad_rows(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
+    tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
 }
 
 }  // namespace hg

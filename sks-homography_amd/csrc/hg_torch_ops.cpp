@@ -98,8 +98,17 @@ Bcast bcast_of(const at::Tensor& t, int64_t B, const char* name) {
 
 bool one_value(const at::Tensor& t) { return t.numel() == 1; }
 
+// Whose evaluation of the statements to reproduce (HG_ORDER_*, include/sks_homography.h):
+// 0 ATen-CPU (the fixtures' order), 1 torch-ROCm (the reference's device='cuda' run).
+int order_of(int64_t order) {
+    TORCH_CHECK(order == HG_ORDER_ATEN_CPU || order == HG_ORDER_ATEN_ROCM,
+                "sks_amd::tensor_aca_rect: order must be 0 (ATen-CPU) or 1 (torch-ROCm), got ",
+                order);
+    return (int)order;
+}
+
 at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& scale_,
-                     const at::Tensor& div_, at::Tensor& out) {
+                     const at::Tensor& div_, int64_t order_, at::Tensor& out) {
     const at::Device dev = tar_.device();
     on_gpu(src_, "src", dev);
     on_gpu(tar_, "tar", dev);
@@ -109,8 +118,17 @@ at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::T
     const int64_t B = tar_.size(0);
     const Bcast sb = bcast_of(scale_, B, "scale"), db = bcast_of(div_, B, "div");
     check_out(out, {B, 3, 3}, dev);
+    const int order = order_of(order_);
     const at::Tensor src = src_.contiguous(), tar = tar_.contiguous();
     const c10::DeviceGuard guard(dev);
+    if (order == HG_ORDER_ATEN_ROCM) {
+        hip_ok(hg_tensor_aca_rect_order_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
+                                            out.data_ptr<float>(), B, scale_.data_ptr<float>(),
+                                            sb.sb, sb.sr, div_.data_ptr<float>(), db.sb, db.sr,
+                                            order, stream_of(tar)),
+               "hg_tensor_aca_rect_order_f32");
+        return out;
+    }
     if (one_value(scale_) && one_value(div_)) {  // the reference's own (1,) tensors (.py:33-35)
         hip_ok(hg_tensor_aca_rect_f32(src.data_ptr<float>(), tar.data_ptr<float>(),
                                       out.data_ptr<float>(), B, scale_.data_ptr<float>(),
@@ -127,9 +145,9 @@ at::Tensor& rect_out(const at::Tensor& src_, const at::Tensor& tar_, const at::T
 }
 
 at::Tensor rect(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
-                const at::Tensor& div) {
+                const at::Tensor& div, int64_t order) {
     at::Tensor out = at::empty({tar.size(0), 3, 3}, tar.options());
-    rect_out(src, tar, scale, div, out);
+    rect_out(src, tar, scale, div, order, out);
     return out;
 }
 
@@ -200,7 +218,7 @@ at::Tensor reduce_param_grad(at::Tensor part, const Bcast& b, const at::Tensor& 
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     const at::Tensor& src_, const at::Tensor& tar_, const at::Tensor& grad_,
     const at::Tensor& scale_, const at::Tensor& div_, bool need_src, bool need_scale_div,
-    int64_t aten_threads) {
+    int64_t aten_threads, int64_t order_) {
     const at::Device dev = tar_.device();
     on_gpu(src_, "src", dev);
     on_gpu(tar_, "tar", dev);
@@ -219,7 +237,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     const c10::DeviceGuard guard(dev);
     void* st = stream_of(tar);
     const int threads = aten_threads_of(aten_threads);
-    if (one_value(scale_) && one_value(div_)) {
+    const int order = order_of(order_);
+    if (order == HG_ORDER_ATEN_CPU && one_value(scale_) && one_value(div_)) {
         at::Tensor part = need_scale_div ? at::empty({2, 3 * B}, tar.options()) : none;
         hip_ok(hg_tensor_aca_rect_backward_f32(
                    src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
@@ -236,17 +255,19 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
         return {g_src, g_tar, g_sd.slice(0, 0, 1).reshape(scale_.sizes()),
                 g_sd.slice(0, 1, 2).reshape(div_.sizes())};
     }
-    // each parameter's terms in the layout its reduction reads (terms_mode)
+    // each parameter's terms in the layout its reduction reads (terms_mode); in ROCm order the
+    // per-problem three-row sums follow the GPU's ((0 + t0) + t2) + t1 and the batch sums stay
+    // ATen-CPU's (ROCm's reduction tree is not restated: include/sks_homography.h)
     const int ms = terms_mode(sb), md = terms_mode(db);
     at::Tensor ps = need_scale_div ? at::empty({ms ? 3 * B : B}, tar.options()) : none;
     at::Tensor pd = need_scale_div ? at::empty({md ? 3 * B : B}, tar.options()) : none;
-    hip_ok(hg_tensor_aca_rect_bcast_backward_f32(
+    hip_ok(hg_tensor_aca_rect_backward_order_f32(
                src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
                scale_.data_ptr<float>(), sb.sb, sb.sr, div_.data_ptr<float>(), db.sb, db.sr,
                need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
                need_scale_div && B ? ps.data_ptr<float>() : nullptr, ms,
-               need_scale_div && B ? pd.data_ptr<float>() : nullptr, md, st),
-           "hg_tensor_aca_rect_bcast_backward_f32");
+               need_scale_div && B ? pd.data_ptr<float>() : nullptr, md, order, st),
+           "hg_tensor_aca_rect_backward_order_f32");
     if (!need_scale_div) return {g_src, g_tar, none, none};
     return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, threads, st),
             reduce_param_grad(pd, db, div_, B, threads, st)};
@@ -464,25 +485,26 @@ at::Tensor meta_b33(const at::Tensor& t) { return at::empty({t.size(0), 3, 3}, t
 
 // ------------------------------------------------------------------ autograd
 at::Tensor call_rect(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
-                     const at::Tensor& div) {
+                     const at::Tensor& div, int64_t order) {
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::tensor_aca_rect", "")
                          .typed<at::Tensor(const at::Tensor&, const at::Tensor&,
-                                           const at::Tensor&, const at::Tensor&)>();
-    return op.call(src, tar, scale, div);
+                                           const at::Tensor&, const at::Tensor&, int64_t)>();
+    return op.call(src, tar, scale, div, order);
 }
 
 // The backward ops are reached through the dispatcher too, so tracing (fake tensors,
 // AOT autograd) sees their Meta kernels instead of a raw launch.
 std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> call_rect_backward(
     const at::Tensor& src, const at::Tensor& tar, const at::Tensor& grad, const at::Tensor& scale,
-    const at::Tensor& div, bool need_src, bool need_sd, int64_t threads) {
+    const at::Tensor& div, bool need_src, bool need_sd, int64_t threads, int64_t order) {
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::tensor_aca_rect_backward", "")
                          .typed<std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor>(
                              const at::Tensor&, const at::Tensor&, const at::Tensor&,
-                             const at::Tensor&, const at::Tensor&, bool, bool, int64_t)>();
-    return op.call(src, tar, grad, scale, div, need_src, need_sd, threads);
+                             const at::Tensor&, const at::Tensor&, bool, bool, int64_t,
+                             int64_t)>();
+    return op.call(src, tar, grad, scale, div, need_src, need_sd, threads, order);
 }
 
 std::tuple<at::Tensor, at::Tensor> call_offsets_backward(const at::Tensor& corner,
@@ -500,12 +522,13 @@ std::tuple<at::Tensor, at::Tensor> call_offsets_backward(const at::Tensor& corne
 class RectFunction : public torch::autograd::Function<RectFunction> {
    public:
     static at::Tensor forward(AutogradContext* ctx, const at::Tensor& src, const at::Tensor& tar,
-                              const at::Tensor& scale, const at::Tensor& div) {
+                              const at::Tensor& scale, const at::Tensor& div, int64_t order) {
         at::AutoDispatchBelowADInplaceOrView below;
         ctx->save_for_backward({src, tar, scale, div});
         // the caller's ATen thread count: the backward may run on an autograd device thread
         ctx->saved_data["threads"] = (int64_t)at::get_num_threads();
-        return call_rect(src, tar, scale, div);
+        ctx->saved_data["order"] = order;
+        return call_rect(src, tar, scale, div, order);
     }
 
     static variable_list backward(AutogradContext* ctx, variable_list grads) {
@@ -515,10 +538,11 @@ class RectFunction : public torch::autograd::Function<RectFunction> {
         const bool need_sd = ctx->needs_input_grad(2) || ctx->needs_input_grad(3);
         auto [g_src, g_tar, g_scale, g_div] =
             call_rect_backward(src, tar, grads[0].contiguous(), scale, div, need_src, need_sd,
-                               ctx->saved_data["threads"].toInt());
+                               ctx->saved_data["threads"].toInt(), ctx->saved_data["order"].toInt());
         at::Tensor none;
         return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none,
-                ctx->needs_input_grad(2) ? g_scale : none, ctx->needs_input_grad(3) ? g_div : none};
+                ctx->needs_input_grad(2) ? g_scale : none, ctx->needs_input_grad(3) ? g_div : none,
+                none};
     }
 };
 
@@ -530,12 +554,12 @@ bool any_requires_grad(std::initializer_list<const at::Tensor*> ts) {
 }
 
 at::Tensor rect_autograd(const at::Tensor& src, const at::Tensor& tar, const at::Tensor& scale,
-                         const at::Tensor& div) {
+                         const at::Tensor& div, int64_t order) {
     if (!any_requires_grad({&src, &tar, &scale, &div})) {  // inference: no graph node
         at::AutoDispatchBelowADInplaceOrView below;
-        return call_rect(src, tar, scale, div);
+        return call_rect(src, tar, scale, div, order);
     }
-    return RectFunction::apply(src, tar, scale, div);
+    return RectFunction::apply(src, tar, scale, div, order);
 }
 
 at::Tensor call_rect_scalar(const at::Tensor& src, const at::Tensor& tar, double scale, double div) {
@@ -566,7 +590,8 @@ class RectScalarFunction : public torch::autograd::Function<RectScalarFunction> 
         const at::Tensor dv = at::full({1}, (float)ctx->saved_data["div"].toDouble(), opts);
         const bool need_src = ctx->needs_input_grad(0);
         auto [g_src, g_tar, g_sc, g_dv] =
-            call_rect_backward(saved[0], saved[1], grads[0].contiguous(), sc, dv, need_src, false, 0);
+            call_rect_backward(saved[0], saved[1], grads[0].contiguous(), sc, dv, need_src, false, 0,
+                               HG_ORDER_ATEN_CPU);
         at::Tensor none;
         return {need_src ? g_src : none, ctx->needs_input_grad(1) ? g_tar : none, none, none};
     }
@@ -715,14 +740,15 @@ TORCH_LIBRARY(sks_amd, m) {
     m.def("solve(Tensor src, Tensor tar, int algo, bool normalize, int layout) -> Tensor");
     m.def("solve.out(Tensor src, Tensor tar, int algo, bool normalize, int layout, *, "
           "Tensor(a!) out) -> Tensor(a!)");
-    m.def("tensor_aca_rect(Tensor src, Tensor tar, Tensor scale, Tensor div) -> Tensor");
-    m.def("tensor_aca_rect.out(Tensor src, Tensor tar, Tensor scale, Tensor div, *, "
+    m.def("tensor_aca_rect(Tensor src, Tensor tar, Tensor scale, Tensor div, int order=0) -> "
+          "Tensor");
+    m.def("tensor_aca_rect.out(Tensor src, Tensor tar, Tensor scale, Tensor div, int order=0, *, "
           "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect.scalar(Tensor src, Tensor tar, float scale, float div) -> Tensor");
     m.def("tensor_aca_rect.scalar_out(Tensor src, Tensor tar, float scale, float div, *, "
           "Tensor(a!) out) -> Tensor(a!)");
     m.def("tensor_aca_rect_backward(Tensor src, Tensor tar, Tensor grad, Tensor scale, "
-          "Tensor div, bool need_src, bool need_scale_div, int aten_threads=0) -> "
+          "Tensor div, bool need_src, bool need_scale_div, int aten_threads=0, int order=0) -> "
           "(Tensor, Tensor, Tensor, Tensor)");
     m.def("aca_backward(Tensor src, Tensor tar, Tensor grad, bool need_src, bool need_tar) -> "
           "(Tensor, Tensor)");
@@ -758,7 +784,8 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
     m.impl("aca", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
     m.impl("sks", [](const at::Tensor& s, const at::Tensor& t, bool) { return meta_b33(t); });
     m.impl("tensor_aca_rect", [](const at::Tensor& s, const at::Tensor& t, const at::Tensor& sc,
-                                 const at::Tensor& dv) {
+                                 const at::Tensor& dv, int64_t order) {
+        order_of(order);
         check_rect(s, t);
         bcast_of(sc, t.size(0), "scale");  // the shapes the reference composition accepts
         bcast_of(dv, t.size(0), "div");
@@ -771,7 +798,7 @@ TORCH_LIBRARY_IMPL(sks_amd, Meta, m) {
     });
     m.impl("tensor_aca_rect_backward",
            [](const at::Tensor& s, const at::Tensor& t, const at::Tensor&, const at::Tensor& sc,
-              const at::Tensor& dv, bool need_src, bool need_sd, int64_t) {
+              const at::Tensor& dv, bool need_src, bool need_sd, int64_t, int64_t) {
                const int64_t B = t.size(0);
                return std::make_tuple(need_src ? at::empty({B, 3, 4}, t.options())
                                                : at::empty({0}, t.options()),

@@ -249,8 +249,20 @@ def _gpu_only(t: torch.Tensor) -> None:
                          f"{t.device} tensor (no CPU fallback by design)")
 
 
+_ORDERS = {"cpu": 0, "rocm": 1}
+
+
+def _order(order: str) -> int:
+    """Whose evaluation of the reference's statements to reproduce bit for bit (HG_ORDER_*)."""
+    try:
+        return _ORDERS[order]
+    except KeyError:
+        raise ValueError(f"order must be 'cpu' (ATen-CPU) or 'rocm' (torch-ROCm), got {order!r}") \
+            from None
+
+
 def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Scalar,
-                    out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                    out: Optional[torch.Tensor] = None, order: str = "cpu") -> torch.Tensor:
     """TensorACA rectangle->quad (Modules_Runtime_Test.py:286-309), unnormalised.
 
     src, tar: (B,3,4) float32 homogeneous (rows x, y, 1; columns M, N, P, Q).
@@ -261,19 +273,24 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     Runs torch.ops.sks_amd.tensor_aca_rect (native, csrc/hg_torch_ops.cpp); with tensor
     scale/div and no ``out`` it is differentiable in all four inputs.
 
-    Which bits: the reference's statements as ATen-CPU evaluates them (FMA-contracted cross,
-    the three cross terms summed ((c0 + c1) + c2) + 0), bit for bit.  The same statements on
-    a ROCm GPU sum the terms as (c0 + c2) + c1 (profiles/r03/rocm_sum_probe.json), so against
-    the reference's device='cuda' run H agrees to ~1e-5 relative on fractional inputs (exactly
-    on the reference's integer batches) -- the spread the reference itself shows between its
-    CPU and GPU runs (tests/test_gpu_parity.py::test_rect_close_to_torch_composed_on_gpu).
+    Which bits (``order``): "cpu" (default) -- the reference's statements as ATen-CPU
+    evaluates them (FMA-contracted cross, the three cross terms summed ((c0 + c1) + c2) + 0),
+    bit for bit, as the golden fixtures pin.  "rocm" -- as torch-ROCm evaluates them on the
+    GPU, the reference's own default run (Modules_Runtime_Test.py:393, device='cuda'): every
+    three-term sum, forward and backward, is ((0 + t0) + t2) + t1
+    (profiles/r04/rocm_grad_probe_r04j.json); H, dL/dtar, dL/dsrc and per-problem
+    dL/dscale, dL/ddiv then equal that run's bits.  Batch sums of a (1,) / (3,1) scale or
+    div gradient stay in ATen-CPU's order in both modes (ROCm's reduction tree is not
+    restated).  The two orders differ by ~1e-5 relative on fractional inputs and agree
+    exactly on the reference's integer batches.
     """
     _gpu_only(tar)  # the op checks that src (and out) share tar's device
-    if isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):
+    o = _order(order)
+    if o or isinstance(scale, torch.Tensor) or isinstance(div, torch.Tensor):
         sc, dv = _dev_scalar(scale, tar.device), _dev_scalar(div, tar.device)
         if out is None:
-            return _OPS.tensor_aca_rect.default(src, tar, sc, dv)
-        return _OPS.tensor_aca_rect.out(src, tar, sc, dv, out=out)
+            return _OPS.tensor_aca_rect.default(src, tar, sc, dv, o)
+        return _OPS.tensor_aca_rect.out(src, tar, sc, dv, o, out=out)
     if out is None:
         return _OPS.tensor_aca_rect.scalar(src, tar, float(scale), float(div))
     return _OPS.tensor_aca_rect.scalar_out(src, tar, float(scale), float(div), out=out)
@@ -281,18 +298,19 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
 
 def tensor_aca_rect_backward(src: torch.Tensor, tar: torch.Tensor, grad: torch.Tensor,
                              scale: Scalar, div: Scalar, need_src: bool = True,
-                             need_scale_div: bool = True, aten_threads: int = 0):
+                             need_scale_div: bool = True, aten_threads: int = 0,
+                             order: str = "cpu"):
     """Gradients of tensor_aca_rect: (dL/dsrc (B,3,4) or empty, dL/dtar (B,3,4), dL/dscale,
     dL/ddiv shaped like scale and div, or empty).  The kernel's (problem, row) terms are
     summed over the dimensions scale / div were broadcast along, on the device, in the
     float32 order ATen-CPU's autograd sums them through the reference's statements
     (hg_sum_aten_f32): for a batch-uniform scale / div of >= 32768 terms that order depends
     on ATen's thread count -- this process's (torch.get_num_threads()) unless
-    ``aten_threads`` names another."""
+    ``aten_threads`` names another.  ``order`` as tensor_aca_rect's."""
     _gpu_only(tar)
     return _OPS.tensor_aca_rect_backward.default(
         src, tar, grad, _dev_scalar(scale, tar.device), _dev_scalar(div, tar.device),
-        need_src, need_scale_div, aten_threads)
+        need_src, need_scale_div, aten_threads, _order(order))
 
 
 def tensor_aca_offsets(corner: torch.Tensor, offsets: torch.Tensor, width: float, height: float,
@@ -316,12 +334,13 @@ def tensor_aca_offsets_backward(corner, offsets, grad, width: float, height: flo
 
 
 def tensor_aca_rect_autograd(src: torch.Tensor, tar: torch.Tensor, scale: Scalar,
-                             div: Scalar) -> torch.Tensor:
+                             div: Scalar, order: str = "cpu") -> torch.Tensor:
     """Differentiable TensorACA (torch.ops.sks_amd.tensor_aca_rect): gradients flow to
-    tar, src (M's coordinates), and scale/div when they are tensors requiring grad."""
+    tar, src (M's coordinates), and scale/div when they are tensors requiring grad.
+    ``order`` as tensor_aca_rect's (the backward follows the forward's)."""
     _gpu_only(tar)
     return _OPS.tensor_aca_rect.default(src, tar, _dev_scalar(scale, tar.device),
-                                        _dev_scalar(div, tar.device))
+                                        _dev_scalar(div, tar.device), _order(order))
 
 
 def fill_uniform(count: int, seed: int, offset: int = 0, lo: float = 0.0, hi: float = 1024.0,

@@ -123,6 +123,36 @@ def test_backward_shapes_bits_and_aten(orc, oracle, pkg, dev, gold):
         _bits(orc, thg.grad, g_tar.cpu().numpy(), f"autograd tar {name}")
 
 
+@pytest.mark.parametrize("shape", [(1,), (4096, 1, 1), (3, 1), (4096, 3, 1)])
+def test_backward_signed_zero_sums(orc, oracle, pkg, dev, shape):
+    """Degenerate targets (all four corners at one point) make every H column-0 entry +0, so
+    dL/dsrc[0][0]'s three-row sum adds -(g2 * +0) = -0 terms from +0 and must give +0.  The
+    gfx950 instruction selector turns a leading 0 - x into a negate modifier (-0 here) unless
+    the kernel keeps the add (hg_solvers.hpp zero_plus); this pins the +0 in every kernel
+    variant against the C restatement."""
+    B = 4096
+    rng = np.random.default_rng(17)
+    corner = rng.integers(10, 30, (B, 2)).astype(np.float32)
+    rect = np.array([[0, 0], [128, 0], [0, 128], [128, 128]], np.float32)
+    src = corner[:, None, :] + rect[None]
+    pt = rng.integers(0, 40, (B, 1, 2)).astype(np.float32)
+    tar = np.repeat(pt, 4, axis=1)
+    tar[::3] += rng.integers(0, 4, (len(tar[::3]), 4, 2)).astype(np.float32)  # a few ordinary ones
+    ones = np.ones((B, 1, 4), np.float32)
+    sh = np.ascontiguousarray(np.concatenate([src.transpose(0, 2, 1), ones], 1))
+    th = np.ascontiguousarray(np.concatenate([tar.transpose(0, 2, 1), ones], 1))
+    gH = np.abs(rng.standard_normal((B, 3, 3))).astype(np.float32)
+    gH[1::4] = 0.0
+    sc_np = np.full(shape, 128.0, np.float32)
+    dv_np = np.full(shape, 1.0, np.float32)
+    g_src, g_tar, _, _ = pkg.tensor_aca_rect_backward(_t(sh, dev), _t(th, dev), _t(gH, dev),
+                                                      _t(sc_np, dev), _t(dv_np, dev), True, True)
+    ws, wt, _, _, _, _ = oracle.tensor_aca_rect_rows_backward(sh, th, gH, sc_np, dv_np)
+    assert (ws[:, 0, 0].view(np.uint32) == 0).sum() > B // 2  # the +0 case is exercised
+    _bits(orc, g_src, ws, f"grad_src signed zeros {shape}")
+    _bits(orc, g_tar, wt, f"grad_tar signed zeros {shape}")
+
+
 def test_c_abi_strides(orc, oracle, pkg, dev):
     """hg_tensor_aca_rect_bcast_f32 with explicit element strides (0 = broadcast)."""
     B = 513

@@ -59,6 +59,7 @@ for step in $STEPS; do
                 -k "rect or offsets or grad" -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         autograd_cost) run autograd_cost 300 python -u tools/autograd_cost.py ;;
         rocm_grad_probe) run rocm_grad_probe 300 python -u tools/rocm_grad_probe.py ;;
+        rocm_grad_probe2) run rocm_grad_probe2 300 python -u tools/rocm_grad_probe2.py ;;
         multi_tests) run pytest_multi 300 python -u -m pytest tests/test_gpu_multi.py tests/test_multi_capi.py -v \
                 -p no:cacheprovider --timeout 120 --timeout-method thread ;;
         gpus2_bare)
