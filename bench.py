@@ -1549,6 +1549,20 @@ def main():
                 f_ba()
             _, ms_bt = timed_region(d, f_bt, 20)
             _, ms_ba = timed_region(d, f_ba, 20)
+            # the opt-in torch-ROCm evaluation order (order="rocm"): the same kernels' forms with
+            # the GPU's 3-term sums -- forward, dL/dtar alone, everything
+            f_rf = lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb, order="rocm")  # noqa
+            f_rbt = lambda: pkg.tensor_aca_rect_backward(bs_h, bt_h, gHb, bsc, bdv, False, False,  # noqa
+                                                         order="rocm")
+            f_rba = lambda: pkg.tensor_aca_rect_backward(bs_h, bt_h, gHb, bsc, bdv, True, True,  # noqa
+                                                         order="rocm")
+            for _ in range(5):
+                f_rf()
+                f_rbt()
+                f_rba()
+            _, ms_rf = timed_region(d, f_rf, 50)
+            _, ms_rbt = timed_region(d, f_rbt, 20)
+            _, ms_rba = timed_region(d, f_rba, 20)
             del gHb
             rect_backward_large = {
                 "large_backward_tar_us": round(ms_bt * 1e3, 2),
@@ -1559,6 +1573,19 @@ def main():
                 "large_backward_all_traffic": pmc_detail(
                     "rect_backward_all", "the backward kernel alone; the scale / div sum "
                     "(hg_sum_aten_f32) is in large_backward_all_us"),
+                "rocm_order": {
+                    "large_us_per_call": round(ms_rf * 1e3, 2),
+                    "large_frac": round(big * RECT_LAYOUT_MIN_BYTES / (ms_rf * 1e-3) / 1e9
+                                        / HBM_PEAK_GBPS, 4),
+                    "large_backward_tar_us": round(ms_rbt * 1e3, 2),
+                    "large_backward_tar_frac": round(big * 140 / (ms_rbt * 1e-3) / 1e9
+                                                     / HBM_PEAK_GBPS, 4),
+                    "large_backward_all_us": round(ms_rba * 1e3, 2),
+                    "large_backward_all_frac": round(big * 212 / (ms_rba * 1e-3) / 1e9
+                                                     / HBM_PEAK_GBPS, 4),
+                    "note": "order='rocm' (the reference's device='cuda' bits); frac of the "
+                            "(B,3,4) layout floor forward, of 140 / 212 B backward",
+                },
             }
             # compact form (corner + 4 offsets) on the same big batch
             corner = bs_h[:, 0:2, 0].contiguous()

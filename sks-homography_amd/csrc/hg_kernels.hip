@@ -526,24 +526,22 @@ int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float*
     return hg::launch_rect<true>(src, tar, H, B, nullptr, nullptr, scale, div, stream);
 }
 
-int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
-                                    int64_t B, const float* scale, const float* div,
-                                    float* grad_src, float* grad_tar, float* grad_scale_div,
-                                    void* stream) {
-    if (B < 0) return hg::kErrInvalid;
-    if (B == 0) return 0;
-    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+extern "C++" {
+namespace hg {
+// The one-value backward: the staged form when every buffer is 16-B aligned
+// (tools/kbench_bwd.py), cache policy by size as the forward; scale / div terms as (2,B,3).
+template <int ORDER>
+int launch_rect_backward(const float* src, const float* tar, const float* grad_H, int64_t B,
+                         const float* scale, const float* div, float* grad_src, float* grad_tar,
+                         float* grad_scale_div, hipStream_t s) {
     const bool ws = grad_src != nullptr, wd = grad_scale_div != nullptr;
-    using hg::aligned16;
     if (aligned16(src) && aligned16(tar) && aligned16(grad_H) && aligned16(grad_tar) &&
         (!ws || aligned16(grad_src)) && (!wd || aligned16(grad_scale_div))) {
-        // staged form (tools/kbench_bwd.py); cache policy by size as the forward
-        const unsigned g = (unsigned)hg::ceil_div(B, hg::kBlock);
-        const bool nt = B * 232 > hg::kMallResidentBytes;
+        const unsigned g = (unsigned)ceil_div(B, kBlock);
+        const bool nt = B * 232 > kMallResidentBytes;
 #define HG_RB(A, Bf, NT)                                                                      \
-    hg::launch(hg::tensor_aca_rect_backward_staged<A, Bf, NT>, g, hg::kBlock, 0, s, src, tar,   \
-               grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div)
+    launch(tensor_aca_rect_backward_staged<A, Bf, NT, ORDER>, g, kBlock, 0, s, src, tar, grad_H, \
+           B, scale, div, grad_src, grad_tar, grad_scale_div)
         if (nt) {
             if (ws && wd) return HG_RB(true, true, true);
             if (ws) return HG_RB(true, false, true);
@@ -556,15 +554,29 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
         return HG_RB(false, false, false);
 #undef HG_RB
     }
-    const unsigned g = hg::generic_grid(B);
+    const unsigned g = generic_grid(B);
 #define HG_RECT_BWD(A, Bf)                                                                    \
-    hg::launch(hg::tensor_aca_rect_backward_kernel<A, Bf>, g, hg::kBlock, 0, s, src, tar, grad_H, \
-               B, scale, div, grad_src, grad_tar, grad_scale_div)
+    launch(tensor_aca_rect_backward_kernel<A, Bf, ORDER>, g, kBlock, 0, s, src, tar, grad_H, B, \
+           scale, div, grad_src, grad_tar, grad_scale_div)
     if (ws && wd) return HG_RECT_BWD(true, true);
     if (ws) return HG_RECT_BWD(true, false);
     if (wd) return HG_RECT_BWD(false, true);
     return HG_RECT_BWD(false, false);
 #undef HG_RECT_BWD
+}
+}  // namespace hg
+}  // extern "C++"
+
+int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
+                                    int64_t B, const float* scale, const float* div,
+                                    float* grad_src, float* grad_tar, float* grad_scale_div,
+                                    void* stream) {
+    if (B < 0) return hg::kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
+    return hg::launch_rect_backward<hg::kAtenCpu>(src, tar, grad_H, B, scale, div, grad_src,
+                                                  grad_tar, grad_scale_div,
+                                                  reinterpret_cast<hipStream_t>(stream));
 }
 
 int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, int64_t B,
@@ -642,10 +654,20 @@ int hg_tensor_aca_rect_backward_order_f32(const float* src, const float* tar, co
     if (B == 0) return 0;
     if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
     if (scale_rows < 0 || scale_rows > 2 || div_rows < 0 || div_rows > 2) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    // one value each, with (B,3) terms side by side (or none): the one-value backward's staged
+    // form, which writes them as one (2,B,3) buffer
+    const bool uniform = !scale_sb && !scale_sr && !div_sb && !div_sr;
+    const bool paired = (!grad_scale && !grad_div) ||
+                        (grad_scale && grad_div == grad_scale + 3 * B && scale_rows == 2 &&
+                         div_rows == 2);
+    if (uniform && paired)
+        return hg::launch_rect_backward<hg::kAtenRocm>(src, tar, grad_H, B, scale, div, grad_src,
+                                                       grad_tar, grad_scale, s);
     const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
     return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel<hg::kAtenRocm>, hg::generic_grid(B),
-                      hg::kBlock, 0, reinterpret_cast<hipStream_t>(stream), src, tar, grad_H, B, a,
-                      grad_src, grad_tar, grad_scale, scale_rows, grad_div, div_rows);
+                      hg::kBlock, 0, s, src, tar, grad_H, B, a, grad_src, grad_tar, grad_scale,
+                      scale_rows, grad_div, div_rows);
 }
 
 int hg_tensor_aca_offsets_f32(const float* corner, const float* offsets, float* H, int64_t B,

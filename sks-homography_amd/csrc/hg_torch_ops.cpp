@@ -238,14 +238,22 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
     void* st = stream_of(tar);
     const int threads = aten_threads_of(aten_threads);
     const int order = order_of(order_);
-    if (order == HG_ORDER_ATEN_CPU && one_value(scale_) && one_value(div_)) {
+    if (one_value(scale_) && one_value(div_)) {
         at::Tensor part = need_scale_div ? at::empty({2, 3 * B}, tar.options()) : none;
-        hip_ok(hg_tensor_aca_rect_backward_f32(
-                   src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
-                   scale_.data_ptr<float>(), div_.data_ptr<float>(),
-                   need_src && B ? g_src.data_ptr<float>() : nullptr, g_tar.data_ptr<float>(),
-                   need_scale_div && B ? part.data_ptr<float>() : nullptr, st),
-               "hg_tensor_aca_rect_backward_f32");
+        float* gs = need_src && B ? g_src.data_ptr<float>() : nullptr;
+        float* pp = need_scale_div && B ? part.data_ptr<float>() : nullptr;
+        if (order == HG_ORDER_ATEN_CPU)
+            hip_ok(hg_tensor_aca_rect_backward_f32(
+                       src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+                       scale_.data_ptr<float>(), div_.data_ptr<float>(), gs,
+                       g_tar.data_ptr<float>(), pp, st),
+                   "hg_tensor_aca_rect_backward_f32");
+        else  // the same (2,B,3) terms, the (B,3) halves named apart
+            hip_ok(hg_tensor_aca_rect_backward_order_f32(
+                       src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+                       scale_.data_ptr<float>(), 0, 0, div_.data_ptr<float>(), 0, 0, gs,
+                       g_tar.data_ptr<float>(), pp, 2, pp ? pp + 3 * B : nullptr, 2, order, st),
+                   "hg_tensor_aca_rect_backward_order_f32");
         if (!need_scale_div) return {g_src, g_tar, none, none};
         // each half's (B,3) terms summed in ATen-CPU's order (two rows of one call)
         at::Tensor g_sd = at::empty({2}, tar.options());

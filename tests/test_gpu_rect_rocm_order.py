@@ -112,7 +112,16 @@ def test_backward_equals_torch_rocm_autograd(orc, pkg, dev, kind, shape):
     _, g_tar, g_sc, g_dv = pkg.tensor_aca_rect_backward(s, t, gH, sc, dv, False, True,
                                                          order="rocm")
     _same(orc, g_tar, tg.grad, f"dtar {kind} {shape}")
-    t2, s2_, d2_ = (x.clone().requires_grad_() for x in (t, sc, dv))
+    # unaligned views take the generic kernels (the aligned one-value case is the staged form)
+    su, tu = (torch.cat([x.reshape(-1), x.new_zeros(1)])[1:].view(B, 3, 4) for x in (s, t))
+    su.copy_(s)
+    tu.copy_(t)
+    _, g_tar_u, g_sc_u, g_dv_u = pkg.tensor_aca_rect_backward(su, tu, gH, sc, dv, True, True,
+                                                              order="rocm")
+    _same(orc, g_tar_u, tg.grad, f"dtar unaligned {kind} {shape}")
+    _same(orc, g_sc_u, g_sc, f"dscale unaligned {kind} {shape}")
+    _same(orc, g_dv_u, g_dv, f"ddiv unaligned {kind} {shape}")
+    t2, s2_, d2_ =(x.clone().requires_grad_() for x in (t, sc, dv))
     pkg.tensor_aca_rect_autograd(s, t2, s2_, d2_, order="rocm").backward(gH)
     _same(orc, t2.grad, tg.grad, f"autograd dtar {kind} {shape}")
     for got, via, want, name in ((g_sc, s2_.grad, sg.grad, "dscale"), (g_dv, d2_.grad, dg.grad, "ddiv")):
