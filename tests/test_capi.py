@@ -357,6 +357,34 @@ def test_pmc_traffic_matches_the_kernel_code():
     assert bench.pmc_traffic("aca_f32_aos_norm") is not None
 
 
+def test_pmc_families_name_built_kernels_and_match_their_code():
+    """Every kernel family tools/pmc_traffic.py reduces names kernels the built library holds
+    (a changed template signature -- a new parameter -- would otherwise drop the family from
+    the PMC summary without a word), and each family's recorded machine-code digest is the
+    built code's, so every `traffic` figure bench.py quotes belongs to the kernel it times."""
+    import json
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
+    sys.path.insert(0, os.path.join(ROOT, "tools"))
+    try:
+        import build_lib as bl
+        import pmc_traffic as pt
+    finally:
+        sys.path.pop(0)
+        sys.path.pop(0)
+    now = {k: bl.kernel_family_digest(prefix) for k, (prefix, _) in pt.KEYS.items()}
+    assert all(now.values()), [k for k, v in now.items() if not v]
+    with open(bench.PMC_TRAFFIC) as f:
+        rec = json.load(f)
+    measured_with = rec.get("provenance", {}).get("compiler")
+    if measured_with and measured_with != bl.compiler_id():
+        pytest.skip(f"PMC figures measured with another compiler ({measured_with})")
+    assert set(rec["detail"]) == set(pt.KEYS), set(pt.KEYS) ^ set(rec["detail"])
+    stale = {k: (rec["detail"][k].get("code"), now[k]) for k in pt.KEYS
+             if rec["detail"][k].get("code") != now[k]}
+    assert not stale, f"kernel code changed since the PMC run: {stale}"
+
+
 def test_kernel_code_digest_reads_the_headline_entry_points(pkg):
     """The digest finds exactly the two headline kernels' code in the gfx950 code objects of
     the built library, and it is a function of the code alone (stable across reads)."""
