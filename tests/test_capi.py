@@ -141,6 +141,25 @@ def test_other_entry_validation(pkg):
                                                      None, None, None, 0, None, 0, None) == 1
     assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
                                                None) == 1
+    # the evaluation-order entry points: HG_ORDER_ATEN_CPU (0) is the bcast form, ROCM (1) its
+    # own launch; anything else is refused before a pointer is looked at
+    for order in (0, 1):
+        assert lib.hg_tensor_aca_rect_order_f32(None, None, None, 0, None, 0, 0, None, 0, 0, order,
+                                                None) == 0
+        assert lib.hg_tensor_aca_rect_order_f32(None, None, None, -1, None, 0, 0, None, 0, 0, order,
+                                                None) == 1
+        assert lib.hg_tensor_aca_rect_order_f32(None, None, None, 4, None, 0, 0, None, 0, 0, order,
+                                                None) == 1
+        assert lib.hg_tensor_aca_rect_backward_order_f32(
+            None, None, None, 0, None, 0, 0, None, 0, 0, None, None, None, 0, None, 0, order, None) == 0
+        assert lib.hg_tensor_aca_rect_backward_order_f32(
+            None, None, None, 3, None, 0, 0, None, 0, 0, None, None, None, 0, None, 0, order, None) == 1
+        assert lib.hg_tensor_aca_rect_backward_order_f32(                           # scale mode 3
+            8, 8, 8, 3, 8, 0, 0, 8, 0, 0, None, 8, 8, 3, 8, 0, order, None) == 1
+    for order in (2, -1):
+        assert lib.hg_tensor_aca_rect_order_f32(16, 16, 16, 4, 16, 0, 0, 16, 0, 0, order, None) == 1
+        assert lib.hg_tensor_aca_rect_backward_order_f32(
+            16, 16, 16, 3, 16, 0, 0, 16, 0, 0, None, 16, None, 0, None, 0, order, None) == 1
     assert lib.hg_solve_one_f32(0, None, None, None, 1, None) == 1               # NULL points
     assert lib.hg_solve_one_f64(2, None, None, None, 1, None) == 1               # algo 2
     assert lib.hg_sum_rows_f32(None, -1, 5, None, None) == 1                      # rows < 0

@@ -126,6 +126,12 @@ def test_native_ops_pass_torch_opcheck(pkg, dev):
     torch.library.opcheck(ops.tensor_aca_offsets.default, (corner, offs_g, 128.0, 128.0),
                           test_utils=tests)
     torch.library.opcheck(ops.tensor_aca_rect.default, (src, tar_g, scale, div), test_utils=tests)
+    # the torch-ROCm evaluation order (int order=1), and its backward op with a per-problem scale
+    torch.library.opcheck(ops.tensor_aca_rect.default, (src, tar_g, scale, div, 1), test_utils=tests)
+    torch.library.opcheck(ops.tensor_aca_rect_backward.default,
+                          (src, tar, torch.randn(B, 3, 3, device=dev), torch.full((B, 1, 1), 128.0,
+                           device=dev), div, True, True, 0, 1),
+                          test_utils=("test_schema", "test_faketensor"))
     q = torch.rand(B, 4, 2, device=dev) * 100
     torch.library.opcheck(ops.aca.default, (q, q + 1.5, True),
                           test_utils=("test_schema", "test_faketensor"))
