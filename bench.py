@@ -116,10 +116,22 @@ def spawn_ranks(gpus: int, argv) -> int:
     print(f"bench.py: {' '.join(cmd[1:5])} ... (--gpus {gpus}, no WORLD_SIZE)", file=sys.stderr,
           flush=True)
     proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
-    for text in proc.stdout:
-        sys.stdout.write(text)
-        sys.stdout.flush()
-    return proc.wait()
+    # a SIGTERM / SIGINT / SIGHUP meant for this process (a driver's time limit) goes on to the
+    # child -- torch.distributed.run passes it to the ranks -- instead of leaving the ranks
+    # running on the GPUs without a parent; the child's exit then ends this process too
+    import signal
+    forwarded = (signal.SIGTERM, signal.SIGINT, signal.SIGHUP)
+    previous = {sig: signal.signal(sig, lambda signum, _f: proc.send_signal(signum))
+                for sig in forwarded}
+    try:
+        for text in proc.stdout:
+            sys.stdout.write(text)
+            sys.stdout.flush()
+        rc = proc.wait()
+    finally:
+        for sig, handler in previous.items():
+            signal.signal(sig, handler)
+    return 128 - rc if rc < 0 else rc  # a child ended by signal N exits 128 + N, as a shell reports
 
 
 def _kfd_gpu_bdfs(base: str = "/sys/class/kfd/kfd/topology/nodes"):

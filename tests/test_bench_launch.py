@@ -76,3 +76,54 @@ def test_refusal_exits_before_gpu(monkeypatch):
     with pytest.raises(SystemExit) as e:
         bench.main()
     assert e.value.code == 2
+
+
+def test_spawn_forwards_termination_to_the_ranks(tmp_path):
+    """A SIGTERM sent to bench.py's process alone (a driver's time limit) reaches the ranks it
+    started: they end instead of running on without a parent, and bench.py exits non-zero."""
+    import signal
+    import subprocess
+    import time
+    script = tmp_path / "rank.py"
+    script.write_text(textwrap.dedent(f"""
+        import os, time
+        open(os.path.join({str(tmp_path)!r}, "rank%s.pid" % os.environ["RANK"]), "w").write(str(os.getpid()))
+        time.sleep(120)
+    """))
+    driver = textwrap.dedent(f"""
+        import sys
+        sys.path.insert(0, {ROOT!r})
+        import bench
+        real = bench.torchrun_cmd
+        bench.torchrun_cmd = lambda n, argv, port: real(n, argv, port)[:-len(argv) - 1] + [{str(script)!r}, *argv]
+        sys.exit(bench.spawn_ranks(2, ["--gpus", "2"]))
+    """)
+    env = {k: v for k, v in os.environ.items() if k != "WORLD_SIZE"}
+    parent = subprocess.Popen([sys.executable, "-c", driver], env=env, stdout=subprocess.DEVNULL,
+                              stderr=subprocess.DEVNULL)
+    pids = []
+    try:
+        deadline = time.time() + 90
+        while time.time() < deadline and len(pids) < 2:
+            pids = [int(p.read_text()) for p in tmp_path.glob("rank*.pid") if p.read_text()]
+            time.sleep(0.2)
+        assert len(pids) == 2, "the ranks did not start"
+        parent.send_signal(signal.SIGTERM)
+        rc = parent.wait(timeout=60)
+        assert rc != 0
+        deadline = time.time() + 30
+        alive = pids
+        while time.time() < deadline and alive:
+            alive = [p for p in pids if os.path.exists(f"/proc/{p}") and
+                     "Z" not in open(f"/proc/{p}/stat").read().split(")")[-1].split()[:1]]
+            time.sleep(0.2)
+        assert not alive, f"ranks {alive} outlived bench.py"
+    finally:
+        if parent.poll() is None:
+            parent.kill()
+            parent.wait()
+        for p in pids:
+            try:
+                os.kill(p, signal.SIGKILL)
+            except (ProcessLookupError, PermissionError):
+                pass
