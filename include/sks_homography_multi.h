@@ -9,9 +9,11 @@
  *
  * Library: sks-homography_amd/lib/libsks_homography_multi.so (links the product library and
  * librccl; the product library itself has no RCCL dependency).  Every call is asynchronous on
- * the shards' streams unless it says otherwise, and returns 0 or a hipError_t / ncclResult_t
- * code (hipErrorInvalidValue = 1 for a bad argument).  N > 1 GPUs: correct by construction
- * and unmeasured on hardware (the build box has one GPU).
+ * the shards' streams unless it says otherwise, and returns 0, a hipError_t code
+ * (hipErrorInvalidValue = 1 for a bad argument), or HG_ERR_RCCL_BASE + an ncclResult_t when
+ * RCCL itself failed (the two code spaces overlap, so RCCL's are moved apart: HG_IS_RCCL_ERR /
+ * HG_RCCL_RESULT recover it).  N > 1 GPUs: correct by construction and unmeasured on hardware
+ * (the build box has one GPU).
  */
 #ifndef SKS_HOMOGRAPHY_MULTI_H_
 #define SKS_HOMOGRAPHY_MULTI_H_
@@ -24,6 +26,10 @@ extern "C" {
 
 #define HG_DTYPE_F32 0
 #define HG_DTYPE_F64 1
+
+#define HG_ERR_RCCL_BASE 0x10000
+#define HG_IS_RCCL_ERR(rc) ((rc) >= HG_ERR_RCCL_BASE)
+#define HG_RCCL_RESULT(rc) ((rc) - HG_ERR_RCCL_BASE)
 
 /* One GPU's block of a batch: device memory on `device` (src, tar, H in `layout`, n problems,
  * the same contracts as hg_<algo>_<dtype>) and a stream on that device (NULL = its null

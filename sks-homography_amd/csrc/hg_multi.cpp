@@ -16,6 +16,9 @@ namespace {
 
 constexpr int kErrInvalid = (int)hipErrorInvalidValue;
 
+// an RCCL failure, apart from the hipError_t codes (sks_homography_multi.h)
+int rccl_err(ncclResult_t r) { return r == ncclSuccess ? 0 : HG_ERR_RCCL_BASE + (int)r; }
+
 // Sets `device` current for the scope; the caller's device comes back on exit.
 class DeviceScope {
    public:
@@ -96,7 +99,7 @@ int hg_comm_init_all(int ndev, const int* devices, void** comms) {
     if (ndev < 1 || !devices || !comms) return kErrInvalid;
     std::vector<ncclComm_t> c(ndev);
     const ncclResult_t r = ncclCommInitAll(c.data(), ndev, devices);
-    if (r != ncclSuccess) return (int)r;
+    if (r != ncclSuccess) return rccl_err(r);
     for (int i = 0; i < ndev; ++i) comms[i] = c[i];
     return 0;
 }
@@ -107,7 +110,7 @@ int hg_comm_destroy(int ndev, void** comms) {
     for (int i = 0; i < ndev; ++i) {
         if (!comms[i]) continue;
         const ncclResult_t r = ncclCommDestroy(static_cast<ncclComm_t>(comms[i]));
-        if (r != ncclSuccess && !first) first = (int)r;
+        if (r != ncclSuccess && !first) first = rccl_err(r);
         comms[i] = nullptr;
     }
     return first;
@@ -136,7 +139,7 @@ int hg_gather_multi(const hg_device_batch* shards, int ndev, int root, int dtype
     }
     if (ndev == 1) return 0;
     ncclResult_t r = ncclGroupStart();
-    if (r != ncclSuccess) return (int)r;
+    if (r != ncclSuccess) return rccl_err(r);
     int first = 0;
     for (int i = 0; i < ndev && !first; ++i) {
         if (i == root || shards[i].n == 0) continue;
@@ -146,10 +149,10 @@ int hg_gather_multi(const hg_device_batch* shards, int ndev, int root, int dtype
         if (r == ncclSuccess)
             r = ncclRecv(dst + lo[i] * row, bytes, ncclUint8, i, static_cast<ncclComm_t>(comms[root]),
                          static_cast<hipStream_t>(rb.stream));
-        if (r != ncclSuccess) first = (int)r;
+        if (r != ncclSuccess) first = rccl_err(r);
     }
     r = ncclGroupEnd();  // always closed, so a failed enqueue leaves no open group behind
-    return first ? first : (int)r;
+    return first ? first : rccl_err(r);
 }
 
 }  // extern "C"

@@ -63,3 +63,17 @@ def test_argument_checks_before_any_hip_call(pkg, multi):
     assert multi.hg_comm_init_all(0, None, comms) == 1
     assert multi.hg_comm_destroy(0, comms) == 1
     assert multi.hg_comm_destroy(2, comms) == 0                    # NULL handles: nothing to free
+
+
+def test_rccl_failures_have_their_own_codes(multi):
+    """RCCL's ncclResult_t codes overlap hipError_t's (1 is both hipErrorInvalidValue and
+    ncclUnhandledCudaError), so the multi ABI returns them as HG_ERR_RCCL_BASE + result.  With
+    no GPU in this container, communicator set-up fails inside RCCL and says so."""
+    import torch
+    if torch.cuda.device_count() > 0:  # counts devices without initialising the runtime
+        pytest.skip("a GPU is present: communicator set-up would succeed")
+    devs = (ctypes.c_int * 1)(0)
+    comms = (ctypes.c_void_p * 1)()
+    rc = multi.hg_comm_init_all(1, devs, comms)
+    assert rc >= 0x10000 and rc - 0x10000 > 0, hex(rc)  # HG_IS_RCCL_ERR, an ncclResult_t != 0
+    assert comms[0] is None
