@@ -329,7 +329,8 @@ int hg_solve_grouped_f64(int algo, const double* const* src, const double* const
 /* Deterministic sums of the rows of x (rows, cols), row-major, into out[rows]: a fixed
  * two-level order (chunks of 4096 in order, folded by halving strides), so the bits do
  * not depend on timing.  x is OVERWRITTEN (used as the scratch for the chunk sums).
- * rows <= 65535.  Reduces hg_tensor_aca_rect_backward_f32's (2,B) partials. */
+ * rows <= 65535.  A general deterministic row sum; the TensorACA gradient terms take
+ * hg_sum_aten_f32 (ATen's own order) since round 4, when this stopped being their reduction. */
 int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stream);
 
 /* Sums in ATen-CPU's float32 order (SumKernel.cpp cascade_sum under TensorIterator's

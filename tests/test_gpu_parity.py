@@ -645,7 +645,8 @@ def _sum_rows_restated(x):
 @pytest.mark.parametrize("rows,cols", [(1, 0), (2, 1), (2, 4095), (2, 4096), (2, 4097),
                                        (3, (1 << 20) + 3), (2, 2_000_000)])
 def test_sum_rows_fixed_order(orc, pkg, dev, rows, cols):
-    """hg_sum_rows_f32 (the reduction of the TensorACA scale/div gradient partials) is
+    """hg_sum_rows_f32 (a general row sum in the C ABI; until round 4 the reduction of the
+    TensorACA scale/div gradient terms, hg_sum_aten_f32's job since) is
     bit-identical to its numpy restatement and to itself across runs."""
     g = torch.Generator(device=dev).manual_seed(cols)
     x = torch.randn(rows, cols, device=dev, generator=g) * 100
