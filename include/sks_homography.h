@@ -345,6 +345,27 @@ int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stre
 int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
                     int lanes, int threads, float* out, void* stream);
 
+/* Sums in ATen-ROCm's float32 GPU order: torch.sum / at::sum_to of a contiguous (B,3,1)
+ * float tensor x -- over {0,1} to out[1] (HG_SUM_ROCM_FULL: a (1,) parameter's gradient) or
+ * over {0} to out[3] (HG_SUM_ROCM_COLS: a (3,1) one) -- with the bits torch-ROCm 2.10 gives
+ * on the current device (its CU count and threads per CU pick the launch shape, as ATen's do;
+ * restated in oracle/aten_rocm_sum.py, pinned against torch.sum on the MI355X).  How
+ * torch-ROCm's autograd reduces TensorACA_rect's batch-uniform scale / div gradient terms
+ * (HG_ORDER_ATEN_ROCM).  x is not modified; any alignment, summed in the order ATen gives an
+ * aligned tensor (its fresh allocations are); workspace: HG_SUM_ROCM_WORKSPACE
+ * device floats, needed when the sum spans several blocks (FULL from B ~ 43K; never COLS).
+ * B = 0 writes +0. */
+#define HG_SUM_ROCM_FULL 0
+#define HG_SUM_ROCM_COLS 1
+#define HG_SUM_ROCM_WORKSPACE 1024
+int hg_sum_rocm_f32(const float* x, int64_t B, int kind, float* out, float* workspace,
+                    void* stream);
+/* The launch shape hg_sum_rocm_f32 takes for B >= 2 on a device with num_mp CUs and max_tpm
+ * threads per CU (a host computation, no GPU): plan[12] = block x, block y, CTAs per output,
+ * input splits x / y / CTA, output splits x / y, input step, output step, loads of 4, grid x.
+ * For tests and tools (against oracle/aten_rocm_sum.py's Config). */
+int hg_sum_rocm_plan(int64_t B, int kind, int num_mp, int max_tpm, int64_t* plan);
+
 /* Device-to-device streaming copy (float4) used by bench.py as the measured
  * achievable-bandwidth yardstick.  bytes must be a multiple of 16. */
 int hg_stream_copy(const void* src, void* dst, int64_t bytes, void* stream);

@@ -45,6 +45,8 @@ SIGNATURES = {
     "hg_tensor_aca_rect_backward_order_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,
                                                _i64, _vp, _vp, _vp, _int, _vp, _int, _int, _vp],
                                               _int),
+    "hg_sum_rocm_f32": ([_vp, _i64, _int, _vp, _vp, _vp], _int),
+    "hg_sum_rocm_plan": ([_i64, _int, _int, _int, _vp], _int),
     "hg_tensor_aca_offsets_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float, _vp],
                                   _int),
     "hg_tensor_aca_offsets_backward_f32": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,

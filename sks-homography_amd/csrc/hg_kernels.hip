@@ -799,6 +799,123 @@ int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stre
     return hg::launch(hg::sum_rows_pass2, (unsigned)rows, hg::kBlock, 0, s, x, cols, chunks, out);
 }
 
+}  // extern "C"
+
+namespace hg {
+// ATen's setReduceConfig (ATen/native/hip/Reduce.cuh, torch 2.10) for the two iterators
+// at::sum_to builds from a contiguous (B,3,1) float tensor: kind 0 -- one dimension of 3B
+// reduced to one output; kind 1 (B >= 2) -- B reduced (stride 3) for each of 3 outputs.
+// Restated in oracle/aten_rocm_sum.py's Config, which the fixture pins.
+inline int64_t rocm_last_pow2(int64_t n) {
+    if (n <= 1) return 1;
+    int64_t p = 1;
+    while (p <= n / 2) p <<= 1;
+    return p;
+}
+
+inline RocmSum rocm_sum_config(const float* x, int64_t B, int kind, int num_mp, int max_tpm) {
+    RocmSum a{};
+    a.x = x;
+    const bool fastest = kind == 0;
+    int64_t dim0, dim1;
+    if (fastest) {
+        a.num_in = 3 * B;
+        a.num_out = 1;
+        a.in_stride = 1;
+        a.out_stride = 0;
+        dim0 = a.num_in;
+        dim1 = 1;
+        a.vec = dim0 >= 128;
+        if (a.vec) dim0 /= 4;
+    } else {
+        a.num_in = B;
+        a.num_out = 3;
+        a.in_stride = 3;
+        a.out_stride = 1;
+        dim0 = 3;  // output vectors: 3 outputs give a vector size of 1
+        dim1 = B;
+        a.vec = 0;
+    }
+    const int64_t d0 = dim0 < kRocmSumThreads ? rocm_last_pow2(dim0) : kRocmSumThreads;
+    const int64_t d1 = dim1 < kRocmSumThreads ? rocm_last_pow2(dim1) : kRocmSumThreads;
+    int64_t bw = d0 < kWave ? d0 : kWave;
+    const int64_t bh = d1 < kRocmSumThreads / bw ? d1 : kRocmSumThreads / bw;
+    bw = d0 < kRocmSumThreads / bh ? d0 : kRocmSumThreads / bh;
+    a.bw = (int)bw;
+    a.bh = (int)bh;
+    a.step_in = a.step_out = 1;
+    auto split_in = [&](int64_t p) { const int64_t s0 = a.step_in; a.step_in *= p; return s0; };
+    auto split_out = [&](int64_t p) { const int64_t s0 = a.step_out; a.step_out *= p; return s0; };
+    if (fastest) a.in_mult[0] = split_in(bw);
+    else a.out_mult[0] = split_out(bw);
+    const int64_t thr = bh * 16 < 256 ? bh * 16 : 256;
+    if (ceil_div(a.num_in, a.step_in) >= thr) a.in_mult[1] = split_in(bh);  // 256 CUs: no
+    else a.out_mult[1] = split_out(bh);                                     // forced output split
+    a.ctas = 1;
+    const int64_t gx = ceil_div((int64_t)a.num_out, a.step_out);
+    int tpm = max_tpm;
+    if (gx != 1) tpm = fastest ? 512 : 256;  // ATen's `grid().x == grid().y == grid().z == 1`
+    const int64_t target = (int64_t)num_mp * (tpm / (bw * bh));
+    const int64_t vpt = ceil_div(a.num_in, a.step_in);
+    if (a.in_mult[1] != 0 && vpt >= 256 && gx <= target) {
+        const int64_t c1 = ceil_div(target, gx), c2 = ceil_div(vpt, (int64_t)16);
+        const int64_t c3 = ceil_div(vpt, (int64_t)256);
+        int64_t c = c1 < c2 ? c1 : c2;
+        c = c > c3 ? c : c3;
+        if (c > num_mp) c = num_mp < 128 ? (int64_t)num_mp * (c > 512 ? 4 : 2) : num_mp;
+        else if (c > ceil_div((int64_t)num_mp, (int64_t)2)) c = ceil_div((int64_t)num_mp, (int64_t)2);
+        else if (c < 16) c = 1;
+        a.ctas = (int)c;
+        if (c > 1) a.in_mult[2] = split_in(c);
+    }
+    return a;
+}
+}  // namespace hg
+
+extern "C" {
+
+int hg_sum_rocm_plan(int64_t B, int kind, int num_mp, int max_tpm, int64_t* plan) {
+    if (B < 2 || (kind != HG_SUM_ROCM_FULL && kind != HG_SUM_ROCM_COLS) || num_mp < 1 ||
+        max_tpm < 1 || !plan)
+        return hg::kErrInvalid;
+    const hg::RocmSum a = hg::rocm_sum_config(nullptr, B, kind, num_mp, max_tpm);
+    const int64_t v[12] = {a.bw, a.bh, a.ctas, a.in_mult[0], a.in_mult[1], a.in_mult[2],
+                           a.out_mult[0], a.out_mult[1], a.step_in, a.step_out, a.vec,
+                           hg::ceil_div((int64_t)a.num_out, a.step_out)};
+    for (int i = 0; i < 12; ++i) plan[i] = v[i];
+    return 0;
+}
+
+int hg_sum_rocm_f32(const float* x, int64_t B, int kind, float* out, float* workspace,
+                    void* stream) {
+    if (B < 0 || (kind != HG_SUM_ROCM_FULL && kind != HG_SUM_ROCM_COLS) || !out)
+        return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    const int nout = kind == HG_SUM_ROCM_FULL ? 1 : 3;
+    if (B == 0) return (int)hipMemsetAsync(out, 0, nout * sizeof(float), s);  // sums of nothing: +0
+    if (!x) return hg::kErrInvalid;
+    if (kind == HG_SUM_ROCM_COLS && B == 1)
+        return hg::launch(hg::rocm_sum_single_kernel, 1u, 64u, 0, s, x, out);
+    if (3 * B > 0x7fffffffLL) return hg::kErrInvalid;  // ATen splits beyond 32-bit indexing
+    int dev = 0, num_mp = 0, max_tpm = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&num_mp, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        hipDeviceGetAttribute(&max_tpm, hipDeviceAttributeMaxThreadsPerMultiProcessor, dev) !=
+            hipSuccess)
+        return (int)hipErrorInvalidDevice;
+    hg::RocmSum a = hg::rocm_sum_config(x, B, kind, num_mp, max_tpm);
+    a.aligned = hg::aligned16(x);
+    if (a.ctas > hg::kRocmSumMaxCtas) return hg::kErrInvalid;
+    const dim3 block((unsigned)a.bw, (unsigned)a.bh);
+    const dim3 grid((unsigned)hg::ceil_div((int64_t)a.num_out, a.step_out), (unsigned)a.ctas);
+    if (a.ctas == 1) return hg::launch(hg::rocm_sum_kernel, grid, block, 0, s, a, out);
+    if (!workspace) return hg::kErrInvalid;
+    const int rc = hg::launch(hg::rocm_sum_kernel, grid, block, 0, s, a, workspace);
+    if (rc) return rc;
+    return hg::launch(hg::rocm_sum_final_kernel, dim3(1), block, 0, s, a,
+                      static_cast<const float*>(workspace), out);
+}
+
 int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
                     int lanes, int threads, float* out, void* stream) {
     if (rows < 0 || m < 0 || lanes < 1 || lanes > hg::kAtenMaxLanes || threads < 1 ||

@@ -241,4 +241,142 @@ __global__ __launch_bounds__(64) void aten_sum_l4(AtenSum a, int threads, int la
     out[row] = 0.f + final_acc;
 }
 
+// ---------------------------------------------------------------------------------------------
+// hg_sum_rocm_f32: a float32 sum in ATen-ROCm's GPU order -- torch.sum / at::sum_to of a
+// contiguous (B,3,1) tensor over {0,1} (to a (1,) parameter: kind 0) or over {0} (to (3,1):
+// kind 1), as torch-ROCm's autograd reduces TensorACA_rect's batch-uniform scale / div
+// gradients in the reference's device='cuda' run (Modules_Runtime_Test.py:301-302, :393).
+// Restated from torch 2.10's ATen/native/hip/Reduce.cuh (float sum: four accumulators, loads
+// of 4 along a contiguous reduced dimension, 512-thread blocks) and pinned by
+// oracle/aten_rocm_sum.py against torch.sum on this GPU (tests/golden/rocm_sum.npz):
+//   * the launch shape (block bw x bh, the input / output splits, the CTA split from the
+//     device's CU count and threads per CU) is chosen on the host exactly as ATen chooses it;
+//   * each thread sums its strided share into four accumulators, folded ((a0+a1)+a2)+a3;
+//   * the block folds x by halving through LDS down to the wave, then the wave tree ROCm's
+//     ATen uses (offsets 1, 2, 4, ... through shfl_down), and y by halving through LDS;
+//   * with several CTAs per output their partials are summed from 0 by one block's threads
+//     (partial t, t + nt, ...) and folded by the same trees -- ATen's last-block pass, made a
+//     second launch here (same additions, no semaphore).
+struct RocmSum {
+    const float* x;
+    int64_t num_in;            // inputs per output
+    int num_out;               // 1 or 3
+    int in_stride, out_stride; // element strides: along the reduction, between outputs
+    int bw, bh, ctas;
+    int64_t in_mult[3], out_mult[2], step_in, step_out;
+    int vec;                   // groups of 4 along a contiguous reduction
+    int aligned;               // x 16-B aligned: each group one 16-B load (else four)
+};
+
+constexpr int kRocmSumThreads = 512;
+constexpr int kRocmSumMaxCtas = 1024;
+
+// the block trees over v (thread x + y bw); returns the folded value (meaningful where ATen
+// stores it: x == 0 after the x tree, y == 0 after the y tree)
+__device__ __forceinline__ float rocm_block_x(float v, float* s, int bw) {
+    const int x = threadIdx.x, t = threadIdx.x + threadIdx.y * bw;
+    int dim = bw;
+    if (dim > kWave) {
+        s[t] = v;
+        for (int off = dim / 2; off >= kWave; off >>= 1) {
+            __syncthreads();
+            if (x < off && x + off < bw) {
+                v = v + s[t + off];
+                s[t] = v;
+            }
+        }
+        dim = kWave;
+    }
+    __syncthreads();
+    for (int off = 1; off < dim; off <<= 1) v = v + __shfl_down(v, off);
+    return v;
+}
+
+__device__ __forceinline__ float rocm_block_y(float v, float* s, int bw, int bh) {
+    const int x = threadIdx.x, y = threadIdx.y;
+    s[x + y * bw] = v;
+    for (int off = bh / 2; off > 0; off >>= 1) {
+        __syncthreads();
+        if (y < off && y + off < bh) {
+            v = v + s[x + (y + off) * bw];
+            s[x + y * bw] = v;
+        }
+    }
+    return v;
+}
+
+// grid (outputs / step_out, ctas), block (bw, bh).  out: the outputs, or (ctas > 1) the CTA
+// partials, partial c of the run at out[c].
+__global__ __launch_bounds__(kRocmSumThreads) void rocm_sum_kernel(RocmSum a, float* __restrict__ out) {
+    __shared__ float s[kRocmSumThreads];
+    const int x = threadIdx.x, y = threadIdx.y;
+    const int64_t o = x * a.out_mult[0] + y * a.out_mult[1] + (int64_t)blockIdx.x * a.step_out;
+    const int64_t i0 = x * a.in_mult[0] + y * a.in_mult[1] + (int64_t)blockIdx.y * a.in_mult[2];
+    float v = 0.f;
+    if (o < a.num_out && i0 < a.num_in) {
+        const float* base = a.x + o * a.out_stride;
+        const int64_t end = a.num_in, stride = a.step_in;
+        float acc[4] = {0.f, 0.f, 0.f, 0.f};
+        if (a.vec) {  // contiguous (in_stride 1): element 4 i + k into acc[k] -- the order ATen
+                      // gives an aligned tensor, whatever x's own alignment
+            for (int64_t i = i0; i * 4 + 3 < end; i += stride) {
+                float4 q;
+                if (a.aligned) {
+                    q = reinterpret_cast<const float4*>(base)[i];
+                } else {
+                    q = float4(base[4 * i], base[4 * i + 1], base[4 * i + 2], base[4 * i + 3]);
+                }
+                acc[0] = acc[0] + q.x;
+                acc[1] = acc[1] + q.y;
+                acc[2] = acc[2] + q.z;
+                acc[3] = acc[3] + q.w;
+            }
+            const bool tail = (a.in_mult[1] == 0 || y == 0) && (a.in_mult[2] == 0 || blockIdx.y == 0);
+            const int64_t e = end - end % 4 + x;
+            if (tail && e < end) acc[0] = acc[0] + base[e];
+        } else {
+            int64_t i = i0;
+            for (; i + 3 * stride < end; i += 4 * stride) {
+                float q[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) q[k] = base[(i + k * stride) * a.in_stride];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = acc[k] + q[k];
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (i >= end) break;
+                acc[k] = acc[k] + base[i * a.in_stride];
+                i += stride;
+            }
+        }
+        v = ((acc[0] + acc[1]) + acc[2]) + acc[3];
+    }
+    if (a.in_mult[0] != 0) v = rocm_block_x(v, s, a.bw);
+    if (a.in_mult[1] != 0) v = rocm_block_y(v, s, a.bw, a.bh);
+    const bool store = o < a.num_out && (a.in_mult[0] == 0 || x == 0) && (a.in_mult[1] == 0 || y == 0);
+    if (!store) return;
+    if (a.in_mult[2] != 0) out[blockIdx.y] = v;  // this CTA's partial (one output: the x tree ran)
+    else out[o] = v;
+}
+
+// The CTA partials of the one output: thread t sums partials t, t + nt, ... from 0, then the
+// y and x trees (ATen's last-block pass).
+__global__ __launch_bounds__(kRocmSumThreads) void rocm_sum_final_kernel(RocmSum a,
+                                                                         const float* __restrict__ part,
+                                                                         float* __restrict__ out) {
+    __shared__ float s[kRocmSumThreads];
+    const int nt = a.bw * a.bh, t = threadIdx.x + threadIdx.y * a.bw;
+    float v = 0.f;
+    for (int c = t; c < a.ctas; c += nt) v = v + part[c];
+    v = rocm_block_y(v, s, a.bw, a.bh);
+    v = rocm_block_x(v, s, a.bw);
+    if (t == 0) out[0] = v;
+}
+
+// B = 1 to (3,1): the reduced dimension has one element: 0 + x (the accumulator's +0)
+__global__ void rocm_sum_single_kernel(const float* __restrict__ x, float* __restrict__ out) {
+    if (threadIdx.x < 3) out[threadIdx.x] = 0.f + x[threadIdx.x];
+}
+
 }  // namespace hg

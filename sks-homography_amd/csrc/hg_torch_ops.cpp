@@ -195,13 +195,32 @@ int terms_mode(const Bcast& b) {
     return b.over_r ? 1 : 2;
 }
 
+// In torch-ROCm's order a batch-reduced parameter's terms are always laid out as the (B,3,1)
+// tensor autograd reduces (mode 2), since ROCm's reduction tree depends on that layout.
+int terms_mode_for(const Bcast& b, int order) {
+    return order == HG_ORDER_ATEN_ROCM && !b.over_b ? 2 : terms_mode(b);
+}
+
+// A batch-wide sum of (B,3) terms in torch-ROCm's GPU order (hg_sum_rocm_f32): at::sum_to of
+// the (B,3,1) tensor to a (1,) parameter (cols = false) or a (3,1) one (cols = true).
+at::Tensor rocm_batch_sum(const at::Tensor& terms, int64_t B, bool cols, void* stream) {
+    at::Tensor g = at::empty({cols ? 3 : 1}, terms.options());
+    at::Tensor ws = !cols && B > 0 ? at::empty({HG_SUM_ROCM_WORKSPACE}, terms.options()) : g;
+    hip_ok(hg_sum_rocm_f32(terms.data_ptr<float>(), B, cols ? HG_SUM_ROCM_COLS : HG_SUM_ROCM_FULL,
+                           g.data_ptr<float>(), ws.data_ptr<float>(), stream),
+           "hg_sum_rocm_f32");
+    return g;
+}
+
 // A parameter's gradient from the kernel's terms: summed over the dimensions it was
-// broadcast along in ATen-CPU's order, and shaped like the parameter.
+// broadcast along in the evaluation order asked for, and shaped like the parameter.
 at::Tensor reduce_param_grad(at::Tensor part, const Bcast& b, const at::Tensor& param, int64_t B,
-                             int threads, void* stream) {
+                             int threads, int order, void* stream) {
     if (b.over_b && b.over_r)  // (3,B) -> (B,3)
         return part.view({3, B}).t().contiguous().reshape(param.sizes());
-    if (b.over_b) return part.reshape(param.sizes());  // (B): ATen's per-problem three-row sums
+    if (b.over_b) return part.reshape(param.sizes());  // (B): the per-problem three-row sums
+    if (order == HG_ORDER_ATEN_ROCM)  // (B,3) terms
+        return rocm_batch_sum(part, B, b.over_r, stream).reshape(param.sizes());
     at::Tensor g = at::empty({b.over_r ? 3 : 1}, part.options());
     // (3,1): each (3,B) row as ATen sums a strided column (one lane, no threads); one value:
     // the (B,3) terms as one run
@@ -255,6 +274,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
                        g_tar.data_ptr<float>(), pp, 2, pp ? pp + 3 * B : nullptr, 2, order, st),
                    "hg_tensor_aca_rect_backward_order_f32");
         if (!need_scale_div) return {g_src, g_tar, none, none};
+        if (order == HG_ORDER_ATEN_ROCM)  // each half as torch-ROCm's autograd sums it
+            return {g_src, g_tar,
+                    rocm_batch_sum(part[0], B, false, st).reshape(scale_.sizes()),
+                    rocm_batch_sum(part[1], B, false, st).reshape(div_.sizes())};
         // each half's (B,3) terms summed in ATen-CPU's order (two rows of one call)
         at::Tensor g_sd = at::empty({2}, tar.options());
         hip_ok(hg_sum_aten_f32(part.data_ptr<float>(), 2, 3 * B, 3 * B, 1, kAtenLanes, threads,
@@ -263,10 +286,10 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
         return {g_src, g_tar, g_sd.slice(0, 0, 1).reshape(scale_.sizes()),
                 g_sd.slice(0, 1, 2).reshape(div_.sizes())};
     }
-    // each parameter's terms in the layout its reduction reads (terms_mode); in ROCm order the
-    // per-problem three-row sums follow the GPU's ((0 + t0) + t2) + t1 and the batch sums stay
-    // ATen-CPU's (ROCm's reduction tree is not restated: include/sks_homography.h)
-    const int ms = terms_mode(sb), md = terms_mode(db);
+    // each parameter's terms in the layout its reduction reads (terms_mode_for); in ROCm order
+    // the per-problem three-row sums follow the GPU's ((0 + t0) + t2) + t1 and the batch sums
+    // its reduction tree (hg_sum_rocm_f32)
+    const int ms = terms_mode_for(sb, order), md = terms_mode_for(db, order);
     at::Tensor ps = need_scale_div ? at::empty({ms ? 3 * B : B}, tar.options()) : none;
     at::Tensor pd = need_scale_div ? at::empty({md ? 3 * B : B}, tar.options()) : none;
     hip_ok(hg_tensor_aca_rect_backward_order_f32(
@@ -277,8 +300,8 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
                need_scale_div && B ? pd.data_ptr<float>() : nullptr, md, order, st),
            "hg_tensor_aca_rect_backward_order_f32");
     if (!need_scale_div) return {g_src, g_tar, none, none};
-    return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, threads, st),
-            reduce_param_grad(pd, db, div_, B, threads, st)};
+    return {g_src, g_tar, reduce_param_grad(ps, sb, scale_, B, threads, order, st),
+            reduce_param_grad(pd, db, div_, B, threads, order, st)};
 }
 
 // ------------------------------------------------------------------ compact offsets form

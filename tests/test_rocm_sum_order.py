@@ -58,3 +58,28 @@ def test_signed_zero_sums_start_from_plus_zero():
         t = -np.zeros((1000, 3), np.float32)
         r = ars.rocm_sum(t, kind, 256, 2048)
         assert (r.view(np.uint32) == 0).all()
+
+
+def test_library_plans_the_restated_launch(pkg):
+    """hg_sum_rocm_plan (the C++ host side of hg_sum_rocm_f32) picks ATen's launch shape --
+    the restatement's Config -- for every B from 2 to 5000 and a spread beyond, on this GPU's
+    (256 CUs, 2048 threads per CU) and on other CU counts."""
+    import ctypes
+    lib = pkg.lib()
+    plan = (ctypes.c_int64 * 12)()
+    sizes = list(range(2, 5001)) + [10922, 10923, 43690, 43691, 65536, 100003, 174762, 174763,
+                                     262144, 1 << 20, 3_000_001, 1 << 24, 700_000_000]
+    for num_mp, max_tpm in ((256, 2048), (304, 2048), (120, 2048), (80, 2048), (64, 1024)):
+        for kind_i, kind in ((0, "full"), (1, "cols")):
+            for B in sizes if num_mp == 256 else sizes[::37]:
+                assert lib.hg_sum_rocm_plan(B, kind_i, num_mp, max_tpm, plan) == 0
+                c = ars.Config(kind, B, num_mp, max_tpm)
+                want = (c.bw, c.bh, c.ctas, *c.input_mult, *c.output_mult, c.step_input,
+                        c.step_output, int(c.vectorize), c.grid_x)
+                assert tuple(plan) == want, (kind, B, num_mp, tuple(plan), want)
+    assert lib.hg_sum_rocm_plan(1, 0, 256, 2048, plan) == 1
+    assert lib.hg_sum_rocm_plan(5, 2, 256, 2048, plan) == 1
+    assert lib.hg_sum_rocm_f32(None, 0, 0, None, None, None) == 1       # NULL out
+    assert lib.hg_sum_rocm_f32(None, 5, 3, 16, None, None) == 1         # kind
+    assert lib.hg_sum_rocm_f32(None, -1, 0, 16, None, None) == 1        # B < 0
+    assert lib.hg_sum_rocm_f32(None, 5, 0, 16, None, None) == 1         # NULL x
