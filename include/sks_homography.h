@@ -145,8 +145,9 @@ int hg_tensor_aca_rect_bcast_backward_f32(const float* src, const float* tar, co
 /* hg_tensor_aca_rect_bcast_f32 / its backward with the evaluation order `order`
  * (HG_ORDER_*); strides 0 / 0 give the batch-uniform (1,) scale / div.  HG_ORDER_ATEN_CPU
  * is exactly the bcast entry points.  The backward's per-parameter modes are theirs, and
- * modes 1 / 2 leave the batch sums to the caller (hg_sum_aten_f32 is ATen-CPU's order; the
- * GPU run's batch sums follow ROCm's reduction tree, which is not restated here). */
+ * modes 1 / 2 leave the batch sums to the caller: hg_sum_aten_f32 for ATen-CPU's order,
+ * hg_sum_rocm_f32 on mode-2 (B,3) terms for the GPU run's (its reduction tree needs that
+ * layout, for a (3,1) parameter too). */
 int hg_tensor_aca_rect_order_f32(const float* src, const float* tar, float* H, int64_t B,
                                  const float* scale, int64_t scale_sb, int64_t scale_sr,
                                  const float* div, int64_t div_sb, int64_t div_sr, int order,

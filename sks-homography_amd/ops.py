@@ -278,11 +278,11 @@ def tensor_aca_rect(src: torch.Tensor, tar: torch.Tensor, scale: Scalar, div: Sc
     bit for bit, as the golden fixtures pin.  "rocm" -- as torch-ROCm evaluates them on the
     GPU, the reference's own default run (Modules_Runtime_Test.py:393, device='cuda'): every
     three-term sum, forward and backward, is ((0 + t0) + t2) + t1
-    (profiles/r04/rocm_grad_probe_r04j.json); H, dL/dtar, dL/dsrc and per-problem
-    dL/dscale, dL/ddiv then equal that run's bits.  Batch sums of a (1,) / (3,1) scale or
-    div gradient stay in ATen-CPU's order in both modes (ROCm's reduction tree is not
-    restated).  The two orders differ by ~1e-5 relative on fractional inputs and agree
-    exactly on the reference's integer batches.
+    (profiles/r04/rocm_grad_probe_r04j.json), and a (1,) / (3,1) scale or div gradient is
+    summed over the batch in ATen-ROCm's reduction order (hg_sum_rocm_f32); H, dL/dtar and
+    dL/dscale, dL/ddiv of every shape then equal that run's bits (dL/dsrc, which the
+    reference cannot take, follows the same sums).  The two orders differ by ~1e-5 relative
+    on fractional inputs and agree exactly on the reference's integer batches.
     """
     _gpu_only(tar)  # the op checks that src (and out) share tar's device
     o = _order(order)
