@@ -44,18 +44,22 @@ def adjust(device, bs: int):
     return src, tar, src_h, tar_h, scale, div
 
 
-def TensorACA_rect(bs: int, src: torch.Tensor, tar: torch.Tensor, scale, div) -> torch.Tensor:
+def TensorACA_rect(bs: int, src: torch.Tensor, tar: torch.Tensor, scale, div, *,
+                   order: str = "cpu") -> torch.Tensor:
     """TensorACA for a source rectangle (.py:286-309): src/tar (bs,3,4) homogeneous,
     returns the unnormalised (bs,3,3) H.  Differentiable (w.r.t. tar, src, scale, div)
     when an input requires grad, as the reference's ATen composition is; the backward
-    is one HIP kernel (hg_tensor_aca_rect_backward_f32)."""
+    is one HIP kernel (hg_tensor_aca_rect_backward_f32).  ``order`` (keyword only, not in
+    the reference's signature): "cpu" gives the bits of the statements run on ATen-CPU,
+    "rocm" those of the reference's default device='cuda' run on a ROCm GPU (.py:393),
+    forward and gradients (ops.tensor_aca_rect)."""
     if src.shape[0] != bs or tar.shape[0] != bs:
         raise ValueError(f"batch size {bs} does not match tensors {tuple(src.shape)}")
     needs_grad = torch.is_grad_enabled() and any(
         isinstance(x, torch.Tensor) and x.requires_grad for x in (src, tar, scale, div))
     if needs_grad:  # differentiable like the reference's ATen composition
-        return ops.tensor_aca_rect_autograd(src, tar, scale, div)
-    return ops.tensor_aca_rect(src, tar, scale, div)
+        return ops.tensor_aca_rect_autograd(src, tar, scale, div, order=order)
+    return ops.tensor_aca_rect(src, tar, scale, div, order=order)
 
 
 def ACA_vanilla(bs: int, src: torch.Tensor, tar: torch.Tensor, loops=None) -> torch.Tensor:

@@ -117,6 +117,12 @@ def test_backward_equals_torch_rocm_autograd(orc, pkg, dev, kind, shape):
     t2, s2_, d2_ = (x.clone().requires_grad_() for x in (t, sc, dv))
     pkg.tensor_aca_rect_autograd(s, t2, s2_, d2_, order="rocm").backward(gH)
     _same(orc, t2.grad, tg.grad, f"autograd dtar {kind} {shape}")
+    # the reference-signature mirror with the keyword
+    t3, s3_, d3_ = (x.clone().requires_grad_() for x in (t, sc, dv))
+    pkg.TensorACA_rect(B, s, t3, s3_, d3_, order="rocm").backward(gH)
+    for got, want, name in ((t3.grad, tg.grad, "tar"), (s3_.grad, sg.grad, "scale"),
+                            (d3_.grad, dg.grad, "div")):
+        _same(orc, got, want, f"TensorACA_rect {name} {kind} {shape}")
     for got, via, want, name in ((g_sc, s2_.grad, sg.grad, "dscale"), (g_dv, d2_.grad, dg.grad, "ddiv")):
         _same(orc, via, got, f"autograd {name} {kind} {shape}")
         # every shape, the batch-wide sums of (1,) and (3,1) included (hg_sum_rocm_f32)
