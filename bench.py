@@ -296,20 +296,57 @@ def timed_region(d: Dist, fn, steps: int):
     return d.max(t1) + d.max(-t0), e0.elapsed_time(e1) / steps
 
 
-def interleaved_ms(d: Dist, fns: dict, rounds: int = 7, steps: int = 40) -> dict:
+def interleaved_ms(d: Dist, fns: dict, rounds: int = 7, steps=40) -> dict:
     """Host-bound per-call figures (eager autograd steps): `rounds` rounds, each timing
     `steps` calls of every function in turn (timed_region), and per function the median of
     its rounds' ms per call, and under "best" the fastest round's.  One mean over a single
     long run took every host stall of the box (its CPU quota's throttling, another process)
     at full weight: the same build's eager autograd step read 30-140 us from run to run that
-    way, its device work 5 us.  The fastest round is the cost with the fewest such stalls."""
+    way, its device work 5 us.  The fastest round is the cost with the fewest such stalls.
+    `steps` may be a dict (calls per round for each function): a round of a short step
+    must be long -- 40 calls of a 33 us step read 60 us a call in a fresh process (about
+    1 ms per round that 400 calls do not show: tools/handoff_probe.py --mimic,
+    profiles/r04/handoff_mimic_r04r.json)."""
     per = {k: [] for k in fns}
+    thr0 = cgroup_throttle()
     for _ in range(rounds):
         for k, f in fns.items():
-            per[k].append(timed_region(d, f, steps)[1])
+            n = steps[k] if isinstance(steps, dict) else steps
+            per[k].append(timed_region(d, f, n)[1])
+    thr1 = cgroup_throttle()
     out = {k: float(np.median(v)) for k, v in per.items()}
     out["best"] = {k: float(np.min(v)) for k, v in per.items()}
+    out["rounds"] = per
+    # the job's CPU quota stopping its threads meanwhile (cgroup v2 cpu.stat), if readable
+    out["throttled"] = ({k: thr1[k] - thr0[k] for k in thr0} if thr0 and thr1 else None)
     return out
+
+
+def warm_host(calls: dict, seconds: float):
+    """Runs each function its number of calls in turn, over and over, for `seconds` of wall
+    time (at least one pass), then waits for the device."""
+    t_end = time.perf_counter() + seconds
+    while True:
+        for f, n in calls.items():
+            for _ in range(n):
+                f()
+        if time.perf_counter() >= t_end:
+            break
+    torch.cuda.synchronize()
+
+
+def cgroup_throttle():
+    """cgroup v2 cpu.stat's throttling counters for this job (nr_periods, nr_throttled,
+    throttled_usec), or None."""
+    text = _read("/sys/fs/cgroup/cpu.stat")
+    if not text:
+        return None
+    vals = {}
+    for ln in text.splitlines():
+        parts = ln.split()
+        if len(parts) == 2 and parts[0] in ("nr_periods", "nr_throttled", "throttled_usec"):
+            vals[parts[0]] = int(parts[1])
+    return vals if len(vals) == 3 else None
 
 
 def launch_stats(d: Dist, fn, groups: int = 40, per_group: int = 10):
@@ -789,11 +826,12 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
         x1.grad = None
         (x1 * 2.0).backward(g1)
 
-    for _ in range(20):
-        f_ours()
-        f_torch()
-        f_floor()
-    eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor})
+    # host warm-up, timed: after the device-bound sections the first ~0.5 s of a host-bound
+    # loop run 1.7x slower (profiles/r04/bench_r04t.log: rounds 50, 50, 50, 29, 29 ... us),
+    # with no CPU-quota throttling meanwhile (cpu.stat) -- the host's clocks coming up
+    warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=1.5)
+    eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor},
+                           steps={"ours": 400, "torch": 40, "floor": 400})
     ms_o, ms_t, ms_floor = eager["ours"], eager["torch"], eager["floor"]
     # 100 fwd + bwd steps (torch.autograd.grad: no .grad accumulation) in one HIP graph
     ops = torch.ops.sks_amd
@@ -814,10 +852,8 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
         Th.grad = None
         torch_tensor_aca_rect(sh, Th, sc, dv).backward(gH)
 
-    for _ in range(20):
-        r_ours()
-        r_torch()
-    eager_r = interleaved_ms(d, {"ours": r_ours, "torch": r_torch})
+    warm_host({r_ours: 400, r_torch: 10}, seconds=0.5)
+    eager_r = interleaved_ms(d, {"ours": r_ours, "torch": r_torch}, steps={"ours": 400, "torch": 40})
     ms_ro, ms_rt = eager_r["ours"], eager_r["torch"]
     g_ro = graph_of(d, lambda: torch.autograd.grad(ops.tensor_aca_rect.default(sh, Th, sc, dv), (Th,), gH), 100)
     g_rt = graph_of(d, lambda: torch.autograd.grad(torch_tensor_aca_rect(sh, Th, sc, dv), (Th,), gH), 100)
@@ -852,7 +888,10 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
                                              "floor": round(eager["best"]["floor"] * 1e3, 2),
                                              "torch": round(eager["best"]["torch"] * 1e3, 2),
                                              "rect_ours": round(eager_r["best"]["ours"] * 1e3, 2)},
-            "eager_method": "median (and fastest) of 7 interleaved rounds of 40 calls (ours, torch, floor)",
+            "eager_rounds_us_per_call": {k: [round(x * 1e3, 1) for x in eager["rounds"][k]]
+                                         for k in ("ours", "floor")},
+            "eager_cgroup_throttling": eager["throttled"],
+            "eager_method": "median (and fastest) of 7 interleaved rounds of 400 calls (ours, floor) / 40 (torch)",
             "gradients_bit_identical_to_torch_composed_on_gpu": same,
             "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
             "backward_large_gbps": round(gbps, 1), "backward_large_frac": round(gbps / HBM_PEAK_GBPS, 4),

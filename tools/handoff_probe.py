@@ -11,6 +11,8 @@ inherit it):
   node8  8 CPUs of that node          node2  2 CPUs          node1  1 CPU
 Each child prints the best of 5 interleaved rounds of 2000 calls per variant.  The parent
 makes no GPU call.  Run on the GPU box: python tools/handoff_probe.py
+`--mimic` instead times the two steps in one process as bench's interleaved_ms does (rounds
+of 40 or 400 calls inside bench.timed_region), then runs bench's section itself.
 """
 import json
 import os
