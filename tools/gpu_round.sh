@@ -27,6 +27,8 @@ run() {  # run <name> <seconds> <cmd...>
 }
 
 rocm-smi --showproductname > "$OUT/rocm_smi.txt" 2>&1 || true
+# device memory already in use before any step of ours (another process on the card shows here)
+rocm-smi --showmeminfo vram >> "$OUT/rocm_smi.txt" 2>&1 || true
 lscpu > "$OUT/lscpu.txt" 2>&1 || true
 for step in $STEPS; do
     case "$step" in
