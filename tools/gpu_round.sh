@@ -74,7 +74,7 @@ for step in $STEPS; do
         aten_tests) run pytest_aten 600 python -u -m pytest tests/test_gpu_aten_sum.py tests/test_gpu_rect_grad.py \
                 tests/test_gpu_rect_bcast.py tests/test_gpu_offsets.py tests/test_gpu_vanilla_grad.py -m gpu -v \
                 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
-        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -q -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --tb=long -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         bench) run bench 600 python bench.py ;;
         prof)
             run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
