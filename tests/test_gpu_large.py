@@ -6,6 +6,7 @@ skips when the device has less free memory."""
 import glob
 import os
 import time
+import warnings
 
 import numpy as np
 import pytest
@@ -41,15 +42,20 @@ def _free_bytes(dev, quiet_s=30.0):
     this process a few seconds after them (every later GPU test failed), while clean boxes
     pass; the memory of an exited process comes back over seconds
     (profiles/r04/cotenant_probe_r04w.json).  A card still shared after the wait: skip."""
-    t_end = time.monotonic() + quiet_s
+    t0 = time.monotonic()
+    first = None
     while True:
         used = _card_used(dev)
         others = None if used is None else used - torch.cuda.memory_reserved(dev)
         if others is None or others <= (4 << 30):
             break
-        if time.monotonic() >= t_end:
+        first = others if first is None else first
+        if time.monotonic() - t0 >= quiet_s:
             pytest.skip(f"{others / 1e9:.0f} GB of the card held by other processes")
         time.sleep(1.0)
+    if first is not None:  # shows in the run's warnings summary
+        warnings.warn(f"waited {time.monotonic() - t0:.0f} s for {first / 1e9:.0f} GB held by "
+                      "other processes to be released")
     free, _ = torch.cuda.mem_get_info(dev)
     return free
 
