@@ -322,17 +322,66 @@ def interleaved_ms(d: Dist, fns: dict, rounds: int = 7, steps=40) -> dict:
     return out
 
 
-def warm_host(calls: dict, seconds: float):
+def card_vram_used(dev):
+    """Card-wide device memory in use (the amdgpu driver's mem_info_vram_used, what rocm-smi
+    shows) for `dev`, or None when /sys does not say."""
+    import glob
+    try:
+        pr = torch.cuda.get_device_properties(dev)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    except (AttributeError, RuntimeError):
+        return None
+    for card in glob.glob("/sys/class/drm/card*/device"):
+        try:
+            if os.path.basename(os.path.realpath(card)).startswith(bdf):
+                return int(_read(os.path.join(card, "mem_info_vram_used")))
+        except (OSError, TypeError, ValueError):
+            continue
+    return None
+
+
+def wait_quiet_card(dev, limit_s: float = 30.0) -> dict:
+    """Waits (up to limit_s) until no more than 4 GB of the card is held outside this
+    process's allocator -- on a box handed over while a previous process's memory is still
+    being released (r04: 200-267 GB in use at the start of a call, gone seconds later;
+    tests/test_gpu_large.py) -- and says what it found."""
+    t0 = time.monotonic()
+    first = None
+    while True:
+        used = card_vram_used(dev)
+        if used is None:
+            return {"vram_in_use_by_others_gb": None, "waited_s": 0.0}
+        others = used - torch.cuda.memory_reserved(dev)
+        first = others if first is None else first
+        if others <= (4 << 30) or time.monotonic() - t0 >= limit_s:
+            return {"vram_in_use_by_others_gb": round(first / 1e9, 1),
+                    "waited_s": round(time.monotonic() - t0, 1),
+                    "still_in_use_gb": round(max(others, 0) / 1e9, 1)}
+        time.sleep(0.5)
+
+
+def warm_host(calls: dict, seconds: float) -> dict:
     """Runs each function its number of calls in turn, over and over, for `seconds` of wall
-    time (at least one pass), then waits for the device."""
-    t_end = time.perf_counter() + seconds
+    time (at least one pass), then waits for the device; returns the first function's first
+    and last pass time.  After the device-bound sections a host runs short host-bound steps
+    slowly for a while -- 0.5 s on one box, about 3 s on another (profiles/r04/
+    bench_r04t.log, bench_r04zb.log), no CPU-quota throttling meanwhile -- so the eager
+    rounds come after this."""
+    t0 = time.perf_counter()
+    first = next(iter(calls))
+    passes = []
     while True:
         for f, n in calls.items():
+            ta = time.perf_counter()
             for _ in range(n):
                 f()
-        if time.perf_counter() >= t_end:
+            if f is first:
+                passes.append((time.perf_counter() - ta) / n)
+        if time.perf_counter() - t0 >= seconds:
             break
     torch.cuda.synchronize()
+    return {"s": round(time.perf_counter() - t0, 2), "passes": len(passes),
+            "first_pass_us": round(passes[0] * 1e6, 1), "last_pass_us": round(passes[-1] * 1e6, 1)}
 
 
 def cgroup_throttle():
@@ -826,10 +875,11 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
         x1.grad = None
         (x1 * 2.0).backward(g1)
 
-    # host warm-up, timed: after the device-bound sections the first ~0.5 s of a host-bound
-    # loop run 1.7x slower (profiles/r04/bench_r04t.log: rounds 50, 50, 50, 29, 29 ... us),
-    # with no CPU-quota throttling meanwhile (cpu.stat) -- the host's clocks coming up
-    warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=1.5)
+    # host warm-up, timed: after the device-bound sections a host-bound loop runs 1.7x
+    # slower for 0.5-3 s depending on the box (profiles/r04/bench_r04t.log: rounds 50, 50,
+    # 50, 29, 29 ... us; bench_r04zb.log: six slow rounds after a 1.5 s warm-up), with no
+    # CPU-quota throttling meanwhile (cpu.stat)
+    warm = warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=4.0)
     eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor},
                            steps={"ours": 400, "torch": 40, "floor": 400})
     ms_o, ms_t, ms_floor = eager["ours"], eager["torch"], eager["floor"]
@@ -891,6 +941,7 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
             "eager_rounds_us_per_call": {k: [round(x * 1e3, 1) for x in eager["rounds"][k]]
                                          for k in ("ours", "floor")},
             "eager_cgroup_throttling": eager["throttled"],
+            "eager_host_warmup": warm,
             "eager_method": "median (and fastest) of 7 interleaved rounds of 400 calls (ours, floor) / 40 (torch)",
             "gradients_bit_identical_to_torch_composed_on_gpu": same,
             "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
@@ -1415,6 +1466,10 @@ def main():
     except (AttributeError, RuntimeError, ValueError):
         numa["bdf_matches_device"] = None
     pkg = ge.load_package()
+    # a card handed over while a previous process's device memory is still coming back:
+    # wait for it before allocating and timing (one rank per GPU only -- gloo rehearsal ranks
+    # share a card, and each other's memory is not foreign)
+    card = wait_quiet_card(d.dev) if d.backend == "nccl" else None
     global SEED
     SEED = args.seed
     n = args.n
@@ -1507,6 +1562,8 @@ def main():
         "rank0_gpu_bdf": numa["bdf"],
         "note": numa.get("note", "each rank bound to its GPU's NUMA node before GPU init"),
     }
+    if card is not None:
+        line["card_at_start_rank0"] = card  # wait_quiet_card: a handed-over card's memory
 
     # Everything after the headline is reported beside it.  A global watchdog and a
     # per-section guard keep any failure there from costing the measured line: an
