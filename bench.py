@@ -363,10 +363,7 @@ def wait_quiet_card(dev, limit_s: float = 30.0) -> dict:
 def warm_host(calls: dict, seconds: float) -> dict:
     """Runs each function its number of calls in turn, over and over, for `seconds` of wall
     time (at least one pass), then waits for the device; returns the first function's first
-    and last pass time.  After the device-bound sections a host runs short host-bound steps
-    slowly for a while -- 0.5 s on one box, about 3 s on another (profiles/r04/
-    bench_r04t.log, bench_r04zb.log), no CPU-quota throttling meanwhile -- so the eager
-    rounds come after this."""
+    and last pass time (allocator and autograd caches warm before the eager rounds)."""
     t0 = time.perf_counter()
     first = next(iter(calls))
     passes = []
@@ -382,6 +379,45 @@ def warm_host(calls: dict, seconds: float) -> dict:
     torch.cuda.synchronize()
     return {"s": round(time.perf_counter() - t0, 2), "passes": len(passes),
             "first_pass_us": round(passes[0] * 1e6, 1), "last_pass_us": round(passes[-1] * 1e6, 1)}
+
+
+def pin_host_threads_l3(prefixes=("pt_autograd",)):
+    """Puts the calling thread and this process's threads named `prefixes` (autograd's device
+    threads) on the CPUs of one L3 domain (the calling thread's current one, within its
+    allowed CPUs), and returns (cpus, restore) -- or (None, no-op) when /sys does not say.
+    A short eager step hands the graph from the main thread to autograd's device thread and
+    back; on two CPUs of different L3 domains that round trip costs up to 3x what it costs
+    within one (tools/host_state_probe.py: the floor's passes 27-29 us with the two threads
+    on one CCD, 44-82 us across CCDs or sockets; pinned, median 27.4 / p90 31.6 us,
+    profiles/r04/host_state_r04zc.json) -- the scheduler's placement, not the code."""
+    try:
+        stat = _read("/proc/thread-self/stat")
+        cur = int(stat.rsplit(")", 1)[1].split()[36])
+        allowed = os.sched_getaffinity(0)
+        cpus = set(_cpu_list(_read(f"/sys/devices/system/cpu/cpu{cur}/cache/index3/"
+                                   "shared_cpu_list"))) & allowed
+    except (AttributeError, TypeError, ValueError, IndexError, OSError):
+        return None, lambda: None
+    if not cpus:
+        return None, lambda: None
+    saved = [(0, allowed)]
+    os.sched_setaffinity(0, cpus)
+    for tid in os.listdir("/proc/self/task"):
+        comm = (_read(f"/proc/self/task/{tid}/comm") or "").strip()
+        if comm.startswith(prefixes):
+            try:
+                saved.append((int(tid), os.sched_getaffinity(int(tid))))
+                os.sched_setaffinity(int(tid), cpus)
+            except OSError:
+                pass
+
+    def restore():
+        for tid, mask in saved:
+            try:
+                os.sched_setaffinity(tid, mask)
+            except OSError:
+                pass
+    return sorted(cpus), restore
 
 
 def cgroup_throttle():
@@ -875,11 +911,14 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
         x1.grad = None
         (x1 * 2.0).backward(g1)
 
-    # host warm-up, timed: after the device-bound sections a host-bound loop runs 1.7x
-    # slower for 0.5-3 s depending on the box (profiles/r04/bench_r04t.log: rounds 50, 50,
-    # 50, 29, 29 ... us; bench_r04zb.log: six slow rounds after a 1.5 s warm-up), with no
-    # CPU-quota throttling meanwhile (cpu.stat)
-    warm = warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=4.0)
+    # unpinned, a host-bound loop ran 1.7x slower for 0.5-3 s at a time depending on where
+    # the scheduler put the two threads (profiles/r04/bench_r04t.log: rounds 50, 50, 50, 29,
+    # 29 ... us; bench_r04zb.log: six slow rounds), with no CPU-quota throttling (cpu.stat)
+    # the eager rounds with the main thread and autograd's device thread on one L3 domain
+    # (pin_host_threads_l3: across domains the hand-off round trip costs up to 3x), after a
+    # short host warm-up; the affinities come back after the TensorACA rounds below
+    l3_cpus, unpin = pin_host_threads_l3()
+    warm = warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=1.0)
     eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor},
                            steps={"ours": 400, "torch": 40, "floor": 400})
     ms_o, ms_t, ms_floor = eager["ours"], eager["torch"], eager["floor"]
@@ -904,6 +943,7 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
 
     warm_host({r_ours: 400, r_torch: 10}, seconds=0.5)
     eager_r = interleaved_ms(d, {"ours": r_ours, "torch": r_torch}, steps={"ours": 400, "torch": 40})
+    unpin()
     ms_ro, ms_rt = eager_r["ours"], eager_r["torch"]
     g_ro = graph_of(d, lambda: torch.autograd.grad(ops.tensor_aca_rect.default(sh, Th, sc, dv), (Th,), gH), 100)
     g_rt = graph_of(d, lambda: torch.autograd.grad(torch_tensor_aca_rect(sh, Th, sc, dv), (Th,), gH), 100)
@@ -942,7 +982,8 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
                                          for k in ("ours", "floor")},
             "eager_cgroup_throttling": eager["throttled"],
             "eager_host_warmup": warm,
-            "eager_method": "median (and fastest) of 7 interleaved rounds of 400 calls (ours, floor) / 40 (torch)",
+            "eager_threads_on_l3_cpus": l3_cpus,
+            "eager_method": "median (and fastest) of 7 interleaved rounds of 400 calls (ours, floor) / 40 (torch), main and autograd device threads on one L3 domain",
             "gradients_bit_identical_to_torch_composed_on_gpu": same,
             "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
             "backward_large_gbps": round(gbps, 1), "backward_large_frac": round(gbps / HBM_PEAK_GBPS, 4),
