@@ -918,32 +918,34 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
     # (pin_host_threads_l3: across domains the hand-off round trip costs up to 3x), after a
     # short host warm-up; the affinities come back after the TensorACA rounds below
     l3_cpus, unpin = pin_host_threads_l3()
-    warm = warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=1.0)
-    eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor},
-                           steps={"ours": 400, "torch": 40, "floor": 400})
-    ms_o, ms_t, ms_floor = eager["ours"], eager["torch"], eager["floor"]
-    # 100 fwd + bwd steps (torch.autograd.grad: no .grad accumulation) in one HIP graph
-    ops = torch.ops.sks_amd
-    g_o = graph_of(d, lambda: torch.autograd.grad(ops.aca.default(S, T, False), (S, T), gH), 100)
-    g_t = graph_of(d, lambda: torch.autograd.grad(torch_aca_vanilla(S, T), (S, T), gH), 100)
-    _, ms_go = timed_region(d, g_o.replay, 10)
-    _, ms_gt = timed_region(d, g_t.replay, 3)
-    del g_o, g_t
-    # the same for TensorACA_rect with tar requiring grad (deep-homography training)
-    _, _, sh, th, sc, dv = pkg.adjust(d.dev, batch)
-    Th = th.clone().requires_grad_()
+    try:
+        warm = warm_host({f_ours: 400, f_floor: 400, f_torch: 10}, seconds=1.0)
+        eager = interleaved_ms(d, {"ours": f_ours, "torch": f_torch, "floor": f_floor},
+                               steps={"ours": 400, "torch": 40, "floor": 400})
+        ms_o, ms_t, ms_floor = eager["ours"], eager["torch"], eager["floor"]
+        # 100 fwd + bwd steps (torch.autograd.grad: no .grad accumulation) in one HIP graph
+        ops = torch.ops.sks_amd
+        g_o = graph_of(d, lambda: torch.autograd.grad(ops.aca.default(S, T, False), (S, T), gH), 100)
+        g_t = graph_of(d, lambda: torch.autograd.grad(torch_aca_vanilla(S, T), (S, T), gH), 100)
+        _, ms_go = timed_region(d, g_o.replay, 10)
+        _, ms_gt = timed_region(d, g_t.replay, 3)
+        del g_o, g_t
+        # the same for TensorACA_rect with tar requiring grad (deep-homography training)
+        _, _, sh, th, sc, dv = pkg.adjust(d.dev, batch)
+        Th = th.clone().requires_grad_()
 
-    def r_ours():
-        Th.grad = None
-        pkg.TensorACA_rect(batch, sh, Th, sc, dv).backward(gH)
+        def r_ours():
+            Th.grad = None
+            pkg.TensorACA_rect(batch, sh, Th, sc, dv).backward(gH)
 
-    def r_torch():
-        Th.grad = None
-        torch_tensor_aca_rect(sh, Th, sc, dv).backward(gH)
+        def r_torch():
+            Th.grad = None
+            torch_tensor_aca_rect(sh, Th, sc, dv).backward(gH)
 
-    warm_host({r_ours: 400, r_torch: 10}, seconds=0.5)
-    eager_r = interleaved_ms(d, {"ours": r_ours, "torch": r_torch}, steps={"ours": 400, "torch": 40})
-    unpin()
+        warm_host({r_ours: 400, r_torch: 10}, seconds=0.5)
+        eager_r = interleaved_ms(d, {"ours": r_ours, "torch": r_torch}, steps={"ours": 400, "torch": 40})
+    finally:
+        unpin()  # a failure in the rounds must not leave the process pinned
     ms_ro, ms_rt = eager_r["ours"], eager_r["torch"]
     g_ro = graph_of(d, lambda: torch.autograd.grad(ops.tensor_aca_rect.default(sh, Th, sc, dv), (Th,), gH), 100)
     g_rt = graph_of(d, lambda: torch.autograd.grad(torch_tensor_aca_rect(sh, Th, sc, dv), (Th,), gH), 100)
