@@ -98,15 +98,26 @@ int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float*
 /* Backward of hg_tensor_aca_rect_f32 (the gradients ATen autograd gives the
  * reference's composed TensorACA_rect, Modules_Runtime_Test.py:294-302).  grad_H:
  * (B,3,3) dL/dH.  Writes grad_tar (B,3,4); grad_src (B,3,4, only [0][0] and [1][0]
- * non-zero) when non-NULL; grad_scale_div (2,B,3) when non-NULL: [0] the (problem, row)
- * terms of dL/dscale, [1] those of dL/ddiv, each in the order of the (B,3,1) tensor ATen
- * autograd sums to the (1,) parameter -- reduce each half with hg_sum_aten_f32 (rows 1,
- * m 3B) for the reference's bits.  scale, div: device pointers.  (Until round 3 this
- * array was (2,B) per-problem sums.) */
+ * non-zero) when non-NULL; grad_scale_div (2,B) when non-NULL: [0][b] problem b's share
+ * of dL/dscale, [1][b] its share of dL/ddiv, each the sum of the problem's three row terms
+ * from +0 (((0 + t0) + t1) + t2, ATen-CPU's reduction to a (B,1,1) operand); their sum over
+ * b is the batch-uniform gradient up to summation order.  scale, div: device pointers.
+ * This layout is the one every version of the library has had under this name; the
+ * (problem, row) terms for ATen's bit-exact batch sum are hg_tensor_aca_rect_backward_terms_f32. */
 int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const float* grad_H,
                                     int64_t B, const float* scale, const float* div,
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
                                     void* stream);
+
+/* The same backward with the (problem, row) terms instead of per-problem sums: grad_terms
+ * (2,B,3) when non-NULL -- [0] the terms of dL/dscale, [1] those of dL/ddiv, each in the
+ * order of the (B,3,1) tensor ATen autograd sums to the (1,) parameter.  Reduce each half
+ * with hg_sum_aten_f32 (rows 1, m 3B) for ATen-CPU's bits, or hg_sum_rocm_f32 (FULL) for
+ * torch-ROCm's.  New in 0.2 (hg_version). */
+int hg_tensor_aca_rect_backward_terms_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, const float* div,
+                                          float* grad_src, float* grad_tar, float* grad_terms,
+                                          void* stream);
 
 /* TensorACA with scale / div broadcast the way the reference composition broadcasts them
  * (Modules_Runtime_Test.py:301-302: torch.mul(div, X) and scale * h_temp, X and h_temp
@@ -342,7 +353,7 @@ int hg_sum_rows_f32(float* x, int64_t rows, int64_t cols, float* out, void* stre
  * threads.  lanes 1, threads 1 give the order of a strided column reduced to (C,1) (the
  * (3,1) parameter case).  1 <= lanes <= 16, 1 <= threads <= 1024, lanes >= 4 when
  * threads > 1; rows * min(threads, ceil(m / 32768)) <= 65535.  x is OVERWRITTEN (scratch).
- * Reduces the gradient terms of hg_tensor_aca_rect_backward_f32 and *_bcast_*. */
+ * Reduces the gradient terms of hg_tensor_aca_rect_backward_terms_f32 and *_bcast_*. */
 int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
                     int lanes, int threads, float* out, void* stream);
 

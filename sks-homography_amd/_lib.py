@@ -36,6 +36,7 @@ SIGNATURES = {
     "hg_tensor_aca_rect_f32_hostscalar": ([_vp, _vp, _vp, _i64, ctypes.c_float, ctypes.c_float,
                                            _vp], _int),
     "hg_tensor_aca_rect_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
+    "hg_tensor_aca_rect_backward_terms_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
     "hg_tensor_aca_rect_bcast_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
                                      _int),
     "hg_tensor_aca_rect_bcast_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,

@@ -529,40 +529,49 @@ int hg_tensor_aca_rect_f32_hostscalar(const float* src, const float* tar, float*
 extern "C++" {
 namespace hg {
 // The one-value backward: the staged form when every buffer is 16-B aligned
-// (tools/kbench_bwd.py), cache policy by size as the forward; scale / div terms as (2,B,3).
-template <int ORDER>
-int launch_rect_backward(const float* src, const float* tar, const float* grad_H, int64_t B,
-                         const float* scale, const float* div, float* grad_src, float* grad_tar,
-                         float* grad_scale_div, hipStream_t s) {
-    const bool ws = grad_src != nullptr, wd = grad_scale_div != nullptr;
+// (tools/kbench_bwd.py), cache policy by size as the forward; dL/dscale, dL/ddiv as (2,B)
+// per-problem sums (kSdSums) or (2,B,3) terms (kSdTerms).
+template <int ORDER, int SD>
+int launch_rect_backward_sd(const float* src, const float* tar, const float* grad_H, int64_t B,
+                            const float* scale, const float* div, float* grad_src,
+                            float* grad_tar, float* grad_sd, hipStream_t s) {
+    const bool ws = grad_src != nullptr;
     if (aligned16(src) && aligned16(tar) && aligned16(grad_H) && aligned16(grad_tar) &&
-        (!ws || aligned16(grad_src)) && (!wd || aligned16(grad_scale_div))) {
+        (!ws || aligned16(grad_src)) && (SD != kSdTerms || aligned16(grad_sd))) {
         const unsigned g = (unsigned)ceil_div(B, kBlock);
         const bool nt = B * 232 > kMallResidentBytes;
-#define HG_RB(A, Bf, NT)                                                                      \
-    launch(tensor_aca_rect_backward_staged<A, Bf, NT, ORDER>, g, kBlock, 0, s, src, tar, grad_H, \
-           B, scale, div, grad_src, grad_tar, grad_scale_div)
-        if (nt) {
-            if (ws && wd) return HG_RB(true, true, true);
-            if (ws) return HG_RB(true, false, true);
-            if (wd) return HG_RB(false, true, true);
-            return HG_RB(false, false, true);
-        }
-        if (ws && wd) return HG_RB(true, true, false);
-        if (ws) return HG_RB(true, false, false);
-        if (wd) return HG_RB(false, true, false);
-        return HG_RB(false, false, false);
+#define HG_RB(A, NT)                                                                           \
+    launch(tensor_aca_rect_backward_staged<A, SD, NT, ORDER>, g, kBlock, 0, s, src, tar, grad_H,  \
+           B, scale, div, grad_src, grad_tar, grad_sd)
+        if (nt) return ws ? HG_RB(true, true) : HG_RB(false, true);
+        return ws ? HG_RB(true, false) : HG_RB(false, false);
 #undef HG_RB
     }
     const unsigned g = generic_grid(B);
-#define HG_RECT_BWD(A, Bf)                                                                    \
-    launch(tensor_aca_rect_backward_kernel<A, Bf, ORDER>, g, kBlock, 0, s, src, tar, grad_H, B, \
-           scale, div, grad_src, grad_tar, grad_scale_div)
-    if (ws && wd) return HG_RECT_BWD(true, true);
-    if (ws) return HG_RECT_BWD(true, false);
-    if (wd) return HG_RECT_BWD(false, true);
-    return HG_RECT_BWD(false, false);
+#define HG_RECT_BWD(A)                                                                        \
+    launch(tensor_aca_rect_backward_kernel<A, SD, ORDER>, g, kBlock, 0, s, src, tar, grad_H, B, \
+           scale, div, grad_src, grad_tar, grad_sd)
+    return ws ? HG_RECT_BWD(true) : HG_RECT_BWD(false);
 #undef HG_RECT_BWD
+}
+
+template <int ORDER, int SD>
+int launch_rect_backward(const float* src, const float* tar, const float* grad_H, int64_t B,
+                         const float* scale, const float* div, float* grad_src, float* grad_tar,
+                         float* grad_sd, hipStream_t s) {
+    if (!grad_sd)
+        return launch_rect_backward_sd<ORDER, kSdNone>(src, tar, grad_H, B, scale, div, grad_src,
+                                                       grad_tar, nullptr, s);
+    return launch_rect_backward_sd<ORDER, SD>(src, tar, grad_H, B, scale, div, grad_src, grad_tar,
+                                              grad_sd, s);
+}
+
+inline int rect_backward_args_ok(const float* src, const float* tar, const float* grad_H, int64_t B,
+                                 const float* scale, const float* div, const float* grad_tar) {
+    if (B < 0) return kErrInvalid;
+    if (B == 0) return 0;
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return kErrInvalid;
+    return -1;  // go on
 }
 }  // namespace hg
 }  // extern "C++"
@@ -571,12 +580,22 @@ int hg_tensor_aca_rect_backward_f32(const float* src, const float* tar, const fl
                                     int64_t B, const float* scale, const float* div,
                                     float* grad_src, float* grad_tar, float* grad_scale_div,
                                     void* stream) {
-    if (B < 0) return hg::kErrInvalid;
-    if (B == 0) return 0;
-    if (!src || !tar || !grad_H || !scale || !div || !grad_tar) return hg::kErrInvalid;
-    return hg::launch_rect_backward<hg::kAtenCpu>(src, tar, grad_H, B, scale, div, grad_src,
-                                                  grad_tar, grad_scale_div,
-                                                  reinterpret_cast<hipStream_t>(stream));
+    const int rc = hg::rect_backward_args_ok(src, tar, grad_H, B, scale, div, grad_tar);
+    if (rc >= 0) return rc;
+    return hg::launch_rect_backward<hg::kAtenCpu, hg::kSdSums>(
+        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_scale_div,
+        reinterpret_cast<hipStream_t>(stream));
+}
+
+int hg_tensor_aca_rect_backward_terms_f32(const float* src, const float* tar, const float* grad_H,
+                                          int64_t B, const float* scale, const float* div,
+                                          float* grad_src, float* grad_tar, float* grad_terms,
+                                          void* stream) {
+    const int rc = hg::rect_backward_args_ok(src, tar, grad_H, B, scale, div, grad_tar);
+    if (rc >= 0) return rc;
+    return hg::launch_rect_backward<hg::kAtenCpu, hg::kSdTerms>(
+        src, tar, grad_H, B, scale, div, grad_src, grad_tar, grad_terms,
+        reinterpret_cast<hipStream_t>(stream));
 }
 
 int hg_tensor_aca_rect_bcast_f32(const float* src, const float* tar, float* H, int64_t B,
@@ -662,8 +681,8 @@ int hg_tensor_aca_rect_backward_order_f32(const float* src, const float* tar, co
                         (grad_scale && grad_div == grad_scale + 3 * B && scale_rows == 2 &&
                          div_rows == 2);
     if (uniform && paired)
-        return hg::launch_rect_backward<hg::kAtenRocm>(src, tar, grad_H, B, scale, div, grad_src,
-                                                       grad_tar, grad_scale, s);
+        return hg::launch_rect_backward<hg::kAtenRocm, hg::kSdTerms>(src, tar, grad_H, B, scale, div,
+                                                                    grad_src, grad_tar, grad_scale, s);
     const hg::RectBcast a{scale, scale_sb, scale_sr, div, div_sb, div_sr};
     return hg::launch(hg::tensor_aca_rect_bcast_backward_kernel<hg::kAtenRocm>, hg::generic_grid(B),
                       hg::kBlock, 0, s, src, tar, grad_H, B, a, grad_src, grad_tar, grad_scale,
@@ -906,6 +925,10 @@ int hg_sum_rocm_f32(const float* x, int64_t B, int kind, float* out, float* work
     hg::RocmSum a = hg::rocm_sum_config(x, B, kind, num_mp, max_tpm);
     a.aligned = hg::aligned16(x);
     if (a.ctas > hg::kRocmSumMaxCtas) return hg::kErrInvalid;
+    // CTA partials exist only for the one-output (FULL) reduction: the (3,1) form's output
+    // split leaves one CTA per output (ATen's shape), and its partials would be indexed by
+    // blockIdx.y past a 3-float output
+    if (a.ctas > 1 && kind != HG_SUM_ROCM_FULL) return hg::kErrInvalid;
     const dim3 block((unsigned)a.bw, (unsigned)a.bh);
     const dim3 grid((unsigned)hg::ceil_div((int64_t)a.num_out, a.step_out), (unsigned)a.ctas);
     if (a.ctas == 1) return hg::launch(hg::rocm_sum_kernel, grid, block, 0, s, a, out);
@@ -930,17 +953,26 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
     if (runs > 65535) return hg::kErrInvalid;
     const hg::AtenSum a{x, row_stride, elem_stride, m, chunks > 1 ? hg::ceil_div(m, chunks) : m,
                         (int)chunks, lanes};
-    const hg::AtenRun r0(a, 0);  // the longest run sizes the grids
-    if (r0.step > hg::kAtenMaxStep) return hg::kErrInvalid;  // runs beyond 2^24 rows per stream
-    if (r0.nb > 0) {
-        const int64_t bx = r0.g1 + 1;  // one block per super-block (the last may be partial)
+    // The grids cover the largest extent over EVERY run: a shorter run (the last chunk) may
+    // take a smaller level step and so have more super-blocks / level-2 groups than run 0.
+    int64_t g1_max = -1, l2_max = 0, step_max = 0;
+    for (int64_t run = 0; run < runs; ++run) {
+        const hg::AtenRun r(a, (int)run);
+        if (r.step > hg::kAtenMaxStep) return hg::kErrInvalid;  // a run of > 2^35 rows per stream
+        if (r.nb > 0 && r.g1 > g1_max) g1_max = r.g1;
+        if (r.g1 > 0 && (r.g2 + 1) * r.S > l2_max) l2_max = (r.g2 + 1) * r.S;
+        if (r.step * r.S > step_max) step_max = r.step * r.S;
+    }
+    if (g1_max >= 0) {
+        const int64_t bx = g1_max + 1;  // one block per super-block (the last may be partial)
         if (bx > 0x7fffffffLL) return hg::kErrInvalid;
         const int rc = hg::launch(hg::aten_sum_l1, dim3((unsigned)bx, (unsigned)runs),
-                                  hg::kAtenL1Threads, 0, s, a);
+                                  hg::kAtenL1Threads, (size_t)step_max * sizeof(float), s, a);
         if (rc) return rc;
     }
-    if (r0.g1 > 0) {
-        const int64_t bx = hg::ceil_div((r0.g2 + 1) * r0.S, (int64_t)256);
+    if (l2_max > 0) {
+        const int64_t bx = hg::ceil_div(l2_max, (int64_t)256);
+        if (bx > 0x7fffffffLL) return hg::kErrInvalid;
         const int rc = hg::launch(hg::aten_sum_l2, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
         if (rc) return rc;
     }
@@ -949,6 +981,6 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
     return hg::launch(hg::aten_sum_l4, (unsigned)rows, 64, 0, s, a, threads, lanes, out);
 }
 
-const char* hg_version(void) { return "sks-homography-amd 0.1 (gfx950)"; }
+const char* hg_version(void) { return "sks-homography-amd 0.2 (gfx950)"; }
 
 }  // extern "C"

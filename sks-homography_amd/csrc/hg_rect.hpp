@@ -78,15 +78,28 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_kernel(
 
 // ---------------------------------------------------------------------------
 // TensorACA rect backward: one lane per problem, grid-stride.  Writes dL/dtar
-// (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and the
-// (problem, row) terms of dL/dscale and dL/ddiv as a (2,B,3) array -- each half in the
-// order of the (B,3,1) tensor ATen autograd sums to the (1,) parameter (hg_sum_aten_f32).
-__device__ __forceinline__ void store_sd_terms(float* __restrict__ gsd, int64_t B, int64_t p,
-                                               const float (&gsr)[3], const float (&gdr)[3]) {
+// (B,3,4), optionally dL/dsrc (B,3,4: only [0][0] and [1][0] are non-zero) and, by SD,
+// dL/dscale and dL/ddiv as
+//   kSdSums  -- a (2,B) array of per-problem sums (the three row terms from +0, ATen's
+//               reduction to a (B,1,1) operand: hg_tensor_aca_rect_backward_f32's contract), or
+//   kSdTerms -- the (problem, row) terms as a (2,B,3) array, each half in the order of the
+//               (B,3,1) tensor ATen autograd sums to the (1,) parameter (hg_sum_aten_f32;
+//               hg_tensor_aca_rect_backward_terms_f32).
+enum : int { kSdNone = 0, kSdSums = 1, kSdTerms = 2 };
+
+template <int SD>
+__device__ __forceinline__ void store_sd(float* __restrict__ gsd, int64_t B, int64_t p,
+                                         const float (&gsr)[3], const float (&gdr)[3], float gs,
+                                         float gd) {
+    if constexpr (SD == kSdSums) {
+        gsd[p] = gs;
+        gsd[B + p] = gd;
+    } else if constexpr (SD == kSdTerms) {
 #pragma unroll
-    for (int r = 0; r < 3; ++r) {
-        gsd[3 * p + r] = gsr[r];
-        gsd[3 * B + 3 * p + r] = gdr[r];
+        for (int r = 0; r < 3; ++r) {
+            gsd[3 * p + r] = gsr[r];
+            gsd[3 * B + 3 * p + r] = gdr[r];
+        }
     }
 }
 
@@ -103,12 +116,13 @@ __device__ __forceinline__ void store_terms3_staged(char* __restrict__ out, cons
     wave_lds_sync();
 }
 
-template <bool WANT_SRC, bool WANT_SD, int ORDER = kAtenCpu>
+template <bool WANT_SRC, int SD, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
     float* __restrict__ gsrc, float* __restrict__ gtar, float* __restrict__ gsd) {
     const float scale = scale_p[0], div = div_p[0];
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
     const int64_t stride = (int64_t)gridDim.x * kBlock;
     for (int64_t p = (int64_t)blockIdx.x * kBlock + threadIdx.x; p < B; p += stride) {
         float tr[12], g[9], gt[12];
@@ -116,16 +130,16 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_kernel(
         for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
-        float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt,
-                                          gmx, gmy, gsr, gdr);
+        float gmx, gmy, gs, gd, gsr[3], gdr[3];
+        tensor_aca_rect_grad_rows<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, g, gt, gmx,
+                                         gmy, gs, gd, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
-        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
+        store_sd<SD>(gsd, B, p, gsr, gdr, gs, gd);
     }
 }
 
@@ -349,7 +363,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
 // there, and the gradient rows leave as contiguous slabs (store_rows_staged) instead
 // of 48-B / 32-B per-lane strided accesses.  The ragged tail takes the per-lane code.
 // Same arithmetic (tensor_aca_rect_grad), same bits.
-template <bool WANT_SRC, bool WANT_SD, bool NT, int ORDER = kAtenCpu>
+template <bool WANT_SRC, int SD, bool NT, int ORDER = kAtenCpu>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -357,6 +371,7 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
     constexpr int kTar = kWave * 48, kG = kWave * 36;
     __shared__ __attribute__((aligned(16))) char smem[kWavesPerBlock][kTar + kG];
     const float scale = scale_p[0], div = div_p[0];
+    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
     const int lane = threadIdx.x & (kWave - 1);
     const int wave = threadIdx.x / kWave;
     const int64_t base = ((int64_t)blockIdx.x * kWavesPerBlock + wave) * kWave;
@@ -373,8 +388,8 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
         __builtin_memcpy(tr, lds + lane * 48, 48);
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
-        float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms<ORDER>(tr, mx, my, scale, div, g, gt, gmx, gmy, gsr, gdr);
+        float gmx, gmy, gs, gd, gsr[3], gdr[3];
+        tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gs, gd, gsr, gdr);
         wave_lds_sync();  // the staging below reuses the input bytes
         store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
         if constexpr (WANT_SRC) {
@@ -383,7 +398,9 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
             for (int k = 0; k < 12; ++k) gs[k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
             store_rows_staged<12, NT>(reinterpret_cast<char*>(gsrc + base * 12), gs, lds, lane);
         }
-        if constexpr (WANT_SD) {
+        if constexpr (SD == kSdSums) {
+            store_sd<SD>(gsd, B, p, gsr, gdr, gs, gd);  // lane-consecutive 4-B stores
+        } else if constexpr (SD == kSdTerms) {
             // the wave's 64 x 3 terms of each parameter are one contiguous 768-B run:
             // staged, then 48 lanes store 16 B each (the second run is 16-B aligned when 3B
             // is a multiple of 4)
@@ -404,16 +421,16 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
         for (int k = 0; k < 12; ++k) tr[k] = tar[p * 12 + k];
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = gH[p * 9 + k];
-        float gmx, gmy, gsr[3], gdr[3];
-        tensor_aca_rect_grad_terms<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], scale, div, g, gt,
-                                          gmx, gmy, gsr, gdr);
+        float gmx, gmy, gs, gd, gsr[3], gdr[3];
+        tensor_aca_rect_grad_rows<ORDER>(tr, src[p * 12 + 0], src[p * 12 + 4], sc, dv, g, gt, gmx,
+                                         gmy, gs, gd, gsr, gdr);
 #pragma unroll
         for (int k = 0; k < 12; ++k) gtar[p * 12 + k] = gt[k];
         if constexpr (WANT_SRC) {
 #pragma unroll
             for (int k = 0; k < 12; ++k) gsrc[p * 12 + k] = k == 0 ? gmx : (k == 4 ? gmy : 0.f);
         }
-        if constexpr (WANT_SD) store_sd_terms(gsd, B, p, gsr, gdr);
+        store_sd<SD>(gsd, B, p, gsr, gdr, gs, gd);
     }
 }
 

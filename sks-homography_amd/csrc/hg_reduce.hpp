@@ -96,10 +96,12 @@ struct AtenRun {
 // row 0; g == g1 is the partial super-block's r1 blocks (acc1 when the cascade stops),
 // written over its row 0 too.  A wave's load touches 128-B runs (32 streams x 4 B).
 constexpr int kAtenL1Threads = 256;
-constexpr int kAtenMaxStep = 64;  // lp <= 6: runs up to 2^27 rows of each stream
+// lp <= 8: runs up to 2^35 rows of each stream (lp = max(4, CeilLog2(n) / 4)); the block sums
+// of one super-block take step * S floats of dynamic LDS (64 KiB at step 256, 16 lanes)
+constexpr int kAtenMaxStep = 256;
 
 __global__ __launch_bounds__(kAtenL1Threads) void aten_sum_l1(AtenSum a) {
-    __shared__ float bs[kAtenMaxStep * 4 * kAtenMaxLanes];
+    extern __shared__ float bs[];  // [step][S] of the launch's largest run
     const AtenRun R(a, blockIdx.y);
     const int64_t g = blockIdx.x;
     if (g > R.g1 || (g == R.g1 && R.r1 == 0)) return;  // block-uniform

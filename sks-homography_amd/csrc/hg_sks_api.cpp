@@ -72,9 +72,15 @@ struct Scratch {
             return (int)e;
         return 0;
     }
+    // A call returns once its completion word is visible, which the kernel stores last --
+    // the kernel may not have retired yet.  So the stream is drained before the mapped
+    // memory it writes is released (hipStreamDestroy does not wait for work in flight).
     ~Scratch() {
         for (Slot& sl : slot) {
-            if (sl.stream) (void)hipStreamDestroy(sl.stream);
+            if (sl.stream) {
+                (void)hipStreamSynchronize(sl.stream);
+                (void)hipStreamDestroy(sl.stream);
+            }
             if (sl.host) (void)hipHostFree(sl.host);
         }
     }

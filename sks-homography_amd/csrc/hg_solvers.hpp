@@ -705,17 +705,4 @@ __device__ __forceinline__ void tensor_aca_rect_grad(const float (&tr)[12], floa
     tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
 }
 
-// The same with each row's share of dL/dscale, dL/ddiv (the (B,3,1) terms ATen autograd sums
-// to a (1,) parameter's shape) instead of the per-problem sums.
-template <int ORDER = kAtenCpu>
-__device__ __forceinline__ void tensor_aca_rect_grad_terms(const float (&tr)[12], float mx,
-                                                           float my, float scale, float div,
-                                                           const float (&g)[9], float (&gt)[12],
-                                                           float& gmx, float& gmy, float (&gsr)[3],
-                                                           float (&gdr)[3]) {
-    const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
-    float gscale, gdiv;
-    tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gscale, gdiv, gsr, gdr);
-}
-
 }  // namespace hg

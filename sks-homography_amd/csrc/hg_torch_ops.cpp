@@ -205,7 +205,7 @@ int terms_mode_for(const Bcast& b, int order) {
 // the (B,3,1) tensor to a (1,) parameter (cols = false) or a (3,1) one (cols = true).
 at::Tensor rocm_batch_sum(const at::Tensor& terms, int64_t B, bool cols, void* stream) {
     at::Tensor g = at::empty({cols ? 3 : 1}, terms.options());
-    at::Tensor ws = !cols && B > 0 ? at::empty({HG_SUM_ROCM_WORKSPACE}, terms.options()) : g;
+    at::Tensor ws = at::empty({HG_SUM_ROCM_WORKSPACE}, terms.options());  // never the output
     hip_ok(hg_sum_rocm_f32(terms.data_ptr<float>(), B, cols ? HG_SUM_ROCM_COLS : HG_SUM_ROCM_FULL,
                            g.data_ptr<float>(), ws.data_ptr<float>(), stream),
            "hg_sum_rocm_f32");
@@ -262,11 +262,11 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
         float* gs = need_src && B ? g_src.data_ptr<float>() : nullptr;
         float* pp = need_scale_div && B ? part.data_ptr<float>() : nullptr;
         if (order == HG_ORDER_ATEN_CPU)
-            hip_ok(hg_tensor_aca_rect_backward_f32(
+            hip_ok(hg_tensor_aca_rect_backward_terms_f32(
                        src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
                        scale_.data_ptr<float>(), div_.data_ptr<float>(), gs,
                        g_tar.data_ptr<float>(), pp, st),
-                   "hg_tensor_aca_rect_backward_f32");
+                   "hg_tensor_aca_rect_backward_terms_f32");
         else  // the same (2,B,3) terms, the (B,3) halves named apart
             hip_ok(hg_tensor_aca_rect_backward_order_f32(
                        src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
@@ -675,12 +675,18 @@ class AcaFunction : public torch::autograd::Function<AcaFunction> {
     }
 };
 
+// One policy for the three forms nothing in the reference differentiates (aca with
+// normalize=True, solve, sks): an input that requires grad while grad mode is on is refused,
+// naming the differentiable form, instead of a result whose graph is silently cut.  Under
+// torch.no_grad() or on detached inputs they run as inference.
 at::Tensor aca_autograd(const at::Tensor& src, const at::Tensor& tar, bool normalize) {
-    if (!any_requires_grad({&src, &tar}) || normalize) {
-        if (normalize && any_requires_grad({&src, &tar}))
-            TORCH_WARN_ONCE("sks_amd::aca: normalize=True (the C++ API's H/H[8], ACA_SKS.cpp:94-98) "
-                            "has no gradient in the reference; H is returned without one -- "
-                            "ACA_vanilla's unnormalised form (normalize=False) is differentiable");
+    const bool grad = any_requires_grad({&src, &tar});
+    TORCH_CHECK(!(grad && normalize),
+                "sks_amd::aca: normalize=True (the C++ API's H/H[8], ACA_SKS.cpp:94-98) has no "
+                "backward in the reference; call it on detached inputs or under torch.no_grad(), "
+                "or use normalize=False (ACA_vanilla's form, Modules_Runtime_Test.py:312-388), "
+                "which is differentiable");
+    if (!grad) {
         at::AutoDispatchBelowADInplaceOrView below;
         return call_aca(src, tar, normalize);
     }
@@ -688,13 +694,13 @@ at::Tensor aca_autograd(const at::Tensor& src, const at::Tensor& tar, bool norma
 }
 
 // sks_amd::solve is the C++ API's batch mirror (sks::runKernel_*, normalised by default):
-// nothing differentiates it in the reference, so it runs below autograd and says so once.
+// nothing differentiates it in the reference, so inputs that require grad are refused.
 at::Tensor solve_autograd(const at::Tensor& src, const at::Tensor& tar, int64_t algo,
                           bool normalize, int64_t layout) {
-    if (any_requires_grad({&src, &tar}))
-        TORCH_WARN_ONCE("sks_amd::solve has no gradient (the C++ API it mirrors, ACA_SKS.cpp, is "
-                        "not differentiated by the reference); its output carries none -- "
-                        "sks_amd::aca (normalize=False, ACA_vanilla's form) is differentiable");
+    TORCH_CHECK(!any_requires_grad({&src, &tar}),
+                "sks_amd::solve has no backward (the C++ API it mirrors, ACA_SKS.cpp, is not "
+                "differentiated by the reference); call it on detached inputs or under "
+                "torch.no_grad(), or use sks_amd::aca (normalize=False) for gradients");
     static auto op = c10::Dispatcher::singleton()
                          .findSchemaOrThrow("sks_amd::solve", "")
                          .typed<at::Tensor(const at::Tensor&, const at::Tensor&, int64_t, bool,

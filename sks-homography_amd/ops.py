@@ -337,7 +337,14 @@ def tensor_aca_rect_autograd(src: torch.Tensor, tar: torch.Tensor, scale: Scalar
                              div: Scalar, order: str = "cpu") -> torch.Tensor:
     """Differentiable TensorACA (torch.ops.sks_amd.tensor_aca_rect): gradients flow to
     tar, src (M's coordinates), and scale/div when they are tensors requiring grad.
-    ``order`` as tensor_aca_rect's (the backward follows the forward's)."""
+    ``order`` as tensor_aca_rect's (the backward follows the forward's).
+
+    With order="cpu", a batch-uniform scale / div gradient of >= 32768 terms is summed in
+    ATen-CPU's order FOR THE FORWARD CALLER'S torch.get_num_threads() (ATen chunks such sums
+    per thread): the bits then differ between, e.g., a plain python run and a torchrun rank
+    with OMP_NUM_THREADS=1, exactly as the reference's own CPU autograd does.  Pin them with
+    torch.set_num_threads(T) before the forward, or call tensor_aca_rect_backward with
+    aten_threads=T.  Other gradients, H, and order="rocm" do not depend on it."""
     _gpu_only(tar)
     return _OPS.tensor_aca_rect.default(src, tar, _dev_scalar(scale, tar.device),
                                         _dev_scalar(div, tar.device), _order(order))

@@ -49,10 +49,19 @@ def TensorACA_rect(bs: int, src: torch.Tensor, tar: torch.Tensor, scale, div, *,
     """TensorACA for a source rectangle (.py:286-309): src/tar (bs,3,4) homogeneous,
     returns the unnormalised (bs,3,3) H.  Differentiable (w.r.t. tar, src, scale, div)
     when an input requires grad, as the reference's ATen composition is; the backward
-    is one HIP kernel (hg_tensor_aca_rect_backward_f32).  ``order`` (keyword only, not in
-    the reference's signature): "cpu" gives the bits of the statements run on ATen-CPU,
-    "rocm" those of the reference's default device='cuda' run on a ROCm GPU (.py:393),
-    forward and gradients (ops.tensor_aca_rect)."""
+    is one HIP kernel (hg_tensor_aca_rect_backward_terms_f32) and a device-side batch sum.
+    ``order`` (keyword only, not in the reference's signature): "cpu" gives the bits of the
+    statements run on ATen-CPU, "rocm" those of the reference's default device='cuda' run on
+    a ROCm GPU (.py:393), forward and gradients (ops.tensor_aca_rect).
+
+    Host dependence (order="cpu"): ATen-CPU sums a batch-uniform scale / div gradient of
+    >= 32768 terms (B >= 10923) in chunks, one per ATen thread, so its bits depend on
+    torch.get_num_threads() of the process running the reference.  This op follows the
+    forward caller's torch.get_num_threads() the same way: a plain `python` run and a
+    torchrun rank (OMP_NUM_THREADS=1) give different dL/dscale, dL/ddiv bits, each equal to
+    what ATen-CPU gives in that process.  To pin them, call torch.set_num_threads(T) first,
+    or use ops.tensor_aca_rect_backward(..., aten_threads=T).  H and dL/dtar, dL/dsrc never
+    depend on it; order="rocm" does not either (the GPU's reduction shape is fixed)."""
     if src.shape[0] != bs or tar.shape[0] != bs:
         raise ValueError(f"batch size {bs} does not match tensors {tuple(src.shape)}")
     needs_grad = torch.is_grad_enabled() and any(

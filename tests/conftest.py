@@ -1,8 +1,15 @@
+import ctypes
+import glob
 import os
 import sys
 
 import numpy as np
 import pytest
+
+# HIP's runtime logs the address and reason of a GPU memory fault at level 1 (errors only):
+# with it set before HIP starts, a fault's own report lands in the failing test's captured
+# stderr, which the driver's log tail shows.
+os.environ.setdefault("AMD_LOG_LEVEL", "1")
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
@@ -18,6 +25,144 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: full-size (10M) parity checks")
 
 
+# ----------------------------------------------------------------------------- GPU test order
+# The oracle / golden / reference parity files run first, the BASELINE configs at their full
+# sizes among the very first, so that a late failure under -x cannot erase the evidence that
+# matters most; then the subprocess programs; then the plumbing and stress tests (threads,
+# host-page registration, pending-error probes, graphs); the >2^31 (~200 GB) tests last.
+# Within a tier the files keep their order and every test its place in its file.  Nothing
+# is dropped or skipped by this.
+_FIRST = [  # (file, test name prefix): BASELINE configs and the reference's own outputs
+    ("test_gpu_parity.py", "test_config2_full_batch_equals_compiled_reference"),  # configs[1], [2]
+    ("test_gpu_parity.py", "test_rect_close_to_torch_composed_on_gpu"),          # configs[3]
+    ("test_gpu_parity.py", "test_config1_gpu_equals_compiled_reference"),        # configs[0]
+    ("test_gpu_config5.py", "test_config5_rank_blocks"),                          # configs[4]
+    ("test_gpu_parity.py", "test_golden_"),
+    ("test_gpu_parity.py", "test_full_size_10m_bit_exact"),
+    ("test_gpu_parity.py", "test_rect_backward_kernel_vs_oracle"),
+]
+_PARITY_FILES = [
+    "test_gpu_parity.py", "test_gpu_refcpp_bits.py", "test_gpu_kat.py", "test_gpu_vanilla_grad.py",
+    "test_gpu_rect_grad.py", "test_gpu_rect_bcast.py", "test_gpu_rect_aten_bits.py",
+    "test_gpu_rect_rocm_order.py", "test_gpu_offsets.py", "test_gpu_table8.py",
+    "test_gpu_ransac.py", "test_gpu_mrg32k3a.py", "test_gpu_aten_sum.py", "test_gpu_rocm_sum.py",
+    "test_gpu_refcu.py", "test_gpu_config5.py", "test_gpu_multi.py",
+]
+_PROGRAM_FILES = ["test_gpu_bench_contract.py", "test_gpu_cpp_api.py"]
+_STRESS_FILES = ["test_gpu_grouped.py", "test_gpu_errors.py", "test_gpu_host.py"]
+_STRESS_TESTS = [  # plumbing tests inside the parity file: threads, host pointers, graphs
+    ("test_gpu_parity.py", "test_cpp_api_single_problem_host_and_device"),
+    ("test_gpu_parity.py", "test_cpp_api_mixed_pointers_and_edge_cases"),
+    ("test_gpu_parity.py", "test_solve_one_c_abi"),
+    ("test_gpu_parity.py", "test_stream_and_graph_capture"),
+    ("test_gpu_parity.py", "test_concurrent_streams"),
+    ("test_gpu_parity.py", "test_c_abi_from_many_threads"),
+]
+_LAST = [("test_gpu_large.py", ""), ("test_gpu_parity.py", "test_beyond_int32_problem_count")]
+
+
+def gpu_tier(fname, name):
+    """(tier, rank within the tier) of a GPU test: lower runs first."""
+    for i, (f, p) in enumerate(_FIRST):
+        if fname == f and name.startswith(p):
+            return 0, i
+    for i, (f, p) in enumerate(_LAST):
+        if fname == f and name.startswith(p):
+            return 4, i
+    for i, (f, p) in enumerate(_STRESS_TESTS):
+        if fname == f and name.startswith(p):
+            return 3, len(_STRESS_FILES) + i
+    for tier, files in ((1, _PARITY_FILES), (2, _PROGRAM_FILES), (3, _STRESS_FILES)):
+        if fname in files:
+            return tier, files.index(fname)
+    return 1, len(_PARITY_FILES)  # a GPU file not listed yet: with the parity files
+
+
+def pytest_collection_modifyitems(session, config, items):
+    gpu = [(i, it) for i, it in enumerate(items) if it.get_closest_marker("gpu") is not None]
+    if not gpu:
+        return
+    slots = [i for i, _ in gpu]
+    ordered = sorted(gpu, key=lambda e: (gpu_tier(os.path.basename(str(e[1].fspath)),
+                                                  e[1].name), e[0]))
+    for slot, (_, it) in zip(slots, ordered):
+        items[slot] = it
+
+
+# ------------------------------------------------------------------- GPU fault attribution
+_FAULTS = {"checked": 0, "first": None}
+_HIP = None
+
+
+def _hip():
+    global _HIP
+    if _HIP is None:
+        _HIP = ctypes.CDLL("libamdhip64.so.7")
+        _HIP.hipGetErrorName.restype = ctypes.c_char_p
+    return _HIP
+
+
+@pytest.fixture(autouse=True)
+def _gpu_fault_check(request):
+    """After every GPU test: a device-wide synchronisation, so that a kernel fault (an illegal
+    address, an aborted queue) is reported against the test whose launches caused it, by
+    name, instead of surfacing at some later test's first copy.  A test that never touched
+    the GPU in this process (the subprocess programs) is not checked here."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import torch
+    if not torch.cuda.is_initialized():
+        return
+    hip = _hip()
+    rc = hip.hipDeviceSynchronize()
+    _FAULTS["checked"] += 1
+    if rc != 0:
+        name = hip.hipGetErrorName(rc).decode()
+        if _FAULTS["first"] is None:
+            _FAULTS["first"] = (request.node.nodeid, name)
+        pytest.fail(f"GPU error {name} ({rc}) pending at the end of {request.node.nodeid}: a "
+                    "kernel launched during this test (or by a thread it started) faulted",
+                    pytrace=False)
+
+
+def _card_used_gb():
+    """Card-wide VRAM in use by every process (amdgpu's mem_info_vram_used), in GB."""
+    vals = []
+    for p in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
+        try:
+            with open(p) as f:
+                vals.append(int(f.read()) / 1e9)
+        except (OSError, ValueError):
+            pass
+    return vals
+
+
+def pytest_sessionstart(session):
+    session.config._card_at_start = _card_used_gb()
+
+
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """One line for the driver's log tail: how many GPU tests were fault-checked, the first
+    fault if any, and what the card held (all processes) when the session began."""
+    if not _FAULTS["checked"] and _FAULTS["first"] is None:
+        return
+    first = _FAULTS["first"]
+    card = getattr(config, "_card_at_start", [])
+    terminalreporter.write_line(
+        f"gpu fault check: {_FAULTS['checked']} GPU tests synchronised after running; "
+        + (f"FIRST FAULT {first[1]} after {first[0]}" if first else "no fault")
+        + "; card VRAM in use at session start (GB, all processes): "
+        + (", ".join(f"{v:.1f}" for v in card) if card else "n/a"))
+    large = [r for r in terminalreporter.stats.get("passed", []) + terminalreporter.stats.get("skipped", [])
+             if "test_gpu_large.py" in r.nodeid and r.when in ("call", "setup")]
+    if large:
+        terminalreporter.write_line(
+            "beyond-2^31 parity: " + "; ".join(f"{r.nodeid.split('::')[-1]} {r.outcome}"
+                                                for r in large))
+
+
+# ----------------------------------------------------------------------------- fixtures
 @pytest.fixture(scope="session")
 def orc():
     """Oracle module (test infrastructure)."""
@@ -64,4 +209,3 @@ class default_dtype:
 
     def __exit__(self, *exc):
         self.torch.set_default_dtype(self.prev)
-

@@ -139,8 +139,10 @@ def test_other_entry_validation(pkg):
     assert lib.hg_tensor_aca_rect_bcast_f32(None, None, None, 4, None, 0, 0, None, 0, 0, None) == 1
     assert lib.hg_tensor_aca_rect_bcast_backward_f32(None, None, None, 3, None, 0, 0, None, 0, 0,
                                                      None, None, None, 0, None, 0, None) == 1
-    assert lib.hg_tensor_aca_rect_backward_f32(None, None, None, 3, None, None, None, None, None,
-                                               None) == 1
+    for fn in (lib.hg_tensor_aca_rect_backward_f32, lib.hg_tensor_aca_rect_backward_terms_f32):
+        assert fn(None, None, None, 3, None, None, None, None, None, None) == 1
+        assert fn(None, None, None, 0, None, None, None, None, None, None) == 0
+        assert fn(None, None, None, -1, None, None, None, None, None, None) == 1
     # the evaluation-order entry points: HG_ORDER_ATEN_CPU (0) is the bcast form, ROCM (1) its
     # own launch; anything else is refused before a pointer is looked at
     for order in (0, 1):

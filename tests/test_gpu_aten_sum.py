@@ -51,6 +51,18 @@ def test_kernel_equals_restatement(orc, pkg, dev, T):
         assert got.tobytes() == want.tobytes(), (m, T, got, want)
 
 
+@pytest.mark.parametrize("m,T", [(2**25 + 63, 2), (3 * 2**24 + 95, 3)])
+def test_last_run_with_a_smaller_level_step(orc, pkg, dev, m, T):
+    """Chunked runs whose LAST (shorter) chunk falls below a level-power boundary: run 0 has
+    2^19 + 1 rows per stream (step 32, 512 super-blocks), the last 2^19 (step 16, 2048
+    super-blocks).  The launch grids must cover the largest extent over every run, not run
+    0's (grids sized from run 0 skipped the last run's super-blocks 513..2047)."""
+    x = _data(m, 77 + T)
+    got = _sum_gpu(pkg, dev, x, 1, m, 0, 1, 8, T)
+    want = np.array([aten_sum(x, 8, T)], np.float32)
+    assert got.tobytes() == want.tobytes(), (m, T, got, want)
+
+
 def test_rows_strides_and_column_form(orc, pkg, dev):
     """Several rows at once; a (B,3) array's columns as strided rows (elem stride 3) and as
     (3,B) rows, both in the one-lane column order of a (3,1) parameter."""

@@ -150,26 +150,28 @@ def test_native_ops_pass_torch_opcheck(pkg, dev):
 
 
 def test_autograd_refusals_and_constants(orc, pkg, dev):
-    """Every native op answers inputs that require grad explicitly: sks_amd::sks (no
-    differentiable SKS in the reference) raises naming the missing backward; aca with
-    normalize=True and solve (the C++ API's forms) return H without a graph; the scalar
-    TensorACA overload gives src / tar the tensor overload's gradients bit for bit."""
-    import warnings
+    """Every native op answers inputs that require grad explicitly, with one policy: the
+    forms the reference never differentiates -- sks_amd::sks, aca with normalize=True and
+    solve (the C++ API's forms) -- raise naming the missing backward while grad mode is on,
+    and run as inference under torch.no_grad() or on detached inputs; the scalar TensorACA
+    overload gives src / tar the tensor overload's gradients bit for bit."""
     ops = torch.ops.sks_amd
     q = (torch.rand(64, 4, 2, device=dev) * 100).requires_grad_(True)
     t = q.detach() + 1.5
     with pytest.raises(RuntimeError, match="sks_amd::sks has no backward"):
         ops.sks.default(q, t, False)
+    with pytest.raises(RuntimeError, match="normalize=True .* has no backward"):
+        ops.aca.default(q, t, True)
+    with pytest.raises(RuntimeError, match="sks_amd::solve has no backward"):
+        ops.solve.default(q.view(64, 8), t.view(64, 8), 1, True, 0)
     with torch.no_grad():
         assert ops.sks.default(q, t, False).shape == (64, 3, 3)
-    assert ops.sks.default(q.detach(), t, True).grad_fn is None
-    with warnings.catch_warnings():
-        warnings.simplefilter("ignore")
         H = ops.aca.default(q, t, True)
         Hs = ops.solve.default(q.view(64, 8), t.view(64, 8), 1, True, 0)
+    assert ops.sks.default(q.detach(), t, True).grad_fn is None
     assert H.grad_fn is None and not H.requires_grad
     assert Hs.grad_fn is None and not Hs.requires_grad
-    _bits(orc, H, ops.aca.default(q.detach(), t, True).cpu().numpy(), "aca normalize=True, grad inputs")
+    _bits(orc, H, ops.aca.default(q.detach(), t, True).cpu().numpy(), "aca normalize=True, no_grad")
     B = 777
     torch.manual_seed(1)
     _, _, sh, th, sc, dv = pkg.adjust(dev, B)

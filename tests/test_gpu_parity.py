@@ -437,9 +437,10 @@ def test_rect_backward_kernel_vs_oracle(orc, oracle, pkg, dev):
             # the (problem, row) terms of dL/dscale, dL/ddiv, via the raw C ABI: (2,B,3)
             part = torch.empty(2, B, 3, device=dev)
             gt2 = torch.empty(B, 3, 4, device=dev)
-            pkg._lib.call("hg_tensor_aca_rect_backward_f32", sh.data_ptr(), th.data_ptr(),
+            stream = torch.cuda.current_stream(dev).cuda_stream
+            pkg._lib.call("hg_tensor_aca_rect_backward_terms_f32", sh.data_ptr(), th.data_ptr(),
                           gH.data_ptr(), B, s_t.data_ptr(), d_t.data_ptr(), None, gt2.data_ptr(),
-                          part.data_ptr(), torch.cuda.current_stream(dev).cuda_stream)
+                          part.data_ptr(), stream)
             *_, gsr, gdr, gss, gds = oracle.tensor_aca_rect_rows_backward(
                 sh.cpu().numpy(), th.cpu().numpy(), gH.cpu().numpy(),
                 np.array([scale], np.float32), np.array([div], np.float32))
@@ -447,6 +448,16 @@ def test_rect_backward_kernel_vs_oracle(orc, oracle, pkg, dev):
             _bits(orc, part[1], gdr, f"div terms B={B}")
             _bits(orc, np.stack([gss, gds], 1), wsd, f"oracle per-problem sums B={B}")
             _bits(orc, gt2, wt, f"grad_tar (no src) B={B}")
+            # the original entry point's (2,B) per-problem sums (its contract since round 1);
+            # a guard float after the buffer must stay untouched
+            sums = torch.full((2 * B + 1,), 7.0, device=dev)
+            gs3 = torch.empty(B, 3, 4, device=dev)
+            pkg._lib.call("hg_tensor_aca_rect_backward_f32", sh.data_ptr(), th.data_ptr(),
+                          gH.data_ptr(), B, s_t.data_ptr(), d_t.data_ptr(), gs3.data_ptr(),
+                          gt2.data_ptr(), sums.data_ptr(), stream)
+            _bits(orc, sums[:2 * B].view(2, B).T, wsd, f"(2,B) per-problem sums B={B}")
+            _bits(orc, gs3, ws, f"grad_src (sums entry) B={B}")
+            assert sums[2 * B].item() == 7.0, "wrote past the (2,B) buffer"
 
 
 def test_rect_autograd_matches_reference_autograd(pkg, dev):

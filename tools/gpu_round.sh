@@ -22,6 +22,10 @@ run() {  # run <name> <seconds> <cmd...>
     local rc=$?
     echo "=== $name rc=$rc" | tee -a "$OUT/steps.log"
     tail -n 5 "$OUT/$name.log"
+    if [ "$rc" != 0 ]; then  # every failed step's whole log is kept (a later step may reuse the name)
+        mkdir -p "$OUT/failed"
+        cp "$OUT/$name.log" "$OUT/failed/${TAG}_${name}_rc${rc}_$(date +%H%M%S).log"
+    fi
     if fatal "$rc"; then echo "FATAL rc=$rc in $name: stopping"; exit "$rc"; fi
     return 0
 }
@@ -75,6 +79,15 @@ for step in $STEPS; do
                 tests/test_gpu_rect_bcast.py tests/test_gpu_offsets.py tests/test_gpu_vanilla_grad.py -m gpu -v \
                 -p no:cacheprovider --timeout 300 --timeout-method thread ;;
         tests) run pytest_gpu 900 python -u -m pytest tests -m gpu -x -v --tb=long -p no:cacheprovider --timeout 300 --timeout-method thread ;;
+        driver_tests)  # the driver's own command, verbatim
+            run pytest_driver 900 python -m pytest tests/ -x -q -m gpu ;;
+        tests_prof)
+            # the whole GPU suite under a kernel trace: if anything faults, the trace names the
+            # last kernels dispatched before it
+            run pytest_prof 1100 rocprofv3 --kernel-trace --stats --output-format csv \
+                -d "$OUT/tests_prof_$TAG" -o run -- python3 -u -m pytest tests -m gpu -x -v \
+                -p no:cacheprovider --timeout 300 --timeout-method thread
+            gzip -f "$OUT/tests_prof_$TAG"/*kernel_trace.csv 2>/dev/null || true ;;
         bench) run bench 600 python bench.py ;;
         prof)
             run prof 900 rocprofv3 --kernel-trace --stats --output-format csv \
