@@ -126,20 +126,37 @@ def _gpu_fault_check(request):
                     pytrace=False)
 
 
-def _card_used_gb():
-    """Card-wide VRAM in use by every process (amdgpu's mem_info_vram_used), in GB."""
-    vals = []
+def _cards_used_gb():
+    """{PCI address: card-wide VRAM in use by every process, GB} (amdgpu's
+    mem_info_vram_used) for every card the host shows -- read without touching HIP."""
+    vals = {}
     for p in glob.glob("/sys/class/drm/card*/device/mem_info_vram_used"):
         try:
             with open(p) as f:
-                vals.append(int(f.read()) / 1e9)
+                vals[os.path.basename(os.path.realpath(os.path.dirname(p)))] = int(f.read()) / 1e9
         except (OSError, ValueError):
             pass
     return vals
 
 
+def _our_card_gb(cards):
+    """The entry of `cards` for cuda:0 (the PCI address from HIP, which the tests started)."""
+    try:
+        import torch
+        if not torch.cuda.is_initialized():
+            return None
+        pr = torch.cuda.get_device_properties(0)
+        bdf = f"{pr.pci_domain_id:04x}:{pr.pci_bus_id:02x}:{pr.pci_device_id:02x}"
+    except Exception:  # noqa: BLE001 -- a summary line must not fail the session
+        return None
+    for addr, gb in cards.items():
+        if addr.startswith(bdf):
+            return gb
+    return None
+
+
 def pytest_sessionstart(session):
-    session.config._card_at_start = _card_used_gb()
+    session.config._cards_at_start = _cards_used_gb()
 
 
 def pytest_terminal_summary(terminalreporter, exitstatus, config):
@@ -148,12 +165,12 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
     if not _FAULTS["checked"] and _FAULTS["first"] is None:
         return
     first = _FAULTS["first"]
-    card = getattr(config, "_card_at_start", [])
+    card = _our_card_gb(getattr(config, "_cards_at_start", {}))
     terminalreporter.write_line(
         f"gpu fault check: {_FAULTS['checked']} GPU tests synchronised after running; "
         + (f"FIRST FAULT {first[1]} after {first[0]}" if first else "no fault")
-        + "; card VRAM in use at session start (GB, all processes): "
-        + (", ".join(f"{v:.1f}" for v in card) if card else "n/a"))
+        + "; this card's VRAM in use at session start (all processes): "
+        + (f"{card:.1f} GB" if card is not None else "n/a"))
     large = [r for r in terminalreporter.stats.get("passed", []) + terminalreporter.stats.get("skipped", [])
              if "test_gpu_large.py" in r.nodeid and r.when in ("call", "setup")]
     if large:

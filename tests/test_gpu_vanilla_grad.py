@@ -111,19 +111,19 @@ def test_backward_c_abi_misaligned_and_ragged(orc, oracle, pkg, dev):
                       x.data_ptr(), None, None)
 
 
-def test_normalised_form_returns_H_without_a_graph(pkg, dev):
+def test_normalised_form_refuses_grad_inputs(pkg, dev):
     """normalize=True (the C++ API's H / H[8], ACA_SKS.cpp:94-98) has no gradient in the
-    reference: with inputs that require grad the op still returns H -- the same bits as
-    without grad -- carrying no graph, and warns once (inference callers need not detach)."""
-    import warnings
+    reference: with inputs that require grad (grad mode on) the op raises, naming the
+    differentiable form, rather than returning H with its graph silently cut; under
+    torch.no_grad() or on detached inputs it returns H, the same bits either way."""
     src = torch.rand(8, 4, 2, device=dev, requires_grad=True)
     tar = torch.rand(8, 4, 2, device=dev)
-    with warnings.catch_warnings(record=True):
-        warnings.simplefilter("always")
+    with pytest.raises(RuntimeError, match="normalize=False"):
+        torch.ops.sks_amd.aca(src, tar, True)
+    with torch.no_grad():
         H = torch.ops.sks_amd.aca(src, tar, True)
     assert H.shape == (8, 3, 3) and H.grad_fn is None and not H.requires_grad
-    with torch.no_grad():
-        assert torch.equal(torch.ops.sks_amd.aca(src, tar, True), H)
+    assert torch.equal(torch.ops.sks_amd.aca(src.detach(), tar, True), H)
 
 
 B = 200_003
