@@ -825,6 +825,12 @@ def torch_aca_vanilla(src, tar):
 # TensorACA rect in the reference's (B,3,4) layout: 48 B tar + 48 B src (whole records: the
 # two floats used, src[:,0,0] and src[:,1,0], touch every 32-B sector) + 36 B H
 RECT_LAYOUT_MIN_BYTES = 132
+# the backwards' floors in the same layout: every 32-B sector of the 48-B src records is fetched
+# for M's two coordinates (16 B apart), so src costs 48 B, not 8.  dL/dtar alone: src 48 + tar
+# 48 + dL/dH 36 in, dL/dtar 48 out; everything: + dL/dsrc 48 and the (problem, row) scale / div
+# terms 24 out.  PMC reads 183.7 / 256.2 B (profiles/pmc_traffic.json)
+RECT_BWD_TAR_LAYOUT_MIN_BYTES = 180
+RECT_BWD_ALL_LAYOUT_MIN_BYTES = 252
 
 # imgs/GPU-runtime.png (Table 8), N = 1M, FP64 SoA, unnamed CUDA GPU
 TABLE8_US = {"aca": 245.0, "sks": 436.0, "gpt": 8390.0, "ge": 589.0}
@@ -947,6 +953,10 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
     finally:
         unpin()  # a failure in the rounds must not leave the process pinned
     ms_ro, ms_rt = eager_r["ours"], eager_r["torch"]
+    # the same rounds with the threads where the scheduler puts them -- what a caller who does
+    # not pin gets; floor measured the same way, in the same rounds
+    warm_host({f_ours: 400, f_floor: 400}, seconds=0.5)
+    eager_u = interleaved_ms(d, {"ours": f_ours, "floor": f_floor}, steps={"ours": 400, "floor": 400})
     g_ro = graph_of(d, lambda: torch.autograd.grad(ops.tensor_aca_rect.default(sh, Th, sc, dv), (Th,), gH), 100)
     g_rt = graph_of(d, lambda: torch.autograd.grad(torch_tensor_aca_rect(sh, Th, sc, dv), (Th,), gH), 100)
     _, ms_gro = timed_region(d, g_ro.replay, 10)
@@ -986,6 +996,12 @@ def vanilla_autograd_section(d: Dist, pkg, batch: int, big: int = 16 * 1024 * 10
             "eager_host_warmup": warm,
             "eager_threads_on_l3_cpus": l3_cpus,
             "eager_method": "median (and fastest) of 7 interleaved rounds of 400 calls (ours, floor) / 40 (torch), main and autograd device threads on one L3 domain",
+            "eager_unpinned": {"fwd_bwd_us_per_call": round(eager_u["ours"] * 1e3, 2),
+                               "autograd_floor_us_per_call": round(eager_u["floor"] * 1e3, 2),
+                               "above_floor_us_per_call": round((eager_u["ours"] - eager_u["floor"]) * 1e3, 2),
+                               "rounds_us_per_call": {k: [round(x * 1e3, 1) for x in eager_u["rounds"][k]]
+                                                      for k in ("ours", "floor")},
+                               "method": "the same interleaved rounds with no thread pinning (the scheduler's placement)"},
             "gradients_bit_identical_to_torch_composed_on_gpu": same,
             "backward_large_batch": n, "backward_large_us_per_launch": round(ms_k * 1e3, 2),
             "backward_large_gbps": round(gbps, 1), "backward_large_frac": round(gbps / HBM_PEAK_GBPS, 4),
@@ -1719,6 +1735,18 @@ def main():
                 f_ba()
             _, ms_bt = timed_region(d, f_bt, 20)
             _, ms_ba = timed_region(d, f_ba, 20)
+            # the all-gradient backward kernel alone (the raw C ABI: no batch sum, no allocation)
+            gs_k, gt_k = torch.empty_like(bs_h), torch.empty_like(bt_h)
+            terms_k = torch.empty((2, big, 3), device=d.dev)
+            stream_k = torch.cuda.current_stream(d.dev).cuda_stream
+            f_bk = lambda: pkg._lib.call(  # noqa: E731
+                "hg_tensor_aca_rect_backward_terms_f32", bs_h.data_ptr(), bt_h.data_ptr(),
+                gHb.data_ptr(), big, bsc.data_ptr(), bdv.data_ptr(), gs_k.data_ptr(),
+                gt_k.data_ptr(), terms_k.data_ptr(), stream_k)
+            for _ in range(5):
+                f_bk()
+            _, ms_bk = timed_region(d, f_bk, 20)
+            del gs_k, gt_k, terms_k
             # the opt-in torch-ROCm evaluation order (order="rocm"): the same kernels' forms with
             # the GPU's 3-term sums -- forward, dL/dtar alone, everything
             f_rf = lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb, order="rocm")  # noqa
@@ -1743,6 +1771,16 @@ def main():
                 "large_backward_all_traffic": pmc_detail(
                     "rect_backward_all", "the backward kernel alone; the scale / div sum "
                     "(hg_sum_aten_f32) is in large_backward_all_us"),
+                # against the (B,3,4) layout's own floors (RECT_BWD_*_LAYOUT_MIN_BYTES)
+                "large_backward_tar_layout_min_bytes_per_problem": RECT_BWD_TAR_LAYOUT_MIN_BYTES,
+                "large_backward_tar_layout_min_frac": round(
+                    big * RECT_BWD_TAR_LAYOUT_MIN_BYTES / (ms_bt * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_all_layout_min_bytes_per_problem": RECT_BWD_ALL_LAYOUT_MIN_BYTES,
+                "large_backward_all_layout_min_frac": round(
+                    big * RECT_BWD_ALL_LAYOUT_MIN_BYTES / (ms_ba * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_all_kernel_us": round(ms_bk * 1e3, 2),
+                "large_backward_all_kernel_layout_min_frac": round(
+                    big * RECT_BWD_ALL_LAYOUT_MIN_BYTES / (ms_bk * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "rocm_order": {
                     "large_us_per_call": round(ms_rf * 1e3, 2),
                     "large_frac": round(big * RECT_LAYOUT_MIN_BYTES / (ms_rf * 1e-3) / 1e9

@@ -102,28 +102,92 @@ def _hip():
     return _HIP
 
 
+_PROBE = {"lib": None, "tried": False}
+
+
+def _fault_probe():
+    """tests/_build/libfault_probe.so (tests/fault_probe.c): a ROCr system-event handler that
+    prints a GPU memory fault's virtual address and reason the moment it happens.  Installed
+    once HIP is up; None when it is not built or cannot register."""
+    if not _PROBE["tried"]:
+        _PROBE["tried"] = True
+        path = os.path.join(ROOT, "tests", "_build", "libfault_probe.so")
+        if os.path.exists(path):
+            lib = ctypes.CDLL(path)
+            lib.hg_fault_probe_read.argtypes = [ctypes.POINTER(ctypes.c_int),
+                                                ctypes.POINTER(ctypes.c_uint64),
+                                                ctypes.POINTER(ctypes.c_uint32)]
+            if lib.hg_fault_probe_install() == 0:
+                _PROBE["lib"] = lib
+    return _PROBE["lib"]
+
+
+def _where(va):
+    """What holds virtual address `va` in this process: its /proc/self/maps line, and the
+    torch caching-allocator segment (device memory) containing it, if any."""
+    out = []
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                lo, hi = (int(x, 16) for x in line.split()[0].split("-"))
+                if lo <= va < hi:
+                    out.append(f"maps: {line.strip()} (+0x{va - lo:x})")
+                    break
+            else:
+                out.append("maps: no mapping holds it")
+    except OSError:
+        pass
+    try:
+        import torch
+        for seg in torch.cuda.memory_snapshot():
+            a, n = seg["address"], seg["total_size"]
+            if a <= va < a + n:
+                out.append(f"torch segment 0x{a:x} + {n} ({seg.get('segment_type')}, offset 0x{va - a:x})")
+                break
+        else:
+            out.append("not in any torch caching-allocator segment")
+    except Exception as e:  # noqa: BLE001 -- diagnostics only
+        out.append(f"torch snapshot unavailable: {e!r}"[:200])
+    return "; ".join(out)
+
+
 @pytest.fixture(autouse=True)
 def _gpu_fault_check(request):
     """After every GPU test: a device-wide synchronisation, so that a kernel fault (an illegal
     address, an aborted queue) is reported against the test whose launches caused it, by
-    name, instead of surfacing at some later test's first copy.  A test that never touched
-    the GPU in this process (the subprocess programs) is not checked here."""
+    name, instead of surfacing at some later test's first copy -- with the faulting address
+    and what holds it (tests/fault_probe.c).  A test that never touched the GPU in this
+    process (the subprocess programs) is not checked here."""
+    gpu = request.node.get_closest_marker("gpu") is not None
+    if gpu:
+        import torch
+        if torch.cuda.is_initialized():
+            _fault_probe()
     yield
-    if request.node.get_closest_marker("gpu") is None:
+    if not gpu:
         return
     import torch
     if not torch.cuda.is_initialized():
         return
+    probe = _fault_probe()
     hip = _hip()
     rc = hip.hipDeviceSynchronize()
     _FAULTS["checked"] += 1
-    if rc != 0:
-        name = hip.hipGetErrorName(rc).decode()
+    seen = 0
+    if probe is not None:
+        t, va, why = ctypes.c_int(), ctypes.c_uint64(), ctypes.c_uint32()
+        seen = probe.hg_fault_probe_read(ctypes.byref(t), ctypes.byref(va), ctypes.byref(why))
+    if rc != 0 or seen:
+        name = hip.hipGetErrorName(rc).decode() if rc else "no HIP error yet"
+        detail = ""
+        if seen:
+            detail = (f"; fault probe: {seen} event(s), first type {t.value}, VA 0x{va.value:x}, "
+                      f"reason 0x{why.value:x}; {_where(va.value)}")
         if _FAULTS["first"] is None:
-            _FAULTS["first"] = (request.node.nodeid, name)
+            _FAULTS["first"] = (request.node.nodeid, name + detail)
         pytest.fail(f"GPU error {name} ({rc}) pending at the end of {request.node.nodeid}: a "
-                    "kernel launched during this test (or by a thread it started) faulted",
-                    pytrace=False)
+                    "kernel launched during this test (or by a thread it started) faulted"
+                    + detail, pytrace=False)
 
 
 def _cards_used_gb():
@@ -166,8 +230,9 @@ def pytest_terminal_summary(terminalreporter, exitstatus, config):
         return
     first = _FAULTS["first"]
     card = _our_card_gb(getattr(config, "_cards_at_start", {}))
+    probe = "fault probe on" if _PROBE["lib"] is not None else "fault probe off"
     terminalreporter.write_line(
-        f"gpu fault check: {_FAULTS['checked']} GPU tests synchronised after running; "
+        f"gpu fault check ({probe}): {_FAULTS['checked']} GPU tests synchronised after running; "
         + (f"FIRST FAULT {first[1]} after {first[0]}" if first else "no fault")
         + "; this card's VRAM in use at session start (all processes): "
         + (f"{card:.1f} GB" if card is not None else "n/a"))

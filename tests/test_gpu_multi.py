@@ -27,8 +27,10 @@ def _batch(pkg, dev, n, dtype, layout):
 
 @pytest.mark.parametrize("dtype,layout,norm", [(torch.float32, "aos", True),
                                                (torch.float64, "soa", False)])
-@pytest.mark.parametrize("parts", [1, 3])
+@pytest.mark.parametrize("parts", [1, 3, 8])
 def test_solve_multi_equals_whole_batch(pkg, dev, dtype, layout, norm, parts):
+    """parts = 8: the shard loop the 8-GPU node runs (BASELINE configs[4]), every shard here
+    on device 0 with its own stream; the calling thread's current device is left as it was."""
     multi = pkg._lib.multi()
     n = 1_000_003
     src, tar = _batch(pkg, dev, n, dtype, layout)
@@ -49,7 +51,11 @@ def test_solve_multi_equals_whole_batch(pkg, dev, dtype, layout, norm, parts):
         shards[r].src, shards[r].tar, shards[r].H = s.data_ptr(), t.data_ptr(), H.data_ptr()
         shards[r].stream = streams[r].cuda_stream
     torch.cuda.synchronize(dev)
+    hip = ctypes.CDLL("libamdhip64.so.7")
+    before, after = ctypes.c_int(-1), ctypes.c_int(-1)
+    assert hip.hipGetDevice(ctypes.byref(before)) == 0
     assert multi.hg_solve_multi(0, dt, shards, parts, 1 if layout == "soa" else 0, 1 if norm else 0) == 0
+    assert hip.hipGetDevice(ctypes.byref(after)) == 0 and after.value == before.value
     assert multi.hg_sync_multi(shards, parts) == 0
     got = torch.cat([H for *_, H in keep], dim=0 if layout == "aos" else 1)
     assert torch.equal(got.view(torch.uint8), want.view(torch.uint8))

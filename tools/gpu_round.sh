@@ -122,6 +122,15 @@ for step in $STEPS; do
                 python3 tools/pmc_sample.py
             python3 tools/pmc_sample.py --reduce "$OUT/pmc_sample_$TAG/run_counter_collection.csv" \
                 "$OUT/pmc_sample_valu.json" > "$OUT/pmc_sample_reduce.log" 2>&1 || true ;;
+        pmc_table8)
+            # the fused Table-8 kernel (draws + gather + solve, binary64) at 10 M, ACA then SKS:
+            # VALU / SALU / LDS instructions, VALU busy, residency, waits (one pass, no tracing)
+            run pmc_table8 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_BUSY_CU_CYCLES \
+                SQ_WAVE_CYCLES SQ_WAVES SQ_INSTS_LDS SQ_INSTS_SALU SQ_WAIT_INST_ANY GRBM_GUI_ACTIVE \
+                --kernel-trace --output-format csv -d "$OUT/pmc_table8_$TAG" -o run -- \
+                python3 tools/pmc_table8.py
+            python3 tools/pmc_table8.py --reduce "$OUT/pmc_table8_$TAG/run_counter_collection.csv" \
+                "$OUT/pmc_table8_$TAG.json" > "$OUT/pmc_table8_reduce.log" 2>&1 || true ;;
         sample_flags) run sample_flags 200 bash tools/sample_flags_probe.sh run ;;
         slp_ab) run slp_ab 300 python tools/slp_ab.py ;;
         kbench) run kbench 600 python tools/kbench.py ;;
