@@ -215,8 +215,10 @@ __global__ __launch_bounds__(gather_block<ALGO>()) void gather_solve_f64_kernel(
 template <int ALGO>
 constexpr int mrg_gather_block() { return ALGO == kGPT || ALGO == kGE ? 512 : 1024; }
 
-template <int ALGO>
-constexpr size_t mrg_words_lds() { return (size_t)2 * 4 * 4 * (mrg_gather_block<ALGO>() / 4) * 4; }
+// Q: positions per chunk (a multiple of 4).  A lane makes Q words of its row per chunk and
+// solves Q / 4 hypotheses from the chunk's words; the words buffer is [2][4][Q][classes].
+template <int ALGO, int Q = 4, int KB = mrg_gather_block<ALGO>()>
+constexpr size_t mrg_words_lds() { return (size_t)2 * 4 * Q * (KB / 4) * 4; }
 
 constexpr int kMrgGroupBatch = 8;  // groups whose engine bases one pass makes
 constexpr size_t kMrgStaticLds = 2 * kMrgGroupBatch * 24 * 4;
@@ -241,17 +243,21 @@ __device__ __forceinline__ double pair_swap(double x) {
 }
 typedef double hg_dbl2 __attribute__((ext_vector_type(2)));
 
-template <int ALGO, bool NORM, bool POOL_LDS, int ABL = kMrgAblNone>
-__global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64_kernel(
+template <int ALGO, bool NORM, bool POOL_LDS, int ABL = kMrgAblNone, int Q = 4,
+          int KB = mrg_gather_block<ALGO>()>
+__global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
     uint32_t size, uint64_t magic, const double2* __restrict__ pool_src,
     const double2* __restrict__ pool_tar, double* __restrict__ H, int64_t n,
     mrg::GatherArgs a) {
-    constexpr int kB = mrg_gather_block<ALGO>();
+    static_assert(Q % 4 == 0 && Q >= 4, "whole hypotheses per lane per chunk");
+    static_assert(KB % 256 == 0 && 24 * kMrgGroupBatch <= KB, "whole waves per row");
+    constexpr int kB = KB;
     constexpr int kC = kB / 4;  // classes per group
-    constexpr int kQ = 4;       // positions per chunk
+    constexpr int kQ = Q;       // positions per chunk
+    constexpr int kPer = Q / 4; // hypotheses a lane solves per chunk
     extern __shared__ __attribute__((aligned(16))) char dyn[];
     uint32_t* words = reinterpret_cast<uint32_t*>(dyn);  // [2][4][kQ][kC]
-    double2* pool = reinterpret_cast<double2*>(dyn + mrg_words_lds<ALGO>());
+    double2* pool = reinterpret_cast<double2*>(dyn + mrg_words_lds<ALGO, Q, KB>());
     if constexpr (POOL_LDS) {
         for (uint32_t i = threadIdx.x; i < size; i += kB) {
             pool[2 * i] = pool_src[i];
@@ -301,28 +307,24 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
                 st = mrg_apply_lo((uint32_t)c - w, a.y[k][1].w);
             }
         }
-        // chunk m holds steps 4m .. 4m+3, in state slots (m + i) mod 3: one copy of the four
-        // steps per phase m mod 3 (a block-uniform branch), so no step moves the state
+        // chunk m holds steps Q m .. Q m + Q - 1, in state slots (Q m + i) mod 3: one copy of
+        // the Q steps per phase (Q m) mod 3 (a block-uniform branch), so no step moves the state
         auto gen = [&](int buf, int phase) {
             uint32_t* w = words + (buf * 4 + k) * kQ * kC + c;
             if constexpr ((ABL & kMrgAblNoDraws) != 0) {
                 const uint32_t x = (uint32_t)threadIdx.x * 2654435761u + (uint32_t)phase;
-                w[0] = x;
-                w[kC] = x ^ 1u;
-                w[2 * kC] = x ^ 2u;
-                w[3 * kC] = x ^ 3u;
+#pragma unroll
+                for (int i = 0; i < kQ; ++i) w[i * kC] = x ^ (uint32_t)i;
                 return;
             }
-            auto four = [&](auto p) {
+            auto steps = [&](auto p) {
                 constexpr int P = decltype(p)::value;
-                w[0] = mrg::step<P % 3>(st);
-                w[kC] = mrg::step<(P + 1) % 3>(st);
-                w[2 * kC] = mrg::step<(P + 2) % 3>(st);
-                w[3 * kC] = mrg::step<P % 3>(st);
+#pragma unroll
+                for (int i = 0; i < kQ; ++i) w[i * kC] = mrg::step_at(st, (P + i) % 3);  // folds
             };
-            if (phase == 0) four(std::integral_constant<int, 0>());
-            else if (phase == 1) four(std::integral_constant<int, 1>());
-            else four(std::integral_constant<int, 2>());
+            if (phase == 0) steps(std::integral_constant<int, 0>());
+            else if (phase == 1) steps(std::integral_constant<int, 1>());
+            else steps(std::integral_constant<int, 2>());
         };
         // positions of the group's first class (the others have as many or one fewer)
         const int64_t qn = (n - g * kC + mrg::kOrder - 1) >> mrg::kOrderLog2;
@@ -330,14 +332,17 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
         __syncthreads();
         int buf = 0, phase = 0;
         for (int64_t q0 = 0; q0 < qn; q0 += kQ, buf ^= 1) {
-            phase = phase == 2 ? 0 : phase + 1;  // the phase of chunk q0 / 4 + 1
+            phase = (phase + kQ) % 3;  // the phase of chunk q0 / Q + 1
             if (q0 + kQ < qn) gen(buf ^ 1, phase);
-            const int64_t h = h0 + ((q0 + k) << mrg::kOrderLog2);
+#pragma unroll
+            for (int j = 0; j < kPer; ++j) {
+            const int qq = k + 4 * j;  // this lane's position in the chunk
+            const int64_t h = h0 + ((q0 + qq) << mrg::kOrderLog2);
             if ((ABL & kMrgSt16) != 0 || h < n) {
                 double s[8], t[8], hh[9];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const uint32_t w = words[((buf * 4 + r) * kQ + k) * kC + c];
+                    const uint32_t w = words[((buf * 4 + r) * kQ + qq) * kC + c];
                     const uint32_t ix = fastmod_u32(w, magic, size);
                     double2 ps, pt;
                     if constexpr ((ABL & kMrgAblNoGather) != 0) {
@@ -386,6 +391,7 @@ __global__ __launch_bounds__(mrg_gather_block<ALGO>()) void mrg_gather_solve_f64
                     for (int r = 0; r < 9; ++r) __builtin_nontemporal_store(hh[r], H + h + r * n);
                 }
             }
+            }
             __syncthreads();
         }
     }
@@ -426,11 +432,11 @@ inline int launch_mrg_words(uint32_t* out, int64_t count, uint64_t seed, int64_t
 
 // variant: -1 shipped (pool in LDS when it fits beside the draws buffer), 0 pool in global
 // memory
-template <int ALGO, bool NORM, int ABL = kMrgAblNone>
+template <int ALGO, bool NORM, int ABL = kMrgAblNone, int Q = 4, int KB = mrg_gather_block<ALGO>()>
 inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32_t size,
                                     uint64_t seed, double* H, int64_t n, hipStream_t s,
                                     int variant = -1) {
-    constexpr int kB = mrg_gather_block<ALGO>();
+    constexpr int kB = KB;
     constexpr size_t kLdsMax = 160 * 1024;
     mrg::GatherArgs a{};
     mrg::Vec x1, x2;
@@ -447,11 +453,11 @@ inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32
     const int64_t cols = n < mrg::kOrder ? n : mrg::kOrder;
     const int64_t groups = (cols + kB / 4 - 1) / (kB / 4);
     const uint64_t magic = fastmod_magic(size);
-    const size_t words = mrg_words_lds<ALGO>();
+    const size_t words = mrg_words_lds<ALGO, Q, KB>();
     const bool pool_lds = variant != 0 && kMrgStaticLds + words + (size_t)size * 32 <= kLdsMax;
     const size_t lds = pool_lds ? words + (size_t)size * 32 : words;
-    auto k = pool_lds ? mrg_gather_solve_f64_kernel<ALGO, NORM, true, ABL>
-                      : mrg_gather_solve_f64_kernel<ALGO, NORM, false, ABL>;
+    auto k = pool_lds ? mrg_gather_solve_f64_kernel<ALGO, NORM, true, ABL, Q, KB>
+                      : mrg_gather_solve_f64_kernel<ALGO, NORM, false, ABL, Q, KB>;
     if (lds + kMrgStaticLds > kSampleLdsMax && !lds_opt_in(k, kMrgStaticLds))
         return (int)hipErrorInvalidValue;
     int64_t per_cu = (int64_t)(kLdsMax / (lds + kMrgStaticLds));

@@ -954,6 +954,18 @@ static int rand_gather_variant(int variant, const double2* ps, const double2* pt
         case 11:  // 9 with 16-B paired stores
             return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve | kMrgAblNoStart | kMrgAblNoDraws |
                                                          kMrgAblNoGather | kMrgSt16>(ps, pt, size, seed, H, n, s);
+        case 15:  // Q = 8 positions per chunk: two hypotheses per lane, half the barriers (bit-exact)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNone, 8>(ps, pt, size, seed, H, n, s);
+        case 16:  // Q = 4 forced (the round-3..4 shape)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNone, 4>(ps, pt, size, seed, H, n, s);
+        case 17:  // Q = 8 with no solve (the draws, gathers and stores of that shape)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNoSolve, 8>(ps, pt, size, seed, H, n, s);
+        case 18:  // Q = 8 in 768-lane blocks (168 VGPRs: no spill, 3 waves per SIMD)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNone, 8, 768>(ps, pt, size, seed, H, n, s);
+        case 19:  // Q = 8 in 512-lane blocks (2 waves per SIMD)
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNone, 8, 512>(ps, pt, size, seed, H, n, s);
+        case 20:  // Q = 4 in 768-lane blocks
+            return launch_rand_gather_solve<ALGO, false, kMrgAblNone, 4, 768>(ps, pt, size, seed, H, n, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -963,7 +975,7 @@ extern "C" {
 int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
                                   const double* pool_tar, uint32_t size, uint64_t seed, double* H,
                                   int64_t n, void* stream) {
-    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 14)
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 20)
         return (int)hipErrorInvalidValue;
     if ((variant == 10 || variant == 11 || variant == 14) && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15)))
         return (int)hipErrorInvalidValue;

@@ -154,6 +154,7 @@ for step in $STEPS; do
                 python tools/kbench_sample.py ;;
         kbench_gather) run kbench_gather 300 python tools/kbench_gather.py ;;
         kbench_mrg) run kbench_mrg 300 python tools/kbench_mrg.py ;;
+        kbench_t8q) run kbench_t8q 300 python tools/kbench_t8q.py ;;
         kbench_mrg_words) run kbench_mrg_words 300 python tools/kbench_mrg_words.py ;;
         t8_order) run t8_order 300 python tools/t8_order_probe.py ;;
         single_call) run single_call 120 tools/_build/single_call_probe ;;

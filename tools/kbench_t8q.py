@@ -1,0 +1,97 @@
+"""The fused Table-8 kernel (hg_rand_gather_solve_f64: MRG32K3A draws + get_rand_list gather +
+cal_Homo_*, binary64; GPU_Runtime Test.cu:52-78, :81-240, :1443-1451) in its chunk shapes
+(round 5): positions per chunk Q (a lane solves Q / 4 hypotheses per
+chunk, one barrier per chunk) and lanes per block KB (the VGPR budget: 128 at 1024 lanes,
+168 at 768, 256 at 512), ACA and SKS at 10 M on the reference's wall pool, against the write-
+only stream of the same 720 MB.  Every variant's H is compared bit for bit with the shipped
+launch.  Device time per launch from events around back-to-back launches, interleaved rounds,
+median.
+    python tools/kbench_t8q.py   -> gpurun_out/kbench_t8q.json
+"""
+import ctypes
+import json
+import os
+import statistics
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import __graft_entry__ as ge  # noqa: E402
+
+ROUNDS = int(os.environ.get("KB_ROUNDS", "7"))
+VARIANTS = {  # hg_tune_rand_gather_solve_f64 variant -> shape
+    16: "Q4 KB1024 (r04 shape)", 20: "Q4 KB768", 15: "Q8 KB1024 (6 VGPRs spilled)",
+    18: "Q8 KB768", 19: "Q8 KB512",
+}
+
+
+def timeit(fns, loops):
+    for f in fns.values():
+        for _ in range(3):
+            f()
+    times = {k: [] for k in fns}
+    for _ in range(ROUNDS):
+        for k, f in fns.items():
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            for _ in range(loops):
+                f()
+            e1.record()
+            e1.synchronize()
+            times[k].append(e0.elapsed_time(e1) * 1e3 / loops)
+    return {k: (round(statistics.median(v), 2), round(min(v), 2)) for k, v in times.items()}
+
+
+def main():
+    pkg = ge.load_package()
+    lib = pkg.lib()
+    t = pkg._lib.tune()
+    vp, i64, u64 = ctypes.c_void_p, ctypes.c_int64, ctypes.c_uint64
+    t.hg_tune_rand_gather_solve_f64.argtypes = [ctypes.c_int, ctypes.c_int, vp, vp,
+                                                ctypes.c_uint32, u64, vp, i64, vp]
+    t.hg_tune_policy.argtypes = [ctypes.c_int, vp, vp, i64, vp]
+    dev = torch.device("cuda:0")
+    st = torch.cuda.current_stream(dev).cuda_stream
+    g = np.load(os.path.join(ROOT, "tests", "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"].astype(np.float64)).to(dev)
+    pt = torch.from_numpy(g["pool_tar"].astype(np.float64)).to(dev)
+    out = {"pool": int(ps.shape[0]), "rounds": ROUNDS}
+    n = int(os.environ.get("KB_N", "10000000"))
+    for algo, aid in (("aca", 0), ("sks", 1)):
+        H = {k: torch.empty((9, n), dtype=torch.float64, device=dev) for k in ["shipped", *VARIANTS]}
+        wsrc = torch.empty(n * 72 // 4, dtype=torch.float32, device=dev)
+        wdst = torch.empty_like(wsrc)
+        fns = {"shipped": lambda: lib.hg_rand_gather_solve_f64(aid, ps.data_ptr(), pt.data_ptr(),
+                                                               ps.shape[0], 11, H["shipped"].data_ptr(),
+                                                               n, 0, st),
+               "write_only_72B": lambda: t.hg_tune_policy(0, wsrc.data_ptr(), wdst.data_ptr(), n * 72, st)}
+        for v in VARIANTS:
+            fns[v] = (lambda v=v: t.hg_tune_rand_gather_solve_f64(v, aid, ps.data_ptr(), pt.data_ptr(),
+                                                                  ps.shape[0], 11, H[v].data_ptr(), n, st))
+        rc = {v: t.hg_tune_rand_gather_solve_f64(v, aid, ps.data_ptr(), pt.data_ptr(), ps.shape[0], 11,
+                                                 H[v].data_ptr(), n, st) for v in VARIANTS}
+        torch.cuda.synchronize()
+        r = timeit(fns, 5)
+        ref = H["shipped"].view(torch.int64)
+        w_us = r["write_only_72B"][0]
+        for k, (us, best) in r.items():
+            rec = {"us": us, "best_us": best, "ghyp_s": round(n / (us * 1e-6) / 1e9, 2),
+                   "frac_of_write_only_stream": round(w_us / us, 4),
+                   "frac_of_spec": round(n * 72 / (us * 1e-6) / 1e9 / 8000.0, 4)}
+            if k in VARIANTS:
+                rec["shape"] = VARIANTS[k]
+                rec["rc"] = rc[k]
+                rec["bit_exact_vs_shipped"] = bool(torch.equal(H[k].view(torch.int64), ref))
+            out[f"{algo} {k}"] = rec
+            print(f"{algo} {k}", rec, flush=True)
+        del H, wsrc, wdst
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "kbench_t8q.json"), "w") as fh:
+        json.dump(out, fh, indent=1)
+
+
+if __name__ == "__main__":
+    main()
