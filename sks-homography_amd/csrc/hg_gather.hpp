@@ -232,6 +232,8 @@ enum MrgAblation : int {
     kMrgAblNoGather = 8,  // no pool reads: the points are the words themselves
     kMrgSt16 = 16,        // H rows stored as 16-B pairs of adjacent hypotheses (n even)
     kMrgStDefault = 32,   // H stores with the default cache policy instead of non-temporal
+    kMrgStBuf = 64,       // H rows through buffer stores: a per-row resource in SGPRs and one
+                          // 32-bit lane offset (8 n < 2^32), instead of nine 64-bit lane addresses
 };
 
 // the value of the other lane of an even/odd lane pair (DPP quad_perm [1, 0, 3, 2])
@@ -382,6 +384,17 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
                     if (h < n) {
                         if constexpr ((ABL & kMrgStDefault) != 0) H[h + 8 * n] = hh[8];
                         else __builtin_nontemporal_store(hh[8], H + h + 8 * n);
+                    }
+                } else if constexpr ((ABL & kMrgStBuf) != 0) {
+                    const uint32_t off = (uint32_t)h * 8u;  // bytes into each row (8 n < 2^32)
+#pragma unroll
+                    for (int r = 0; r < 9; ++r) {
+                        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(H + (int64_t)r * n, 0,
+                                                                            (int)(uint32_t)(n * 8), 0x00020000);
+                        typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, hh[r]),
+                                                              rsrc, off, 0,
+                                                              (ABL & kMrgStDefault) != 0 ? 0 : 2);
                     }
                 } else if constexpr ((ABL & kMrgStDefault) != 0) {
 #pragma unroll
