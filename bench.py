@@ -1188,9 +1188,17 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
     wb = torch.empty(4 * big, dtype=torch.int32, device=d.dev)
     for algo in ("aca", "sks"):
         aid = {"aca": 0, "sks": 1}[algo]
-        Hb = torch.empty((9, big), dtype=torch.float64, device=d.dev)
-        f_one = lambda: pkg._lib.call("hg_rand_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(),  # noqa: E731
-                                      ps.shape[0], SEED, Hb.data_ptr(), big, 0, stream)
+        # three output buffers used in turn: the 10 M figure moves by up to +-10 % with where
+        # the 720 MB of H land (KERNEL_NOTES.md, tools/kbench_t8q.py), so the launch is timed
+        # over three placements rather than one
+        Hbs = [torch.empty((9, big), dtype=torch.float64, device=d.dev) for _ in range(3)]
+        Hb = Hbs[0]
+        turn = [0]
+
+        def f_one():
+            turn[0] = (turn[0] + 1) % len(Hbs)
+            pkg._lib.call("hg_rand_gather_solve_f64", aid, ps.data_ptr(), pt.data_ptr(),
+                          ps.shape[0], SEED, Hbs[turn[0]].data_ptr(), big, 0, stream)
 
         def f_two():
             pkg._lib.call("hg_rand_mrg32k3a_u32", wb.data_ptr(), 4 * big, SEED, stream)
@@ -1212,8 +1220,9 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
             "traffic": pmc_detail(f"rand_gather_solve_f64_{algo}"),
             "write_only_stream_gbps": round(big * 72 / (ms_write * 1e-3) / 1e9, 1),
             "frac_of_write_only_stream": round(ms_write / ms_one, 4),
-            "draws_then_gather_solve_us": round(ms_two * 1e3, 2)}
-        del Hb
+            "draws_then_gather_solve_us": round(ms_two * 1e3, 2),
+            "placements": len(Hbs)}
+        del Hb, Hbs
     del wbuf, wb
     return out
 
