@@ -88,10 +88,36 @@ struct Registration {
     int refs;
 };
 
+// A record of every page range the library registered (the last kHistory of them), with its
+// fate -- kept for fault diagnosis: a GPU fault on a host address can be matched against the
+// ranges this library mapped and unmapped (hg_internal_host_registry_find).  Updated under the
+// registry mutex.
+constexpr size_t kHistory = 4096;
+enum : int { kLive = 1, kReleased = 2, kReleaseFailed = 3 };
+struct HistoryEntry {
+    uint64_t lo = 0, hi = 0, seq = 0;
+    int state = 0, err = 0;
+};
+
 struct Registry {
     std::mutex mu;
     std::condition_variable released;
     std::vector<Registration> regs;
+    HistoryEntry history[kHistory];
+    uint64_t registered = 0;         // registrations made so far (history[registered % kHistory])
+    uint64_t unregister_failures = 0;
+    int last_failure = 0;
+
+    void note(uintptr_t lo, int state, int err) {
+        for (uint64_t k = 0; k < kHistory && k < registered; ++k) {  // newest first
+            HistoryEntry& h = history[(registered - 1 - k) % kHistory];
+            if (h.lo == lo && h.state == kLive) {
+                h.state = state;
+                h.err = err;
+                return;
+            }
+        }
+    }
 
     std::vector<host::Range> ranges() const {
         std::vector<host::Range> out;
@@ -113,7 +139,15 @@ struct Registry {
             for (size_t j = 0; j < regs.size(); ++j) {
                 if (regs[j].r.lo != base) continue;
                 if (--regs[j].refs == 0) {
-                    (void)hipHostUnregister(reinterpret_cast<void*>(regs[j].r.lo));
+                    // a failed unregistration would leave a mapping of pages the caller is about
+                    // to free or reuse: counted and recorded (hg_internal_host_registry_stats)
+                    const hipError_t e = hipHostUnregister(reinterpret_cast<void*>(regs[j].r.lo));
+                    if (e != hipSuccess) {
+                        ++unregister_failures;
+                        last_failure = (int)e;
+                        (void)hipGetLastError();
+                    }
+                    note(regs[j].r.lo, e == hipSuccess ? kReleased : kReleaseFailed, (int)e);
                     regs.erase(regs.begin() + (long)j);
                 }
                 break;
@@ -151,6 +185,8 @@ struct Registry {
                 }
                 regs.push_back({need[i], 1});
                 j = (long)regs.size() - 1;
+                HistoryEntry& h = history[registered % kHistory];
+                h = HistoryEntry{need[i].lo, need[i].hi, ++registered, kLive, 0};
             } else {
                 ++regs[(size_t)j].refs;
             }
@@ -267,6 +303,36 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
 }  // namespace
 
 extern "C" {
+
+// Library-internal diagnostics (not in the public header): {live registrations, registrations
+// made, unregistration failures, last failure code}.
+int hg_internal_host_registry_stats(int64_t* out) {
+    if (!out) return kInvalid;
+    Registry& reg = registry();
+    std::lock_guard<std::mutex> lock(reg.mu);
+    out[0] = (int64_t)reg.regs.size();
+    out[1] = (int64_t)reg.registered;
+    out[2] = (int64_t)reg.unregister_failures;
+    out[3] = reg.last_failure;
+    return 0;
+}
+
+// The newest recorded registration whose page range holds `va`: its range, sequence number
+// and state (1 live, 2 released, 3 release failed; 0 = none of the last 4096 holds it).
+int hg_internal_host_registry_find(uint64_t va, uint64_t* lo, uint64_t* hi, uint64_t* seq) {
+    Registry& reg = registry();
+    std::lock_guard<std::mutex> lock(reg.mu);
+    for (uint64_t k = 0; k < kHistory && k < reg.registered; ++k) {
+        const HistoryEntry& h = reg.history[(reg.registered - 1 - k) % kHistory];
+        if (va >= h.lo && va < h.hi) {
+            if (lo) *lo = h.lo;
+            if (hi) *hi = h.hi;
+            if (seq) *seq = h.seq;
+            return h.state;
+        }
+    }
+    return 0;
+}
 
 int hg_solve_host_f32(int algo, const float* src, const float* tar, float* H, int64_t n,
                       int layout, int flags, void* stream) {

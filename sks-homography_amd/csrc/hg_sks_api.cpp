@@ -4,6 +4,8 @@
 
 #include <chrono>
 #include <cstring>
+#include <mutex>
+#include <vector>
 
 #include "sks_aca_sks.hpp"
 
@@ -34,55 +36,91 @@ bool is_device_pointer(const void* p) {
 // space -- 16 values for H plus a completion word -- which the kernel writes directly.
 // The points go in the kernel arguments, so a call is one launch, and the thread then
 // spins on the completion word (the kernel stores it after H, system scope) instead of
-// waiting on the stream: ~half the latency of a stream synchronisation.  One slot per
-// device the thread has used; released when the thread exits.
+// waiting on the stream: ~half the latency of a stream synchronisation.
+//
+// Slots (one per device a thread uses) come from a process-wide pool and go back to it when
+// the thread exits; they are never freed.  So a thread's exit makes no HIP call (a HIP call
+// from a thread-local destructor runs after the runtime's and any tool's own per-thread
+// state may be gone -- under rocprofv3 it aborts the process), and the stream and mapped
+// memory a call may still have in flight -- the kernel retires after it has stored the
+// completion word -- stay valid: the next thread to take the slot orders its launch after
+// that kernel on the same stream.
+template <typename T>
+struct Slot {
+    static constexpr size_t kDoneOffset = 16 * sizeof(T);  // the completion word, after H
+    T* host = nullptr;
+    T* mapped = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t seq = 0;
+    volatile uint32_t* done_host() { return reinterpret_cast<volatile uint32_t*>(reinterpret_cast<char*>(host) + kDoneOffset); }
+    uint32_t* done_dev() { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(mapped) + kDoneOffset); }
+};
+
+constexpr int kMaxDevices = 64;
+
+template <typename T>
+struct SlotPool {
+    std::mutex mu;
+    std::vector<Slot<T>*> idle[kMaxDevices];
+
+    // A slot for `dev` on the calling thread's current device: an idle one, or a new one.
+    int take(int dev, Slot<T>*& out) {
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            if (!idle[dev].empty()) {
+                out = idle[dev].back();
+                idle[dev].pop_back();
+                return 0;
+            }
+        }
+        auto* sl = new Slot<T>();
+        hipError_t e = hipStreamCreateWithFlags(&sl->stream, hipStreamNonBlocking);
+        if (e == hipSuccess)
+            e = hipHostMalloc(reinterpret_cast<void**>(&sl->host), Slot<T>::kDoneOffset + 64,
+                              hipHostMallocMapped | hipHostMallocCoherent);
+        if (e == hipSuccess) {
+            *sl->done_host() = 0;
+            e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sl->mapped), sl->host, 0);
+        }
+        if (e != hipSuccess) {  // nothing half-made is kept
+            if (sl->host) (void)hipHostFree(sl->host);
+            if (sl->stream) (void)hipStreamDestroy(sl->stream);
+            delete sl;
+            return (int)e;
+        }
+        out = sl;
+        return 0;
+    }
+    void give_back(int dev, Slot<T>* sl) {
+        std::lock_guard<std::mutex> lock(mu);
+        idle[dev].push_back(sl);
+    }
+};
+
+template <typename T>
+SlotPool<T>& slot_pool() {
+    static SlotPool<T>* p = new SlotPool<T>();  // never destroyed: slots outlive every thread
+    return *p;
+}
+
 template <typename T>
 struct Scratch {
-    static constexpr int kMaxDevices = 64;
-    static constexpr size_t kDoneOffset = 16 * sizeof(T);  // the completion word, after H
-    struct Slot {
-        T* host = nullptr;
-        T* mapped = nullptr;
-        hipStream_t stream = nullptr;
-        uint32_t seq = 0;
-        volatile uint32_t* done_host() { return reinterpret_cast<volatile uint32_t*>(reinterpret_cast<char*>(host) + kDoneOffset); }
-        uint32_t* done_dev() { return reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(mapped) + kDoneOffset); }
-    };
-    Slot slot[kMaxDevices];
-    Slot* cur = nullptr;
+    Slot<T>* slot[kMaxDevices] = {};
+    int cur_dev = -1;
 
     int ensure() {
         int dev = 0;
-        hipError_t e = hipGetDevice(&dev);
+        const hipError_t e = hipGetDevice(&dev);
         if (e != hipSuccess) return (int)e;
         if (dev < 0 || dev >= kMaxDevices) return (int)hipErrorInvalidDevice;
-        Slot& sl = slot[dev];
-        cur = &sl;
-        if (sl.mapped) return 0;
-        if (!sl.stream && (e = hipStreamCreateWithFlags(&sl.stream, hipStreamNonBlocking)) != hipSuccess)
-            return (int)e;
-        if (!sl.host) {
-            if ((e = hipHostMalloc(reinterpret_cast<void**>(&sl.host), kDoneOffset + 64,
-                                   hipHostMallocMapped | hipHostMallocCoherent)) != hipSuccess)
-                return (int)e;
-            *sl.done_host() = 0;
-        }
-        if ((e = hipHostGetDevicePointer(reinterpret_cast<void**>(&sl.mapped), sl.host, 0)) !=
-            hipSuccess)
-            return (int)e;
-        return 0;
+        cur_dev = dev;
+        if (slot[dev]) return 0;
+        return slot_pool<T>().take(dev, slot[dev]);
     }
-    // A call returns once its completion word is visible, which the kernel stores last --
-    // the kernel may not have retired yet.  So the stream is drained before the mapped
-    // memory it writes is released (hipStreamDestroy does not wait for work in flight).
-    ~Scratch() {
-        for (Slot& sl : slot) {
-            if (sl.stream) {
-                (void)hipStreamSynchronize(sl.stream);
-                (void)hipStreamDestroy(sl.stream);
-            }
-            if (sl.host) (void)hipHostFree(sl.host);
-        }
+    Slot<T>& cur() { return *slot[cur_dev]; }
+    ~Scratch() {  // no HIP call: the slots go back to the pool
+        for (int d = 0; d < kMaxDevices; ++d)
+            if (slot[d]) slot_pool<T>().give_back(d, slot[d]);
     }
 };
 
@@ -100,7 +138,7 @@ using OneFn = int (*)(int, const T*, const T*, T*, int, uint32_t*, uint32_t, voi
 // Waits until the kernel has published H (*done == seq): a spin with pause, bounded; past
 // the bound (a fault, a stalled device) the stream's own status decides.
 template <typename T>
-int wait_done(typename Scratch<T>::Slot& sl, uint32_t seq) {
+int wait_done(Slot<T>& sl, uint32_t seq) {
     auto seen = [&] { return __atomic_load_n(sl.done_host(), __ATOMIC_ACQUIRE) == seq; };
     const auto t0 = std::chrono::steady_clock::now();
     for (uint32_t i = 0; !seen(); ++i) {
@@ -129,7 +167,7 @@ int solve_one(T* src, T* tar, T* result) {
     Scratch<T>& s = scratch<T>();
     int rc = s.ensure();
     if (rc) return rc;
-    auto& sl = *s.cur;
+    Slot<T>& sl = s.cur();
     const uint32_t seq = ++sl.seq ? sl.seq : ++sl.seq;  // never 0, the word's initial value
     if (ds || dt) {
         // mixed: stage device-resident inputs to the host first (rare)
@@ -143,8 +181,8 @@ int solve_one(T* src, T* tar, T* result) {
     }
     if (rc) return rc;
     if ((rc = wait_done<T>(sl, seq))) return rc;
-    if (dr) return (int)hipMemcpy(result, s.cur->host, 9 * sizeof(T), hipMemcpyHostToDevice);
-    std::memcpy(result, s.cur->host, 9 * sizeof(T));
+    if (dr) return (int)hipMemcpy(result, sl.host, 9 * sizeof(T), hipMemcpyHostToDevice);
+    std::memcpy(result, sl.host, 9 * sizeof(T));
     return 0;
 }
 

@@ -137,6 +137,31 @@ def _where(va):
                 out.append("maps: no mapping holds it")
     except OSError:
         pass
+    try:  # what HIP itself takes the address for (a registered or pinned host range?)
+        hip = _hip()
+        attrs = (ctypes.c_uint64 * 8)()
+        rc = hip.hipPointerGetAttributes(attrs, ctypes.c_void_p(va))
+        hip.hipGetLastError()
+        raw = ctypes.string_at(attrs, 40)
+        mtype = int.from_bytes(raw[0:4], "little")
+        out.append(f"hipPointerGetAttributes rc {rc} type {mtype} (0 unregistered, 1 host, 2 device, 3 "
+                   f"managed) device ptr 0x{int.from_bytes(raw[8:16], 'little'):x} host ptr "
+                   f"0x{int.from_bytes(raw[16:24], 'little'):x}")
+    except Exception as e:  # noqa: BLE001 -- diagnostics only
+        out.append(f"hipPointerGetAttributes unavailable: {e!r}"[:120])
+    try:  # the library's own page registrations (hg_host.cpp history)
+        lib = ctypes.CDLL(os.path.join(ROOT, "sks-homography_amd", "lib", "libsks_homography_amd.so"))
+        lo, hi, seq = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+        st = lib.hg_internal_host_registry_find(ctypes.c_uint64(va), ctypes.byref(lo), ctypes.byref(hi),
+                                                ctypes.byref(seq))
+        stats = (ctypes.c_int64 * 4)()
+        lib.hg_internal_host_registry_stats(stats)
+        state = {0: "never registered by the library (last 4096)", 1: "LIVE library registration",
+                 2: "library registration, released", 3: "library registration, RELEASE FAILED"}[st]
+        out.append(f"{state}" + (f" [0x{lo.value:x}, 0x{hi.value:x}) #{seq.value}" if st else "")
+                   + f"; registry: {stats[0]} live, {stats[1]} made, {stats[2]} unregister failures")
+    except Exception as e:  # noqa: BLE001 -- diagnostics only
+        out.append(f"registry history unavailable: {e!r}"[:120])
     try:
         import torch
         for seg in torch.cuda.memory_snapshot():

@@ -16,6 +16,18 @@ pytestmark = pytest.mark.gpu
 SEED = 5
 
 
+@pytest.fixture(autouse=True)
+def _registrations_released(pkg):
+    """After every host-memory test: no page registration of the library's is left, and none
+    failed to be released (hg_host.cpp; a leftover would map pages the caller frees or reuses)."""
+    yield
+    lib = pkg.lib()
+    stats = (ctypes.c_int64 * 4)()
+    assert lib.hg_internal_host_registry_stats(stats) == 0
+    assert stats[0] == 0, f"{stats[0]} registrations still live"
+    assert stats[2] == 0, f"{stats[2]} unregistrations failed (last hipError {stats[3]})"
+
+
 def _inputs(pkg, dev, n, dtype, layout, off=0):
     s = pkg.fill_uniform(n * 8, SEED, off, device=dev)
     t = pkg.fill_uniform(n * 8, SEED, off + n * 8, device=dev)
