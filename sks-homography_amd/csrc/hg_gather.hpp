@@ -234,6 +234,10 @@ enum MrgAblation : int {
     kMrgStDefault = 32,   // H stores with the default cache policy instead of non-temporal
     kMrgStBuf = 64,       // H rows through buffer stores: a per-row resource in SGPRs and one
                           // 32-bit lane offset (8 n < 2^32), instead of nine 64-bit lane addresses
+    kMrgInterleave = 128, // with kMrgStBuf: a chunk's gathers, then the NEXT chunk's draws, then
+                          // its solves, in one basic block (the chunk loop unrolled by the three
+                          // engine phases, the draws unconditional): the scheduler may overlap the
+                          // independent draw and solve chains (same bits)
 };
 
 // the value of the other lane of an even/odd lane pair (DPP quad_perm [1, 0, 3, 2])
@@ -332,6 +336,69 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
         const int64_t qn = (n - g * kC + mrg::kOrder - 1) >> mrg::kOrderLog2;
         gen(0, 0);
         __syncthreads();
+        if constexpr ((ABL & kMrgInterleave) != 0) {
+            static_assert((ABL & kMrgStBuf) != 0 && (ABL & ~(kMrgInterleave | kMrgStBuf)) == 0,
+                          "the interleaved chunk is the shipped one with buffer stores");
+            int buf = 0;
+            int64_t q0 = 0;
+            auto chunk = [&](auto pn) {  // pn: the engine phase of the NEXT chunk
+                constexpr int PN = decltype(pn)::value;
+                double s[kPer][8], t[kPer][8];
+#pragma unroll
+                for (int j = 0; j < kPer; ++j) {
+#pragma unroll
+                    for (int r = 0; r < 4; ++r) {
+                        const uint32_t w = words[((buf * 4 + r) * kQ + k + 4 * j) * kC + c];
+                        const uint32_t ix = fastmod_u32(w, magic, size);
+                        double2 ps, pt;
+                        if constexpr (POOL_LDS) {
+                            ps = pool[2 * ix];
+                            pt = pool[2 * ix + 1];
+                        } else {
+                            ps = pool_src[ix];
+                            pt = pool_tar[ix];
+                        }
+                        s[j][2 * r] = ps.x; s[j][2 * r + 1] = ps.y;
+                        t[j][2 * r] = pt.x; t[j][2 * r + 1] = pt.y;
+                    }
+                }
+                {  // the next chunk's words (past a group's last chunk: drawn, never read)
+                    uint32_t* w = words + ((buf ^ 1) * 4 + k) * kQ * kC + c;
+#pragma unroll
+                    for (int i = 0; i < kQ; ++i) w[i * kC] = mrg::step_at(st, (PN + i) % 3);
+                }
+#pragma unroll
+                for (int j = 0; j < kPer; ++j) {
+                    double hh[9];
+                    solve<ALGO, NORM>(s[j], t[j], hh);
+                    const int64_t h = h0 + ((q0 + k + 4 * j) << mrg::kOrderLog2);
+                    if (h < n) {
+                        const uint32_t off = (uint32_t)h * 8u;
+#pragma unroll
+                        for (int r = 0; r < 9; ++r) {
+                            const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+                                H + (int64_t)r * n, 0, (int)(uint32_t)(n * 8), 0x00020000);
+                            typedef unsigned u32x2v __attribute__((ext_vector_type(2)));
+                            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2v, hh[r]),
+                                                                  rsrc, off, 0, 2);
+                        }
+                    }
+                }
+                __syncthreads();
+                buf ^= 1;
+                q0 += kQ;
+            };
+            // chunk m's words are in phase (Q m) mod 3: unrolled by three, every phase is static
+            for (;;) {
+                chunk(std::integral_constant<int, (1 * kQ) % 3>());
+                if (q0 >= qn) break;
+                chunk(std::integral_constant<int, (2 * kQ) % 3>());
+                if (q0 >= qn) break;
+                chunk(std::integral_constant<int, 0>());
+                if (q0 >= qn) break;
+            }
+            continue;
+        }
         int buf = 0, phase = 0;
         for (int64_t q0 = 0; q0 < qn; q0 += kQ, buf ^= 1) {
             phase = (phase + kQ) % 3;  // the phase of chunk q0 / Q + 1

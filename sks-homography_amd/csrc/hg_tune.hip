@@ -970,6 +970,10 @@ static int rand_gather_variant(int variant, const double2* ps, const double2* pt
             return launch_rand_gather_solve<ALGO, false, kMrgStBuf, 4>(ps, pt, size, seed, H, n, s);
         case 22:  // Q = 8, buffer stores (8 n < 2^32)
             return launch_rand_gather_solve<ALGO, false, kMrgStBuf, 8>(ps, pt, size, seed, H, n, s);
+        case 23:  // Q = 4, buffer stores, draws of the next chunk interleaved with the solves
+            return launch_rand_gather_solve<ALGO, false, kMrgStBuf | kMrgInterleave, 4>(ps, pt, size, seed, H, n, s);
+        case 24:  // Q = 8, the same
+            return launch_rand_gather_solve<ALGO, false, kMrgStBuf | kMrgInterleave, 8>(ps, pt, size, seed, H, n, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -979,11 +983,11 @@ extern "C" {
 int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
                                   const double* pool_tar, uint32_t size, uint64_t seed, double* H,
                                   int64_t n, void* stream) {
-    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 22)
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 24)
         return (int)hipErrorInvalidValue;
     if ((variant == 10 || variant == 11 || variant == 14) && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15)))
         return (int)hipErrorInvalidValue;
-    if ((variant == 21 || variant == 22) && n >= (int64_t)1 << 29) return (int)hipErrorInvalidValue;
+    if (variant >= 21 && variant <= 24 && n >= (int64_t)1 << 29) return (int)hipErrorInvalidValue;
     const auto* ps = reinterpret_cast<const double2*>(pool_src);
     const auto* pt = reinterpret_cast<const double2*>(pool_tar);
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);

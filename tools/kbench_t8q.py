@@ -23,11 +23,12 @@ import __graft_entry__ as ge  # noqa: E402
 
 ROUNDS = int(os.environ.get("KB_ROUNDS", "7"))
 VARIANTS = {  # hg_tune_rand_gather_solve_f64 variant -> shape
-    16: "Q4 KB1024 (r04 shape)", 15: "Q8 KB1024 (6 VGPRs spilled)", 21: "Q4 KB1024 buffer stores",
+    16: "Q4 KB1024 (r04 shape)", 21: "Q4 KB1024 buffer stores (r05 shipped)",
+    23: "Q4 KB1024 buffer stores, next chunk's draws interleaved with the solves",
     22: "Q8 KB1024 buffer stores",
 }
 if os.environ.get("KB_ALL"):
-    VARIANTS.update({20: "Q4 KB768", 18: "Q8 KB768", 19: "Q8 KB512"})
+    VARIANTS.update({20: "Q4 KB768", 18: "Q8 KB768", 19: "Q8 KB512", 15: "Q8 KB1024 (6 VGPRs spilled)"})
 NBUF = int(os.environ.get("KB_NBUF", "3"))  # output buffers per variant, used in turn: the
 # 10 M figures move with where the 720 MB of H land (KERNEL_NOTES.md), so every variant is
 # timed over the same number of distinct placements
