@@ -43,6 +43,13 @@ int hg_tune_soa(int algo, int variant, const void* src, const void* tar, void* H
 int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int64_t B, float a,
                  float b, void* stream);
 
+/* TensorACA (B,3,4) backward with every gradient (gsrc, gtar, gterms (2,B,3); 16-B aligned,
+ * B % 64 == 0): 0 = the shipped staged kernel, 1 = its no-arithmetic twin (same loads and
+ * stores: the memory pattern's ceiling). */
+int hg_tune_rect_backward(int variant, const float* src, const float* tar, const float* gH,
+                          int64_t B, const float* scale, const float* div, float* gsrc,
+                          float* gtar, float* gterms, void* stream);
+
 /* q = a / b elementwise (n even) in packed pairs as the RANSAC samplers divide: packed != 0
  * the shipped expansion (div_rn, hg_solvers.hpp), 0 the compiler's scalar divisions. */
 int hg_tune_div_pairs(int packed, const float* a, const float* b, float* q, int64_t n,

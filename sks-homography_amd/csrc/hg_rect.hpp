@@ -363,7 +363,9 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_offsets_backward_kernel(
 // there, and the gradient rows leave as contiguous slabs (store_rows_staged) instead
 // of 48-B / 32-B per-lane strided accesses.  The ragged tail takes the per-lane code.
 // Same arithmetic (tensor_aca_rect_grad), same bits.
-template <bool WANT_SRC, int SD, bool NT, int ORDER = kAtenCpu>
+// NOSOLVE (tune only): the same loads and stores with the gradients replaced by a copy of the
+// loaded values -- the memory pattern's own ceiling.
+template <bool WANT_SRC, int SD, bool NT, int ORDER = kAtenCpu, bool NOSOLVE = false>
 __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
     int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
@@ -389,7 +391,21 @@ __global__ __launch_bounds__(kBlock) void tensor_aca_rect_backward_staged(
 #pragma unroll
         for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
         float gmx, gmy, gs, gd, gsr[3], gdr[3];
-        tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gs, gd, gsr, gdr);
+        if constexpr (NOSOLVE) {
+#pragma unroll
+            for (int q = 0; q < 12; ++q) gt[q] = tr[q] + g[q % 9];
+            gmx = mx + g[0];
+            gmy = my + g[1];
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                gsr[r] = tr[r] * g[r];
+                gdr[r] = tr[r + 4] * g[r + 3];
+            }
+            gs = gsr[0];
+            gd = gdr[0];
+        } else {
+            tensor_aca_rect_grad_rows<ORDER>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gs, gd, gsr, gdr);
+        }
         wave_lds_sync();  // the staging below reuses the input bytes
         store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
         if constexpr (WANT_SRC) {

@@ -615,6 +615,27 @@ int hg_tune_rect(int variant, const float* src, const float* tar, float* H, int6
     return (int)hipGetLastError();
 }
 
+// The TensorACA (B,3,4) backward with every gradient (dL/dsrc, dL/dtar and the (2,B,3) scale /
+// div terms; 16-B aligned buffers, B a multiple of 64): variant 0 the shipped staged kernel
+// (non-temporal), 1 its no-arithmetic twin -- the same loads and stores, the pattern's own
+// ceiling (tools/kbench_bwd.py).
+int hg_tune_rect_backward(int variant, const float* src, const float* tar, const float* gH,
+                          int64_t B, const float* scale, const float* div, float* gsrc,
+                          float* gtar, float* gterms, void* stream) {
+    if (B <= 0 || (B & 63) || !src || !tar || !gH || !scale || !div || !gsrc || !gtar || !gterms)
+        return (int)hipErrorInvalidValue;
+    hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+    const unsigned g = (unsigned)((B + kBlock - 1) / kBlock);
+    switch (variant) {
+        case 0: tensor_aca_rect_backward_staged<true, kSdTerms, true, kAtenCpu, false><<<g, kBlock, 0, st>>>(
+                    src, tar, gH, B, scale, div, gsrc, gtar, gterms); break;
+        case 1: tensor_aca_rect_backward_staged<true, kSdTerms, true, kAtenCpu, true><<<g, kBlock, 0, st>>>(
+                    src, tar, gH, B, scale, div, gsrc, gtar, gterms); break;
+        default: return (int)hipErrorInvalidValue;
+    }
+    return (int)hipGetLastError();
+}
+
 // cal_ACA's timing loop (GPU_Runtime Test.cu:1183-1200) in native code: `loops` back-to-
 // back launches of the C-ABI solver from a C++ loop, bracketed by HIP events on
 // `stream`.  Returns microseconds per launch, or -(hipError_t) on failure.  algo 0 ACA,

@@ -2,6 +2,7 @@
 per call from HIP-graph replays, algorithmic GB/s.  Bytes per problem: rect in tar 48 +
 src 8 + dL/dH 36, out dL/dtar 48 (+ dL/dsrc 48 + scale/div partials 8); compact in
 corner 8 + offsets 32 + dL/dH 36, out dL/doffsets 32 (+ dL/dcorner 8)."""
+import ctypes
 import json
 import os
 import statistics
@@ -53,6 +54,24 @@ def main():
             "offsets bwd (+corner)": (lambda: pkg.tensor_aca_offsets_backward(corner, offs, gH, 128.0, 128.0, True), 76 + 40),
             "offsets fwd": (lambda: pkg.tensor_aca_offsets(corner, offs, 128.0, 128.0), 76),
         }
+        if B % 64 == 0:  # the all-gradient kernel alone and its no-arithmetic twin (tune library)
+            t = pkg._lib.tune()
+            vp = ctypes.c_void_p
+            t.hg_tune_rect_backward.argtypes = [ctypes.c_int, vp, vp, vp, ctypes.c_int64, vp, vp, vp,
+                                                vp, vp, vp]
+            gs_, gt_ = torch.empty_like(src), torch.empty_like(tar)
+            terms = torch.empty((2, B, 3), device=dev)
+            cur = lambda: torch.cuda.current_stream(dev).cuda_stream  # noqa: E731 -- the capture stream
+            for v, name in ((0, "rect bwd kernel (all, raw)"), (1, "rect bwd kernel twin (no arithmetic)")):
+                cases[name] = ((lambda v=v: t.hg_tune_rect_backward(
+                    v, src.data_ptr(), tar.data_ptr(), gH.data_ptr(), B, sc.data_ptr(), dv.data_ptr(),
+                    gs_.data_ptr(), gt_.data_ptr(), terms.data_ptr(), cur())), 92 + 48 + 48 + 24)
+            # a copy of the same 252 B per problem (hg_stream_copy: half read, half written)
+            cbuf = torch.empty(B * 126 // 4, dtype=torch.float32, device=dev)
+            cdst = torch.empty_like(cbuf)
+            cases["copy yardstick (252 B per problem)"] = (
+                lambda: pkg._lib.call("hg_stream_copy", cbuf.data_ptr(), cdst.data_ptr(), B * 126, cur()),
+                252)
         res = {}
         for name, (fn, bpp) in cases.items():
             us = timed(fn, calls)
