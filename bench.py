@@ -1756,6 +1756,18 @@ def main():
                 f_bk()
             _, ms_bk = timed_region(d, f_bk, 20)
             del gs_k, gt_k, terms_k
+            # a plain copy of the same 252 B per problem (half read, half written): what the
+            # box's HBM gives this read/write mix with two streams instead of the layout's seven
+            cpy_src = torch.empty(big * RECT_BWD_ALL_LAYOUT_MIN_BYTES // 8, dtype=torch.float32,
+                                  device=d.dev)
+            cpy_dst = torch.empty_like(cpy_src)
+            f_cp = lambda: pkg._lib.call(  # noqa: E731
+                "hg_stream_copy", cpy_src.data_ptr(), cpy_dst.data_ptr(),
+                big * RECT_BWD_ALL_LAYOUT_MIN_BYTES // 2, stream_k)
+            for _ in range(5):
+                f_cp()
+            _, ms_cp = timed_region(d, f_cp, 20)
+            del cpy_src, cpy_dst
             # the opt-in torch-ROCm evaluation order (order="rocm"): the same kernels' forms with
             # the GPU's 3-term sums -- forward, dL/dtar alone, everything
             f_rf = lambda: pkg.ops.tensor_aca_rect(bs_h, bt_h, bsc, bdv, out=Hb, order="rocm")  # noqa
@@ -1790,6 +1802,9 @@ def main():
                 "large_backward_all_kernel_us": round(ms_bk * 1e3, 2),
                 "large_backward_all_kernel_layout_min_frac": round(
                     big * RECT_BWD_ALL_LAYOUT_MIN_BYTES / (ms_bk * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_all_copy_yardstick_us": round(ms_cp * 1e3, 2),
+                # > 1: the kernel moves its layout's bytes faster than a plain copy of them
+                "large_backward_all_kernel_vs_copy": round(ms_cp / ms_bk, 4),
                 "rocm_order": {
                     "large_us_per_call": round(ms_rf * 1e3, 2),
                     "large_frac": round(big * RECT_LAYOUT_MIN_BYTES / (ms_rf * 1e-3) / 1e9

@@ -39,9 +39,9 @@ KEYS = {
     "tensor_aca_rect": ("void hg::tensor_aca_rect_kernel", M16 * 92),
     "tensor_aca_rect_bcast": ("void hg::tensor_aca_rect_bcast_staged<true, 0>", M16 * 100),
     # dL/dtar alone: src M 8 + tar 48 + dL/dH 36 in, dL/dtar 48 out
-    "rect_backward_tar": ("void hg::tensor_aca_rect_backward_staged<false, 0, true, 0>", M16 * 140),
+    "rect_backward_tar": ("void hg::tensor_aca_rect_backward_staged<false, 0, true, 0, false>", M16 * 140),
     # + dL/dsrc 48 and the (problem, row) scale / div terms 24 out
-    "rect_backward_all": ("void hg::tensor_aca_rect_backward_staged<true, 2, true, 0>", M16 * 212),
+    "rect_backward_all": ("void hg::tensor_aca_rect_backward_staged<true, 2, true, 0, false>", M16 * 212),
     "aten_sum_l1": ("hg::aten_sum_l1", None),
     "tensor_aca_offsets": ("void hg::tensor_aca_offsets_kernel", M16 * 76),
     # corner 8 + offsets 32 + dL/dH 36 in, dL/doffsets 32 out
