@@ -10,6 +10,13 @@ import pytest
 # with it set before HIP starts, a fault's own report lands in the failing test's captured
 # stderr, which the driver's log tail shows.
 os.environ.setdefault("AMD_LOG_LEVEL", "1")
+# HIP copies a pageable host buffer of >= 2 MB by mapping the user's pages into the GPU's
+# address space in place (KFD shared-virtual-memory ranges over the heap) and keeps those
+# mappings after the copy; every GPU fault this suite ever had was such a copy writing a heap
+# page.  The tests' own .cpu() / .to() copies go through HIP's staging
+# buffers instead (the runtime reads this before it starts): no heap page of the test process
+# is mapped for the GPU except by the library's own host-memory calls, which are under test.
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "65536")  # MiB
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:

@@ -60,3 +60,50 @@ int hg_fault_probe_read(int* type, uint64_t* va, uint32_t* reason) {
     if (reason) *reason = g_reason;
     return g_events;
 }
+
+/* What ROCr itself holds at a host address (a query: no GPU access): its pointer type
+ * (hsa_amd_pointer_type_t: 0 unknown, 1 HSA allocation, 2 locked host memory, ...), the range
+ * it belongs to and the device address of that range.  HIP's pinned copies lock user pages
+ * through ROCr without telling hipPointerGetAttributes; this sees them.  Returns the status. */
+int hg_fault_probe_pointer(uint64_t va, uint32_t* type, uint64_t* host_base, uint64_t* agent_base,
+                           uint64_t* bytes) {
+    hsa_amd_pointer_info_t info;
+    info.size = sizeof(info);
+    hsa_status_t s = hsa_amd_pointer_info((void*)(uintptr_t)va, &info, NULL, NULL, NULL);
+    if (s != HSA_STATUS_SUCCESS) return (int)s;
+    if (type) *type = (uint32_t)info.type;
+    if (host_base) *host_base = (uint64_t)(uintptr_t)info.hostBaseAddress;
+    if (agent_base) *agent_base = (uint64_t)(uintptr_t)info.agentBaseAddress;
+    if (bytes) *bytes = (uint64_t)info.sizeInBytes;
+    return 0;
+}
+
+static hsa_status_t first_gpu(hsa_agent_t a, void* out) {
+    hsa_device_type_t t;
+    if (hsa_agent_get_info(a, HSA_AGENT_INFO_DEVICE, &t) == HSA_STATUS_SUCCESS &&
+        t == HSA_DEVICE_TYPE_GPU) {
+        *(hsa_agent_t*)out = a;
+        return HSA_STATUS_INFO_BREAK;
+    }
+    return HSA_STATUS_SUCCESS;
+}
+
+/* KFD's shared-virtual-memory view of [va, va + bytes) (hsa_amd_svm_attributes_get, a query):
+ * the first GPU's access (HSA_AMD_SVM_ATTRIB_AGENT_ACCESSIBLE 0x200, ..._IN_PLACE 0x201,
+ * ..._NO_ACCESS 0x202), the read-only and the global-flag attributes.  Returns the status
+ * (an error for a range KFD holds no SVM attributes for). */
+int hg_fault_probe_svm(uint64_t va, uint64_t bytes, uint64_t* access, uint64_t* read_only,
+                       uint64_t* global_flag) {
+    hsa_agent_t gpu = {0};
+    hsa_iterate_agents(first_gpu, &gpu);
+    if (!gpu.handle) return -1;
+    hsa_amd_svm_attribute_pair_t at[3] = {{HSA_AMD_SVM_ATTRIB_ACCESS_QUERY, gpu.handle},
+                                          {HSA_AMD_SVM_ATTRIB_READ_ONLY, 0},
+                                          {HSA_AMD_SVM_ATTRIB_GLOBAL_FLAG, 0}};
+    hsa_status_t s = hsa_amd_svm_attributes_get((void*)(uintptr_t)va, (size_t)bytes, at, 3);
+    if (s != HSA_STATUS_SUCCESS) return (int)s;
+    if (access) *access = at[0].attribute;
+    if (read_only) *read_only = at[1].value;
+    if (global_flag) *global_flag = at[2].value;
+    return 0;
+}

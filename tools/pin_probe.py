@@ -51,9 +51,126 @@ def main():
         print(json.dumps(rec), flush=True)
         out.append(rec)
         keep += [a, b, d]
+    out += interplay(kind, dev)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/pin_probe.json", "w") as fh:
         json.dump(out, fh, indent=1)
+
+
+def interplay(kind, dev):
+    """HIP's own pins beside the library's registrations of the same pages (hg_solve_host:
+    hipHostRegister of page-rounded ranges).  The GPU only READS pages shared with an earlier
+    pin here (H2D copies, the solver's src/tar reads), and every step asks ROCr itself what it
+    holds at the buffers (tests/fault_probe.c: hsa_amd_pointer_info, a host-side query) --
+    HIP's cached copy pins are invisible to hipPointerGetAttributes."""
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    fp = ctypes.CDLL(os.path.join(root, "tests", "_build", "libfault_probe.so"))
+    u32, u64 = ctypes.c_uint32, ctypes.c_uint64
+    fp.hg_fault_probe_pointer.argtypes = [u64, ctypes.POINTER(u32), ctypes.POINTER(u64),
+                                          ctypes.POINTER(u64), ctypes.POINTER(u64)]
+    fp.hg_fault_probe_svm.argtypes = [u64, u64] + [ctypes.POINTER(u64)] * 3
+    assert fp.hg_fault_probe_install() == 0
+
+    def rocr(p):
+        t, hb, ab, nb = u32(), u64(), u64(), u64()
+        rc = fp.hg_fault_probe_pointer(p, ctypes.byref(t), ctypes.byref(hb), ctypes.byref(ab),
+                                       ctypes.byref(nb))
+        acc, ro, gf = u64(), u64(), u64()
+        src = fp.hg_fault_probe_svm(p // 4096 * 4096, 4096, ctypes.byref(acc), ctypes.byref(ro),
+                                    ctypes.byref(gf))
+        return {"rc": rc, "type": t.value, "host_base": hex(hb.value), "agent_base": hex(ab.value),
+                "bytes": hex(nb.value), "svm_rc": src, "svm_access": hex(acc.value),
+                "svm_read_only": ro.value, "svm_global_flag": gf.value}
+
+    n = 200_003  # 6.4 MB of src: HIP pins its copies in place (>= 2 MB)
+    ds = pkg.fill_uniform(n * 8, 3, 0, device=dev).view(n, 8)
+    dt = pkg.fill_uniform(n * 8, 3, n * 8, device=dev).view(n, 8)
+    want = pkg.solve("aca", ds, dt).cpu()
+    recs = []
+    keep = []
+    src, tar = None, None
+
+    def step(tag, fn):
+        print(f"--- {tag}", file=sys.stderr, flush=True)
+        fn()
+        torch.cuda.synchronize()
+        rec = {"step": tag, "src_hip_kind": kind(src.data_ptr()),
+               "rocr_src": rocr(src.data_ptr()), "rocr_src_slice": rocr(src[1000].data_ptr()),
+               "rocr_tar": rocr(tar.data_ptr())}
+        print(json.dumps(rec), flush=True)
+        recs.append(rec)
+
+    def d2h():
+        nonlocal src, tar
+        src, tar = ds.cpu(), dt.cpu()
+
+    step("D2H into fresh src, tar (HIP pins their pages for the copy)", d2h)
+    step("library solve_host on slices inside those pages (registers, releases)",
+         lambda: keep.append(pkg.solve_host("aca", src[1000:150_000], tar[1000:150_000])))
+    # no further GPU access to src / tar: if the release above took HIP's pin with it, HIP's
+    # next copy through that pin would fault -- the ROCr queries answer without one
+    ok = torch.equal(keep[0], want[1000:150_000])
+    recs.append({"solve_host_bits_equal_device_solve": bool(ok)})
+    print(json.dumps(recs[-1]), flush=True)
+
+    # registration and release alone (no GPU access), against a fresh HIP copy pin each time:
+    # the same page range, a range inside it, a range around it
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipHostRegister.argtypes = [ctypes.c_void_p, ctypes.c_size_t, ctypes.c_uint]
+    hip.hipHostUnregister.argtypes = [ctypes.c_void_p]
+    page = 4096
+    for case in ("same range", "inside", "around"):
+        x = ds.cpu()  # fresh pageable memory: HIP pins it for the copy
+        keep.append(x)
+        lo, hi = x.data_ptr() // page * page, -(-(x.data_ptr() + x.numel() * 4) // page) * page
+        pin = rocr(x.data_ptr())
+        if case == "same range":
+            r_lo, r_hi = int(pin["host_base"], 16), int(pin["host_base"], 16) + int(pin["bytes"], 16)
+        elif case == "inside":
+            r_lo, r_hi = lo + 16 * page, hi - 16 * page
+        else:
+            r_lo, r_hi = lo - 4 * page, hi + 4 * page  # the neighbours' pages too (heap)
+        rc_r = hip.hipHostRegister(r_lo, r_hi - r_lo, 3)
+        during = rocr(x.data_ptr() + 20 * page)
+        rc_u = hip.hipHostUnregister(r_lo)
+        hip.hipGetLastError()
+        rec = {"case": case, "pin_before": pin, "registered": [hex(r_lo), hex(r_hi - r_lo), rc_r],
+               "during": during, "unregister_rc": rc_u, "after": rocr(x.data_ptr() + 20 * page)}
+        print(json.dumps(rec), flush=True)
+        recs.append(rec)
+
+    # pages no HIP copy ever touched: CPU-filled memory, registered and released directly
+    y = torch.arange(2_000_000, dtype=torch.float32) + 1  # 8 MB, written by the CPU only
+    keep.append(y)
+    y_lo = -(-y.data_ptr() // page) * page
+    y_n = (y.numel() * 4 - page) // page * page
+    before = rocr(y_lo + 8 * page)
+    rc_r = hip.hipHostRegister(y_lo, y_n, 3)
+    during = rocr(y_lo + 8 * page)
+    rc_u = hip.hipHostUnregister(y_lo)
+    hip.hipGetLastError()
+    rec = {"case": "fresh CPU pages, register + unregister", "before": before,
+           "register_rc": rc_r, "during": during, "unregister_rc": rc_u,
+           "after": rocr(y_lo + 8 * page)}
+    print(json.dumps(rec), flush=True)
+    recs.append(rec)
+    # the same through the library: a batch whose src / tar / H are CPU-filled pages
+    m = 100_000
+    s2 = src[:m].clone()
+    t2 = tar[:m].clone()
+    h2 = torch.full((m, 9), float("nan"))
+    keep += [s2, t2, h2]
+    b2 = {"src": rocr(s2.data_ptr() + 8 * page), "H": rocr(h2.data_ptr() + 8 * page)}
+    pkg.solve_host("aca", s2, t2, out=h2)
+    rec = {"case": "library solve_host on CPU-filled pages", "before": b2,
+           "after": {"src": rocr(s2.data_ptr() + 8 * page), "H": rocr(h2.data_ptr() + 8 * page)},
+           "bits_equal": bool(torch.equal(h2, want[:m]))}
+    print(json.dumps(rec), flush=True)
+    recs.append(rec)
+    return recs
 
 
 if __name__ == "__main__":
