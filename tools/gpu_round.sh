@@ -174,6 +174,9 @@ for step in $STEPS; do
         kbench_soa_small) run kbench_soa_small 300 python tools/kbench_soa_small.py ;;
         launch_floor) run launch_floor 300 python tools/launch_floor.py ;;
         kbench_bwd) run kbench_bwd 300 python tools/kbench_bwd.py ;;
+        pin_probe)  # which host copies HIP maps in place, and what KFD keeps mapped
+            AMD_LOG_LEVEL=4 run pin_probe 120 python tools/pin_probe.py
+            cp "$OUT/pin_probe.json" "$OUT/pin_probe_$TAG.json" 2>/dev/null || true ;;
         hbm_ceilings) run hbm_ceilings 300 python tools/hbm_ceilings.py ;;
         kbench_f64) run kbench_f64 300 python tools/kbench_f64.py ;;
         soa_streams) run soa_streams 300 python tools/soa_streams.py ;;

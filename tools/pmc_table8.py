@@ -1,7 +1,8 @@
 """Workload for a counter pass over the fused Table-8 pipeline (MRG32K3A draws + get_rand_list
 gather + cal_Homo_*, binary64, hg_rand_gather_solve_f64; GPU_Runtime Test.cu:52-78, :81-240,
 :1443-1451) at the bench size: 10 M hypotheses over the reference's wall pool, 3 ACA then 3
-SKS launches (tools/gpu_round.sh pmc_table8).
+SKS launches (tools/gpu_round.sh pmc_table8); then 3 launches of the seeded f32 sampler
+(hg_sample_solve_seeded_f32) at its bench size, 16 M.
 `--reduce <counter_collection.csv> [out.json]` turns the pass into per-kernel figures: VALU
 wave-instructions per hypothesis-wave (64 hypotheses), VALU busy against the CU's busy cycles
 (a wave64 VALU instruction holds a SIMD 4 cycles at full rate), waves resident per SIMD
@@ -16,6 +17,8 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 N = 10_000_000
+SEEDED_N = 16 << 20
+SEEDED = "sample_solve_lds_kernel<0, true, 2, 0, 4, 1"  # the seeded ACA instantiation
 CUS = 256
 
 
@@ -36,6 +39,13 @@ def run():
             else:
                 pkg.rand_gather_solve_variant(ps, pt, N, 11, algo, variant)
         torch.cuda.synchronize()
+    # the seeded f32 sampler at its bench size (16 M hypotheses, the draws made in the kernel,
+    # hg_sample_solve_seeded_f32; VERDICT r04 item 3 asks for the same reading)
+    ps32 = torch.from_numpy(g["pool_src"]).to(dev)
+    pt32 = torch.from_numpy(g["pool_tar"]).to(dev)
+    for _ in range(3):
+        pkg.sample_solve_seeded(ps32, pt32, SEEDED_N, 7, 0)
+    torch.cuda.synchronize()
     print("pmc_table8 done")
 
 
@@ -43,7 +53,7 @@ def reduce(path):
     per, meta = {}, {}
     for r in csv.DictReader(open(path)):
         name = r["Kernel_Name"]
-        if "mrg_gather_solve" not in name:
+        if "mrg_gather_solve" not in name and SEEDED not in name:
             continue
         per.setdefault(name, {}).setdefault(r["Dispatch_Id"], {})[r["Counter_Name"]] = float(r["Counter_Value"])
         meta[name] = {k: r.get(k) for k in ("Grid_Size", "Workgroup_Size", "VGPR_Count", "Accum_VGPR_Count",
@@ -52,7 +62,7 @@ def reduce(path):
     for name, disp in per.items():
         keys = sorted(set().union(*disp.values()))
         med = {k: statistics.median(d[k] for d in disp.values() if k in d) for k in keys}
-        hw = N / 64  # hypothesis-waves
+        hw = (SEEDED_N if SEEDED in name else N) / 64  # hypothesis-waves
         busy = med.get("SQ_BUSY_CU_CYCLES", 0) / CUS
         derived = {"valu_wave_instr_per_hypothesis_wave": round(med["SQ_INSTS_VALU"] / hw, 1)}
         if "SQ_INSTS_SALU" in med:
