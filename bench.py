@@ -23,6 +23,13 @@ import sys
 import threading
 import time
 
+# HIP maps pageable host buffers of >= 2 MB in place for its copies and KFD keeps those mappings;
+# such a copy writing a reused heap page is the one GPU fault this project's runs ever had
+# (DESIGN.md section 10).  This process's own .cpu() / .to() copies of pageable memory go through
+# HIP's staging buffers instead (read when the runtime starts; no timed region copies pageable
+# memory: the staged host-boundary baseline uses pinned buffers).
+os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "65536")  # MiB
+
 import numpy as np
 import torch
 
