@@ -156,6 +156,18 @@ def _where(va):
                    f"0x{int.from_bytes(raw[16:24], 'little'):x}")
     except Exception as e:  # noqa: BLE001 -- diagnostics only
         out.append(f"hipPointerGetAttributes unavailable: {e!r}"[:120])
+    try:  # KFD's view of the page: HIP's in-place copies and registrations live here
+        probe = _fault_probe()
+        if probe is not None:
+            u64 = ctypes.c_uint64
+            probe.hg_fault_probe_svm.argtypes = [u64, u64] + [ctypes.POINTER(u64)] * 3
+            acc, ro, gf = u64(), u64(), u64()
+            rc = probe.hg_fault_probe_svm(va // 4096 * 4096, 4096, ctypes.byref(acc), ctypes.byref(ro),
+                                          ctypes.byref(gf))
+            out.append(f"SVM attributes rc {rc} access 0x{acc.value:x} (0x200 accessible, 0x201 in "
+                       f"place, 0x202 none) read-only {ro.value} global flag {gf.value}")
+    except Exception as e:  # noqa: BLE001 -- diagnostics only
+        out.append(f"SVM attributes unavailable: {e!r}"[:120])
     try:  # the library's own page registrations (hg_host.cpp history)
         lib = ctypes.CDLL(os.path.join(ROOT, "sks-homography_amd", "lib", "libsks_homography_amd.so"))
         lo, hi, seq = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
