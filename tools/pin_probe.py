@@ -19,6 +19,27 @@ import torch
 SIZES_MB = [0.0625, 1, 2, 4, 5.76, 8, 16, 33, 64, 129]
 
 
+def svm_query():
+    """KFD's SVM access attribute of the page holding a host address (tests/fault_probe.c),
+    or None when the probe library is not built."""
+    path = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests",
+                        "_build", "libfault_probe.so")
+    if not os.path.exists(path):
+        return None
+    fp = ctypes.CDLL(path)
+    u64 = ctypes.c_uint64
+    fp.hg_fault_probe_svm.argtypes = [u64, u64] + [ctypes.POINTER(u64)] * 3
+    if fp.hg_fault_probe_install() != 0:
+        return None
+
+    def q(p):
+        acc, ro, gf = u64(), u64(), u64()
+        rc = fp.hg_fault_probe_svm(p // 4096 * 4096, 4096, ctypes.byref(acc), ctypes.byref(ro),
+                                   ctypes.byref(gf))
+        return hex(acc.value) if rc == 0 else f"rc {rc}"
+    return q
+
+
 def main():
     hip = ctypes.CDLL("libamdhip64.so")
     hip.hipPointerGetAttributes.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
@@ -31,7 +52,8 @@ def main():
 
     dev = torch.device("cuda:0")
     torch.ones(1, device=dev)
-    out = []
+    svm = svm_query()
+    out = [{"GPU_PINNED_MIN_XFER_SIZE": os.environ.get("GPU_PINNED_MIN_XFER_SIZE")}]
     keep = []  # nothing freed during the probe: no address is reused
     for mb in SIZES_MB:
         n = int(mb * 2**20) // 4
@@ -48,12 +70,17 @@ def main():
         ok = bool(torch.equal(a, b))
         rec = {"mb": mb, "h2d_src_kind_after": ka, "d2h_dst_kind_after": kb, "equal": ok,
                "src": hex(a.data_ptr()), "dst": hex(b.data_ptr())}
+        if svm is not None:  # 0x202: no GPU access; 0x201: the GPU maps the page in place
+            rec["svm_src_after"] = svm(a.data_ptr() + a.numel() * 2)
+            rec["svm_dst_after"] = svm(b.data_ptr() + b.numel() * 2)
         print(json.dumps(rec), flush=True)
         out.append(rec)
         keep += [a, b, d]
-    out += interplay(kind, dev)
+    if not os.environ.get("PIN_PROBE_SIZES_ONLY"):
+        out += interplay(kind, dev)
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/pin_probe.json", "w") as fh:
+    tag = os.environ.get("PIN_PROBE_TAG", "")
+    with open(f"gpurun_out/pin_probe{tag}.json", "w") as fh:
         json.dump(out, fh, indent=1)
 
 
