@@ -46,6 +46,7 @@ _FIRST = [  # (file, test name prefix): BASELINE configs and the reference's own
     ("test_gpu_config5.py", "test_config5_rank_blocks"),                          # configs[4]
     ("test_gpu_parity.py", "test_golden_"),
     ("test_gpu_parity.py", "test_full_size_10m_bit_exact"),
+    ("test_gpu_copies.py", ""),  # before any library host call maps heap pages
     ("test_gpu_parity.py", "test_rect_backward_kernel_vs_oracle"),
 ]
 _PARITY_FILES = [

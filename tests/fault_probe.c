@@ -46,11 +46,16 @@ static hsa_status_t on_event(const hsa_amd_event_t* e, void* data) {
     return HSA_STATUS_SUCCESS;
 }
 
-/* 0 when the handler is in place, else the HSA status (no GPU: hsa_init fails). */
+/* 0 when the handler is in place, else the HSA status (no GPU: hsa_init fails).  A second
+ * call (another loader of this library in the same process) changes nothing. */
 int hg_fault_probe_install(void) {
+    static int installed = 0;
+    if (installed) return 0;
     hsa_status_t s = hsa_init();
     if (s != HSA_STATUS_SUCCESS) return (int)s;
-    return (int)hsa_amd_register_system_event_handler(on_event, NULL);
+    s = hsa_amd_register_system_event_handler(on_event, NULL);
+    if (s == HSA_STATUS_SUCCESS) installed = 1;
+    return (int)s;
 }
 
 /* Events seen so far; the first one's type, address and reason bits. */
