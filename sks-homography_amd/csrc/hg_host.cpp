@@ -3,12 +3,15 @@
 // link directions carry traffic at once and no device buffer is needed.  Measured at 10 M
 // f32 AoS (tools/host_probe.py, profiles/r01/host_probe.json): 12.0 ms pinned and 13.4 ms
 // pageable, against 17.7 / 18.8 ms for H2D + solve + D2H on one stream; the H2D direction
-// alone takes 11.7 ms, so the call runs at the PCIe read bound.
+// alone takes 11.7 ms, so the call runs at the PCIe read bound.  Batches whose pageable
+// buffers fit kStageBytes are copied through library-owned pinned memory instead of being
+// registered (cheaper than the registration below that size).
 #include <hip/hip_runtime_api.h>
 
 #include <algorithm>
 #include <condition_variable>
 #include <cstdint>
+#include <cstring>
 #include <mutex>
 #include <unistd.h>
 #include <vector>
@@ -216,6 +219,64 @@ Registry& registry() {
     return r;
 }
 
+// Small batches: the pageable buffers are copied through library-owned pinned memory instead
+// of being registered.  Registering and releasing three page ranges costs ≈ 6 µs a call
+// (INTEGRATION.md §1), more than copying up to kStageBytes, and leaves the caller's pages alone:
+// KFD keeps registered pages mapped for the GPU after their release.  Stages
+// come from a process-wide pool and are never freed, so no HIP call runs at thread or process
+// exit.
+constexpr size_t kStageBytes = 128 << 10;
+constexpr size_t kStageAlign = 256;
+
+struct Stage {
+    char* host = nullptr;  // pinned, mapped
+    char* dev = nullptr;   // its device address
+};
+
+struct StagePool {
+    std::mutex mu;
+    std::vector<Stage*> idle;
+
+    int take(Stage*& out) {
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            if (!idle.empty()) {
+                out = idle.back();
+                idle.pop_back();
+                return 0;
+            }
+        }
+        auto* st = new Stage();
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), kStageBytes, hipHostMallocMapped);
+        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->dev), st->host, 0);
+        if (e != hipSuccess) {  // nothing half-made is kept
+            if (st->host) (void)hipHostFree(st->host);
+            delete st;
+            return (int)e;
+        }
+        out = st;
+        return 0;
+    }
+    void give_back(Stage* st) {
+        std::lock_guard<std::mutex> lock(mu);
+        idle.push_back(st);
+    }
+};
+
+StagePool& stage_pool() {
+    static StagePool* p = new StagePool();  // never destroyed
+    return *p;
+}
+
+size_t stage_round(size_t b) { return (b + kStageAlign - 1) / kStageAlign * kStageAlign; }
+
+// Bytes a batch's pageable views take in a stage (each at a kStageAlign boundary).
+size_t staged_bytes(const std::vector<View*>& pageable) {
+    size_t b = 0;
+    for (const View* x : pageable) b += stage_round(x->bytes);
+    return b;
+}
+
 // The solvers with the host-memory cache policy (hg_kernels.hip, library-internal).
 extern "C" int hg_internal_solve_host_f32(int, const float*, const float*, float*, int64_t, int,
                                           int, void*);
@@ -286,6 +347,28 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
         const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
         return rc ? rc : (int)e;
     };
+    if (!pageable.empty() && staged_bytes(pageable) <= kStageBytes) {
+        lock.unlock();  // no registration: the registry is not involved
+        Stage* st = nullptr;
+        int rc = stage_pool().take(st);
+        if (rc) return rc;
+        size_t off = 0, h_off = 0;
+        bool h_staged = false;
+        for (View* x : pageable) {
+            if (x == &v[2]) {  // H: written by the kernel into the stage, copied out after
+                h_staged = true;
+                h_off = off;
+            } else {
+                std::memcpy(st->host + off, x->host, x->bytes);
+            }
+            x->dev = st->dev + off;
+            off += stage_round(x->bytes);
+        }
+        rc = run();
+        if (rc == 0 && h_staged) std::memcpy(H, st->host + h_off, v[2].bytes);
+        stage_pool().give_back(st);
+        return rc;
+    }
     std::vector<uintptr_t> held;
     if (!pageable.empty()) {
         const int rc = reg.acquire(pageable, held, lock);

@@ -238,6 +238,69 @@ def test_host_full_size(pkg, dev):
     assert torch.equal(_bits(got), _bits(want))
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_small_pageable_batches_are_staged(pkg, dev, dtype, layout):
+    """Batches whose pageable buffers fit the library's 128 KiB stage (hg_host.cpp kStageBytes)
+    are copied through library-owned pinned memory, not registered: bits equal the device
+    solve for every solver, ragged sizes up to the stage's edge and just past it, H at a 4-B
+    offset; the staged calls make no page registration at all."""
+    lib = pkg.lib()
+    stats = (ctypes.c_int64 * 4)()
+    algos = ["aca", "sks", "ge"] + (["gpt"] if dtype is torch.float64 else [])
+    per = 100 if dtype is torch.float32 else 200  # bytes a problem stages (src + tar + H)
+    edge = (128 << 10) // per - 16
+    for n in (1, 2, 7, 64, 100, 1000 if dtype is torch.float32 else 500, edge, edge + 40):
+        ds, dt = _inputs(pkg, dev, n, dtype, layout, off=n)
+        hs, ht = ds.cpu(), dt.cpu()
+        for algo in algos:
+            want = pkg.solve(algo, ds, dt, normalize=True, layout=layout).cpu()
+            buf = torch.full((want.numel() + 1,), float("nan"), dtype=dtype)
+            out = buf[1:].view(want.shape)  # one element past the allocation's start
+            assert lib.hg_internal_host_registry_stats(stats) == 0
+            made = stats[1]
+            got = pkg.solve_host(algo, hs, ht, normalize=True, layout=layout, out=out)
+            assert got is out
+            assert torch.equal(_bits(got), _bits(want)), (n, algo)
+            assert lib.hg_internal_host_registry_stats(stats) == 0
+            staged = n <= edge
+            assert (stats[1] == made) == staged, (n, "staged" if staged else "registered", stats[1] - made)
+
+
+def test_small_pageable_batches_from_threads(pkg, dev):
+    """Eight threads, each 60 small pageable calls (staged through pooled stages), one of them
+    with pinned inputs and a pageable H: every result bit-exact, no registration made."""
+    lib = pkg.lib()
+    stats = (ctypes.c_int64 * 4)()
+    jobs = []
+    for k in range(8):
+        n = 37 + 113 * k
+        ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=7 * k)
+        hs, ht = ds.cpu(), dt.cpu()
+        if k == 3:
+            hs, ht = hs.pin_memory(), ht.pin_memory()
+        jobs.append((hs, ht, pkg.solve("sks", ds, dt).cpu()))
+    assert lib.hg_internal_host_registry_stats(stats) == 0
+    made = stats[1]
+    bad = []
+
+    def work(k):
+        s, t, want = jobs[k]
+        for _ in range(60):
+            got = pkg.solve_host("sks", s, t)
+            if not torch.equal(_bits(got), _bits(want)):
+                bad.append(k)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad
+    assert lib.hg_internal_host_registry_stats(stats) == 0
+    assert stats[1] == made, f"{stats[1] - made} registrations made by staged calls"
+
+
 def test_host_entry_errors(pkg, dev):
     lib = pkg.lib()
     s = torch.zeros((4, 8))
