@@ -347,11 +347,18 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
         const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
         return rc ? rc : (int)e;
     };
+    Stage* st = nullptr;
     if (!pageable.empty() && staged_bytes(pageable) <= kStageBytes) {
+        // a stage that cannot be made (pinned memory exhausted) leaves the call to the
+        // registration below, with the allocation's own error cleared
+        if (stage_pool().take(st) != 0) {
+            st = nullptr;
+            (void)hipGetLastError();
+        }
+    }
+    if (st) {
         lock.unlock();  // no registration: the registry is not involved
-        Stage* st = nullptr;
-        int rc = stage_pool().take(st);
-        if (rc) return rc;
+        int rc = 0;
         size_t off = 0, h_off = 0;
         bool h_staged = false;
         for (View* x : pageable) {
