@@ -247,7 +247,9 @@ struct StagePool {
             }
         }
         auto* st = new Stage();
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), kStageBytes, hipHostMallocMapped);
+        // coherent (fine-grained): the GPU never holds a stale line of a stage another call refilled
+        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), kStageBytes,
+                                     hipHostMallocMapped | hipHostMallocCoherent);
         if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->dev), st->host, 0);
         if (e != hipSuccess) {  // nothing half-made is kept
             if (st->host) (void)hipHostFree(st->host);
