@@ -763,6 +763,58 @@ def cpu_baseline(n_sample: int):
     return rec
 
 
+def config0_check(pkg, dev, n: int = 1000) -> dict:
+    """BASELINE configs[0]: ACA on 1 000 problems (seed SEED), the reference's own compiled
+    C++ (oracle/_ref, the checker of the cpu_baseline leg) against the GPU kernel's bits."""
+    orc = ge.load_oracle()
+    gen = orc.Oracle()
+    s = gen.fill_uniform(n * 8, SEED, 0).reshape(n, 8)
+    t = gen.fill_uniform(n * 8, SEED, n * 8).reshape(n, 8)
+    got = pkg.solve("aca", torch.from_numpy(s).to(dev), torch.from_numpy(t).to(dev),
+                    normalize=True).cpu().numpy()
+    ref = orc.RefOracle() if orc.RefOracle.available() else None
+    want = ref.solve("aca", s, t) if ref else gen.solve("aca", s, t)
+    return {"n": n, "checker": "reference" if ref else "port",
+            "bit_exact": bool(np.array_equal(got.view(np.uint32), want.view(np.uint32)))}
+
+
+def baseline_configs(line: dict, args, world: int) -> dict:
+    """One compact entry per BASELINE.json config, drawn from the sections above, printed at
+    the END of the line so that a tail of it shows all five."""
+    def get(*path):
+        x = line
+        for k in path:
+            if not isinstance(x, dict) or k not in x:
+                return None
+            x = x[k]
+        return x
+
+    def tb(tr):
+        return tr.get("traffic_bytes") if isinstance(tr, dict) else tr
+
+    head = get("config", "algo") == "aca" and get("config", "layout") == "aos" and get("dtype") == "f32"
+    c0 = get("cpu_baseline", "config0_n1000")
+    return {
+        "c0_aca_n1000_cpu": ({"bit_exact": c0.get("bit_exact"), "checker": c0.get("checker"),
+                              "ref_cpu_M_H_s": get("cpu_baseline", "value")} if c0 else
+                             {"bit_exact": None, "reason": "cpu leg runs at N=1 on rank 0 only"}),
+        "c1_aca_10M": ({"M_H_s": get("value"), "frac": get("roofline", "frac"),
+                        "traffic_B": tb(get("roofline", "traffic"))} if head else None),
+        "c2_sks_10M": {"M_H_s": get("sks", "value"), "frac": get("sks", "frac"),
+                       "traffic_B": tb(get("sks", "traffic")),
+                       "sks_over_aca_time": get("sks", "sks_over_aca_time")},
+        "c3_tensor_aca_64K": {"us": get("tensor_aca_rect", "us_per_call"),
+                              "torch_us": get("tensor_aca_rect", "torch_composed_us_per_call"),
+                              "graph_us": get("tensor_aca_rect", "graph_us_per_call"),
+                              "torch_graph_us": get("tensor_aca_rect", "torch_composed_graph_us_per_call"),
+                              "large_16M_frac": get("tensor_aca_rect", "large_frac")},
+        "c4_aca_80M_8gpu": ({"n_gpus": world, "M_H_s": get("value"), "global_batch": get("config", "global_batch")}
+                            if world == 8 else
+                            {"n_gpus": world, "M_H_s": None,
+                             "reason": f"configs[4] is the 8-GPU run (driver's SCALE); this run has {world}"}),
+    }
+
+
 def torch_tensor_aca_rect(src, tar, scale, div):
     """The reference's composed ATen formulation (Modules_Runtime_Test.py:294-302),
     restated for timing on the same GPU (the comparison the survey asks for)."""
@@ -1240,9 +1292,13 @@ def host_boundary_section(d: Dist, pkg, n: int):
     (the points ride in the launch, H comes back through mapped memory; synchronous like
     ACA_SKS.cpp:24); (2) a host-resident n-problem batch, the PCIe-inclusive rate of a
     caller whose data lives in host memory: `staged` = pinned H2D of src/tar + the kernel
-    + D2H of H on one stream; `zero_copy_*` = hg_solve_host_f32, the kernel reading and
-    writing the host buffers over PCIe itself, from pinned and from pageable memory (the
-    latter registered for the call); `h2d_bound` = the 64 B/problem H2D copy alone."""
+    + D2H of H on one stream; `zero_copy_pinned` = hg_solve_host_f32 on pinned buffers, the
+    kernel reading and writing them over PCIe itself; `pageable_staged` = hg_solve_host_f32 on
+    pageable buffers, the default since 0.3 -- host threads copy them through the library's
+    ring of pinned stages while the kernel reads the stage before, and the caller's pages are
+    never mapped for the GPU; `pageable_registered` = the same with HG_FLAG_HOST_REGISTER (the
+    pages registered for the call, zero-copy -- what round 5 did by default);
+    `h2d_bound` = the 64 B/problem H2D copy alone."""
     import ctypes
     lib = pkg.lib()
     f = lib._ZN3sks13runKernel_ACAEPfS0_S0_
@@ -1283,7 +1339,9 @@ def host_boundary_section(d: Dist, pkg, n: int):
            "pcie_bytes_per_problem": 100}
     for name, fn, res in (("staged", staged, hH),
                           ("zero_copy_pinned", lambda: pkg.solve_host("aca", hs, ht, out=hH), hH),
-                          ("zero_copy_pageable", lambda: pkg.solve_host("aca", qs, qt, out=qH), qH),
+                          ("pageable_staged", lambda: pkg.solve_host("aca", qs, qt, out=qH), qH),
+                          ("pageable_registered",
+                           lambda: pkg.solve_host("aca", qs, qt, out=qH, register=True), qH),
                           ("h2d_bound", h2d, None)):
         fn()
         torch.cuda.synchronize(d.dev)
@@ -1294,6 +1352,11 @@ def host_boundary_section(d: Dist, pkg, n: int):
             rec["bit_exact"] = bool(torch.equal(res.view(torch.int32), want.view(torch.int32)))
         out[name] = rec
     out["zero_copy_speedup_vs_staged"] = round(out["staged"]["ms"] / out["zero_copy_pinned"]["ms"], 2)
+    prev = (ctypes.c_int64 * 3)()
+    lib.hg_internal_host_stage_config.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                                                  ctypes.POINTER(ctypes.c_int64)]
+    if lib.hg_internal_host_stage_config(0, 0, 0, prev) == 0:
+        out["pageable_ring"] = {"stage_bytes": prev[0], "depth": prev[1], "copy_threads": prev[2]}
     del hs, ht, hH, qs, qt, qH, ds, dt, dH
     return out
 
@@ -1953,6 +2016,7 @@ def main():
     if d.rank == 0 and d.world == 1 and not args.no_cpu:
         try:
             line["cpu_baseline"] = cpu_baseline(min(n, 10_000_000))
+            line["cpu_baseline"]["config0_n1000"] = config0_check(pkg, d.dev)
             # the speed-up is quoted against the multi-threaded host baseline
             line["cpu_baseline"]["gpu_speedup"] = round(
                 line["value"] / line["cpu_baseline"]["value"], 1)
@@ -1963,6 +2027,7 @@ def main():
                 nat["gpu_speedup"] = round(line["value"] / nat["aca_value"], 1)
         except Exception as e:  # noqa: BLE001
             line["cpu_baseline"] = {"error": f"{type(e).__name__}: {e}"}
+    line["baseline_configs"] = baseline_configs(line, args, d.world)  # last: the driver's tail
     all_done.set()
     emit()
     d.close()

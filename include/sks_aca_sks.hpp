@@ -15,8 +15,8 @@
 // The *_batch overloads are the bulk entry points a caller should use: AoS
 // (n,8)/(n,8)/(n,9), normalised.  Device-visible buffers (device, managed or pinned host
 // memory) are solved asynchronously on `stream` (hipStream_t or NULL); if any buffer is
-// pageable host memory the call goes through hg_solve_host_* (registered for the call,
-// read and written over PCIe by the kernel, synchronous).
+// pageable host memory the call goes through hg_solve_host_* (copied through the library's
+// ring of pinned stages -- the caller's pages are never mapped for the GPU -- synchronous).
 #pragma once
 #include <cstdint>
 

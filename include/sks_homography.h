@@ -42,6 +42,9 @@ extern "C" {
 #define HG_LAYOUT_AOS 0
 #define HG_LAYOUT_SOA 1
 #define HG_FLAG_NORMALIZE 1
+/* hg_solve_host_* only (new in 0.3): register the caller's pageable pages for the call
+ * instead of staging them -- see hg_solve_host_f32. */
+#define HG_FLAG_HOST_REGISTER 2
 
 /* ACA, binary32.  Replaces sks::runKernel_ACA (C++ Codes/modules/ACA_SKS.cpp:24-102)
  * batched; with HG_LAYOUT_SOA and no flag it is the FP32 analogue of
@@ -302,22 +305,31 @@ int hg_solve_one_f64(int algo, const double* src, const double* tar, double* H, 
 
 /* A batch whose src/tar/H live in HOST memory -- the reference C++ API's data placement
  * (ACA_SKS.hpp:17-20 take host arrays; CPU_Runtime Test/main.cpp:87-114), batched.  The
- * kernel of hg_<algo>_f32/_f64 reads src/tar from host memory over PCIe and writes H back
- * there directly (zero-copy: both link directions busy at once, no device buffer): pinned
- * memory (hipHostMalloc / hipHostRegister with a device mapping) is used as it is;
- * pageable memory is registered (hipHostRegisterMapped, whole pages, overlapping buffers
- * merged) for the call and unregistered once no call uses it any more: concurrent calls on
- * buffers that share pages (slices of one allocation) share the library's registration,
- * reference-counted, and run at once; a call whose pages only partly overlap another's
- * registration waits for it.  A call fails (hipErrorHostMemoryAlreadyRegistered ...) if the
- * caller itself holds a registration over part of those pages.  Device or managed pointers
- * are accepted too.
+ * kernel of hg_<algo>_f32/_f64 solves it with the same bits:
+ *  - pinned memory (hipHostMalloc, or the caller's own hipHostRegister with a device mapping)
+ *    is read and written by the kernel in place over PCIe (zero-copy: both link directions
+ *    busy at once, no device buffer);
+ *  - pageable memory is copied, by host threads, through a ring of library-owned pinned
+ *    stages (chunk k copied in while the kernel reads chunk k-1's stage, H copied out once
+ *    its chunk is done).  The caller's pages are only ever touched by the CPU: the call
+ *    leaves no GPU mapping of them behind (0.3);
+ *  - with HG_FLAG_HOST_REGISTER, pageable memory is instead registered
+ *    (hipHostRegisterMapped, whole pages, overlapping buffers merged) for the call and
+ *    unregistered once no call uses it any more (concurrent calls on buffers that share
+ *    pages share the library's registration, reference-counted; a call whose pages only
+ *    partly overlap another's registration waits for it; a call fails
+ *    (hipErrorHostMemoryAlreadyRegistered ...) if the caller itself holds a registration over
+ *    part of those pages).  Zero-copy, but the driver keeps the pages mapped for the GPU
+ *    after the unregistration: a later HIP copy of >= 2 MB into those heap pages, once reused,
+ *    can fault.  Use it only on memory that is never handed back
+ *    to the heap (e.g. a shared-memory mapping kept for the process's life).
+ * Device or managed pointers are accepted too.
  * SYNCHRONOUS, unlike every other entry point: H is complete on return.  stream NULL =
  * hipStreamPerThread when any buffer is host memory, else the legacy default stream.
- * Same layouts, flags, validation and bits as hg_<algo>_*; algo is an HG_ALGO_* id
- * (HG_ALGO_GPT binary64 only).  hipErrorInvalidValue also when a buffer's first and
- * last bytes lie in different kinds of memory (e.g. a pinned block and pageable memory
- * after it).  Buffers must be the caller's own, whole: the call cannot see every
+ * Same layouts, flags (plus HG_FLAG_HOST_REGISTER), validation and bits as hg_<algo>_*; algo
+ * is an HG_ALGO_* id (HG_ALGO_GPT binary64 only).  hipErrorInvalidValue also when a buffer's
+ * first and last bytes lie in different kinds of memory (e.g. a pinned block and pageable
+ * memory after it).  Buffers must be the caller's own, whole: the call cannot see every
  * overrun. */
 int hg_solve_host_f32(int algo, const float* src, const float* tar, float* H, int64_t n,
                       int layout, int flags, void* stream);

@@ -18,6 +18,7 @@ MULTI_LIB_PATH = os.path.join(HERE, "lib", "libsks_homography_multi.so")
 HG_LAYOUT_AOS = 0
 HG_LAYOUT_SOA = 1
 HG_FLAG_NORMALIZE = 1
+HG_FLAG_HOST_REGISTER = 2  # hg_solve_host_* only: register pageable pages instead of staging
 
 _vp = ctypes.c_void_p
 _i64 = ctypes.c_int64

@@ -1,14 +1,19 @@
-// hg_host.cpp -- host-resident batches (hg_solve_host_f32/_f64): the kernels read src/tar
-// straight out of host memory over PCIe and write H straight back (zero-copy), so both
-// link directions carry traffic at once and no device buffer is needed.  Measured at 10 M
-// f32 AoS (tools/host_probe.py, profiles/r01/host_probe.json): 12.0 ms pinned and 13.4 ms
-// pageable, against 17.7 / 18.8 ms for H2D + solve + D2H on one stream; the H2D direction
-// alone takes 11.7 ms, so the call runs at the PCIe read bound.  Batches whose pageable
-// buffers fit kStageBytes are copied through library-owned pinned memory instead of being
-// registered (cheaper than the registration below that size).
+// hg_host.cpp -- host-resident batches (hg_solve_host_f32/_f64).  Pinned (device-mapped)
+// buffers are read and written by the kernel in place over PCIe (zero-copy: both link
+// directions carry traffic at once, no device buffer; at 10 M f32 AoS 12.0 ms against
+// 17.7 ms for H2D + solve + D2H, profiles/r01/host_probe.json).  Pageable buffers go through a
+// ring of library-owned pinned stages, filled and emptied by host threads while the kernel
+// reads the stage before (solve_staged below): the caller's pages are never registered, so
+// the call leaves no GPU mapping of them behind.  Registering them instead (zero-copy on the
+// caller's pages) is opt-in, HG_FLAG_HOST_REGISTER: KFD keeps registered pages mapped for the
+// GPU after hipHostUnregister, which is how heap pages reach a later HIP copy
+// in the state the round-4/5 faults came from.
 #include <hip/hip_runtime_api.h>
+#include <sched.h>
 
 #include <algorithm>
+#include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstdint>
 #include <cstring>
@@ -17,6 +22,7 @@
 #include <vector>
 
 #include "hg_host_ranges.hpp"
+#include "hg_host_stage.hpp"
 #include "sks_homography.h"
 
 namespace {
@@ -71,7 +77,9 @@ int classify(View& v) {
     return 0;
 }
 
-// Library-owned registrations of pageable host memory, shared between concurrent calls.
+// Library-owned registrations of pageable host memory (HG_FLAG_HOST_REGISTER calls), shared
+// between concurrent calls.  A staged call also consults the registry: pages a registering
+// call holds read as pinned memory, and are still the caller's pageable memory to it.
 //
 // Two calls may solve buffers that share pages (two threads, each with half of one numpy
 // or torch allocation).  A page the library registered for call A reads as pinned memory
@@ -219,43 +227,91 @@ Registry& registry() {
     return r;
 }
 
-// Small batches: the pageable buffers are copied through library-owned pinned memory instead
-// of being registered.  Registering and releasing three page ranges costs ≈ 6 µs a call
-// (INTEGRATION.md §1), more than copying up to kStageBytes, and leaves the caller's pages alone:
-// KFD keeps registered pages mapped for the GPU after their release.  Stages
-// come from a process-wide pool and are never freed, so no HIP call runs at thread or process
-// exit.
-constexpr size_t kStageBytes = 128 << 10;
-constexpr size_t kStageAlign = 256;
+// ---------------------------------------------------------------------------------------------
+// Pageable buffers (the default): a ring of library-owned pinned stages (hg_host_stage.hpp).
+// The caller's pages are only ever read and written by host threads, so the call leaves them
+// exactly as it found them -- no registration, no GPU mapping.  Chunk k is
+// copied into stage k % D while the kernels of the chunks before it read their stages over
+// PCIe; a stage is refilled once its chunk's kernel has finished (an event per stage) and that
+// chunk's H has been copied out.  Batches whose staged bytes fit kSmallStageBytes take one
+// small stage and no helper thread (about 6 us cheaper a call than registering three page
+// ranges).  Stages come from a process-wide pool and are never freed, so no
+// HIP call runs at thread or process exit; they are portable (mapped for every device) and
+// their device address is looked up per device.
+constexpr size_t kSmallStageBytes = 128 << 10;
+constexpr int kDevSlots = 64;
+
+struct StageConfig {
+    std::atomic<int64_t> ring_bytes{8 << 20};  // one ring stage
+    std::atomic<int> depth{4};                 // ring stages a call cycles through
+};
+
+StageConfig& stage_config() {
+    static StageConfig* c = new StageConfig();  // never destroyed
+    return *c;
+}
+
+host::CopyPool& copy_pool() {
+    static host::CopyPool* p = [] {
+        auto* q = new host::CopyPool();  // never destroyed: its helpers never exit
+        cpu_set_t set;
+        int cpus = 8;
+        if (sched_getaffinity(0, sizeof(set), &set) == 0) cpus = CPU_COUNT(&set);
+        q->set_threads(std::max(1, std::min(cpus, 8)));
+        return q;
+    }();
+    return *p;
+}
 
 struct Stage {
-    char* host = nullptr;  // pinned, mapped
-    char* dev = nullptr;   // its device address
+    char* host = nullptr;  // pinned, mapped, coherent, portable
+    size_t bytes = 0;
+    char* dev[kDevSlots] = {};  // its address on device d (filled on first use there)
 };
+
+struct StageStats {
+    std::atomic<int64_t> made{0}, calls{0}, chunks{0}, leaked{0}, ring_calls{0};
+    std::atomic<int64_t> copy_ns{0}, wait_ns{0}, copy_bytes{0};  // host copies; event waits
+};
+
+int64_t now_ns() {
+    return std::chrono::duration_cast<std::chrono::nanoseconds>(
+               std::chrono::steady_clock::now().time_since_epoch())
+        .count();
+}
+
+StageStats& stage_stats() {
+    static StageStats* s = new StageStats();
+    return *s;
+}
 
 struct StagePool {
     std::mutex mu;
     std::vector<Stage*> idle;
 
-    int take(Stage*& out) {
+    // An idle stage of exactly `bytes`, or a new one.
+    int take(size_t bytes, Stage*& out) {
         {
             std::lock_guard<std::mutex> lock(mu);
-            if (!idle.empty()) {
-                out = idle.back();
-                idle.pop_back();
+            for (size_t i = idle.size(); i-- > 0;) {
+                if (idle[i]->bytes != bytes) continue;
+                out = idle[i];
+                idle.erase(idle.begin() + (long)i);
                 return 0;
             }
         }
         auto* st = new Stage();
-        // coherent (fine-grained): the GPU never holds a stale line of a stage another call refilled
-        hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), kStageBytes,
-                                     hipHostMallocMapped | hipHostMallocCoherent);
-        if (e == hipSuccess) e = hipHostGetDevicePointer(reinterpret_cast<void**>(&st->dev), st->host, 0);
+        // coherent (fine-grained): the GPU never holds a stale line of a stage another call
+        // refilled; portable: a stage serves calls on any device of the process
+        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), bytes,
+                                           hipHostMallocMapped | hipHostMallocCoherent |
+                                               hipHostMallocPortable);
         if (e != hipSuccess) {  // nothing half-made is kept
-            if (st->host) (void)hipHostFree(st->host);
             delete st;
             return (int)e;
         }
+        st->bytes = bytes;
+        ++stage_stats().made;
         out = st;
         return 0;
     }
@@ -270,13 +326,21 @@ StagePool& stage_pool() {
     return *p;
 }
 
-size_t stage_round(size_t b) { return (b + kStageAlign - 1) / kStageAlign * kStageAlign; }
-
-// Bytes a batch's pageable views take in a stage (each at a kStageAlign boundary).
-size_t staged_bytes(const std::vector<View*>& pageable) {
-    size_t b = 0;
-    for (const View* x : pageable) b += stage_round(x->bytes);
-    return b;
+// The stage's address on the current device.
+int stage_dev(Stage* st, char*& out) {
+    int d = 0;
+    hipError_t e = hipGetDevice(&d);
+    if (e != hipSuccess) return (int)e;
+    if (d >= 0 && d < kDevSlots && st->dev[d]) {
+        out = st->dev[d];
+        return 0;
+    }
+    void* p = nullptr;
+    e = hipHostGetDevicePointer(&p, st->host, 0);
+    if (e != hipSuccess) return (int)e;
+    out = static_cast<char*>(p);
+    if (d >= 0 && d < kDevSlots) st->dev[d] = out;
+    return 0;
 }
 
 // The solvers with the host-memory cache policy (hg_kernels.hip, library-internal).
@@ -312,13 +376,137 @@ int launch(int algo, const T* s, const T* t, T* h, int64_t n, int layout, int fl
     }
 }
 
+// The staged solve of a batch with at least one pageable buffer (v[i].dev == nullptr).
+template <typename T>
+int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipStream_t s) {
+    host::StagePlan p;
+    p.n = n;
+    p.elem = sizeof(T);
+    p.soa = layout == HG_LAYOUT_SOA;
+    for (int i = 0; i < 3; ++i) p.mode[i] = v[i].dev ? host::kDirect : host::kCpu;
+    size_t per = 0;
+    for (int i = 0; i < 3; ++i)
+        if (p.staged(i)) per += host::align_up((size_t)n * p.per_problem(i));
+    const bool small = per <= kSmallStageBytes;
+    const size_t cap = small ? kSmallStageBytes : (size_t)stage_config().ring_bytes.load();
+    if (!host::plan_chunks(p, cap)) return kInvalid;
+    if (p.soa && p.chunks > 1) {
+        // an SoA chunk is C-wide rows: a buffer used in place would have n-wide rows, so every
+        // buffer goes through the stage -- host memory by the copy threads, device memory by
+        // the DMA engines
+        for (int i = 0; i < 3; ++i)
+            if (p.mode[i] == host::kDirect) p.mode[i] = v[i].in_host ? host::kCpu : host::kDma;
+        if (!host::plan_chunks(p, cap)) return kInvalid;
+    }
+    const int64_t K = p.chunks;
+    const int D = (int)std::min<int64_t>(K, std::max(1, stage_config().depth.load()));
+    std::vector<Stage*> st((size_t)D, nullptr);
+    std::vector<char*> sd((size_t)D, nullptr);
+    std::vector<hipEvent_t> ev;
+    int rc = 0;
+    for (int j = 0; j < D && !rc; ++j) {
+        rc = stage_pool().take(cap, st[(size_t)j]);
+        if (!rc) rc = stage_dev(st[(size_t)j], sd[(size_t)j]);
+    }
+    if (!rc && K > 1) {
+        ev.assign((size_t)D, nullptr);
+        for (int j = 0; j < D && !rc; ++j)
+            rc = (int)hipEventCreateWithFlags(&ev[(size_t)j], hipEventDisableTiming);
+    }
+    ++stage_stats().calls;
+    if (!small) ++stage_stats().ring_calls;
+    host::CopyPool& pool = copy_pool();
+    std::vector<host::Piece> pieces;
+    const char* in_user[3] = {static_cast<const char*>(v[0].host),
+                              static_cast<const char*>(v[1].host), nullptr};
+    char* H_user = static_cast<char*>(const_cast<void*>(v[2].host));
+    auto copy_out = [&](int64_t k, int j) {
+        if (p.mode[2] == host::kCpu)
+            host::chunk_pieces(p, 2, k, nullptr, H_user, st[(size_t)j]->host, false, pieces);
+    };
+    auto copy_in = [&](int64_t k, int j) {
+        for (int i = 0; i < 2; ++i)
+            if (p.mode[i] == host::kCpu)
+                host::chunk_pieces(p, i, k, in_user[i], nullptr, st[(size_t)j]->host, true, pieces);
+    };
+    const size_t E = sizeof(T);
+    StageStats& stats = stage_stats();
+    auto run_pieces = [&]() {
+        const int64_t t0 = now_ns();
+        pool.run(pieces);
+        stats.copy_ns += now_ns() - t0;
+        int64_t b = 0;
+        for (const host::Piece& x : pieces) b += (int64_t)x.bytes;
+        stats.copy_bytes += b;
+    };
+    for (int64_t k = 0; k < K && !rc; ++k) {
+        const int j = (int)(k % D);
+        pieces.clear();
+        if (k >= D) {  // stage j still holds chunk k - D: wait for its kernel, take its H out
+            const int64_t t0 = now_ns();
+            rc = (int)hipEventSynchronize(ev[(size_t)j]);
+            stats.wait_ns += now_ns() - t0;
+            if (rc) break;
+            copy_out(k - D, j);
+        }
+        copy_in(k, j);
+        run_pieces();
+        const int64_t lo = p.lo(k), c = p.count(k);
+        char* ptr[3];
+        for (int i = 0; i < 3; ++i) {
+            if (p.mode[i] == host::kDirect)  // AoS (or a one-chunk SoA batch): in place
+                ptr[i] = static_cast<char*>(v[i].dev) + (size_t)lo * p.per_problem(i);
+            else
+                ptr[i] = sd[(size_t)j] + p.off[i];
+        }
+        for (int i = 0; i < 2 && !rc; ++i)  // device-memory SoA rows into the stage
+            if (p.mode[i] == host::kDma)
+                rc = (int)hipMemcpy2DAsync(st[(size_t)j]->host + p.off[i], (size_t)c * E,
+                                           static_cast<const char*>(v[i].dev) + (size_t)lo * E,
+                                           (size_t)n * E, (size_t)c * E, (size_t)p.rows[i],
+                                           hipMemcpyDeviceToHost, s);
+        if (!rc)
+            rc = launch<T>(algo, reinterpret_cast<const T*>(ptr[0]),
+                           reinterpret_cast<const T*>(ptr[1]), reinterpret_cast<T*>(ptr[2]), c,
+                           layout, flags, s, true);
+        if (!rc && p.mode[2] == host::kDma)
+            rc = (int)hipMemcpy2DAsync(static_cast<char*>(v[2].dev) + (size_t)lo * E,
+                                       (size_t)n * E, st[(size_t)j]->host + p.off[2],
+                                       (size_t)c * E, (size_t)c * E, (size_t)p.rows[2],
+                                       hipMemcpyHostToDevice, s);
+        if (!rc && K > 1) rc = (int)hipEventRecord(ev[(size_t)j], s);
+        ++stage_stats().chunks;
+    }
+    // every stage's last chunk: H out once the stream has drained
+    const int64_t t_drain = now_ns();
+    const hipError_t e = hipStreamSynchronize(s);
+    stats.wait_ns += now_ns() - t_drain;
+    if (!rc && e == hipSuccess) {
+        pieces.clear();
+        for (int64_t k = std::max<int64_t>(0, K - D); k < K; ++k) copy_out(k, (int)(k % D));
+        run_pieces();
+    }
+    for (hipEvent_t x : ev)
+        if (x) (void)hipEventDestroy(x);
+    for (Stage* x : st) {
+        if (!x) continue;
+        // a stream that did not drain may still have a kernel reading or writing the stage:
+        // it is never handed to another call
+        if (e == hipSuccess) stage_pool().give_back(x);
+        else ++stage_stats().leaked;
+    }
+    return rc ? rc : (int)e;
+}
+
 template <typename T>
 int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout, int flags,
                void* stream) {
     const int max_algo = sizeof(T) == 8 ? HG_ALGO_GPT : HG_ALGO_GE;
     if (algo < HG_ALGO_ACA || algo > max_algo || n < 0) return kInvalid;
     if (layout != HG_LAYOUT_AOS && layout != HG_LAYOUT_SOA) return kInvalid;
-    if (flags & ~HG_FLAG_NORMALIZE) return kInvalid;
+    if (flags & ~(HG_FLAG_NORMALIZE | HG_FLAG_HOST_REGISTER)) return kInvalid;
+    const bool register_pages = flags & HG_FLAG_HOST_REGISTER;
+    flags &= HG_FLAG_NORMALIZE;
     if (n == 0) return 0;
     if (!src || !tar || !H) return kInvalid;
     if (n > INT64_MAX / (9 * (int64_t)sizeof(T))) return kInvalid;
@@ -343,48 +531,24 @@ int solve_host(int algo, const T* src, const T* tar, T* H, int64_t n, int layout
     // data has no such producer and goes on the calling thread's own default stream.
     hipStream_t s = static_cast<hipStream_t>(stream);
     if (!s && !all_device) s = hipStreamPerThread;
-    auto run = [&]() -> int {
-        int rc = launch<T>(algo, static_cast<const T*>(v[0].dev), static_cast<const T*>(v[1].dev),
-                           static_cast<T*>(v[2].dev), n, layout, flags, s, !all_device);
-        const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
-        return rc ? rc : (int)e;
-    };
-    Stage* st = nullptr;
-    if (!pageable.empty() && staged_bytes(pageable) <= kStageBytes) {
-        // a stage that cannot be made (pinned memory exhausted) leaves the call to the
-        // registration below, with the allocation's own error cleared
-        if (stage_pool().take(st) != 0) {
-            st = nullptr;
-            (void)hipGetLastError();
-        }
-    }
-    if (st) {
+    if (!pageable.empty() && !register_pages) {
         lock.unlock();  // no registration: the registry is not involved
-        int rc = 0;
-        size_t off = 0, h_off = 0;
-        bool h_staged = false;
         for (View* x : pageable) {
-            if (x == &v[2]) {  // H: written by the kernel into the stage, copied out after
-                h_staged = true;
-                h_off = off;
-            } else {
-                std::memcpy(st->host + off, x->host, x->bytes);
-            }
-            x->dev = st->dev + off;
-            off += stage_round(x->bytes);
+            x->dev = nullptr;  // a page another call registered is still the caller's pageable memory
+            x->in_host = true;
         }
-        rc = run();
-        if (rc == 0 && h_staged) std::memcpy(H, st->host + h_off, v[2].bytes);
-        stage_pool().give_back(st);
-        return rc;
+        return solve_staged<T>(algo, v, n, layout, flags, s);
     }
     std::vector<uintptr_t> held;
-    if (!pageable.empty()) {
+    if (!pageable.empty()) {  // HG_FLAG_HOST_REGISTER: the caller's pages, mapped for the call
         const int rc = reg.acquire(pageable, held, lock);
         if (rc) return rc;
     }
     lock.unlock();  // the solve itself runs unlocked: other calls may share the registrations
-    const int rc = run();
+    int rc = launch<T>(algo, static_cast<const T*>(v[0].dev), static_cast<const T*>(v[1].dev),
+                       static_cast<T*>(v[2].dev), n, layout, flags, s, !all_device);
+    const hipError_t e = hipStreamSynchronize(s);  // H is complete when the call returns
+    if (!rc) rc = (int)e;
     if (!held.empty()) {
         lock.lock();
         reg.release(held);
@@ -423,6 +587,42 @@ int hg_internal_host_registry_find(uint64_t va, uint64_t* lo, uint64_t* hi, uint
             return h.state;
         }
     }
+    return 0;
+}
+
+// Library-internal (tests and tools/host_probe.py): the staged ring's shape -- bytes of a ring
+// stage (>= 64 KiB), stages a call cycles through (1 ... 16), copy threads including the
+// caller (1 ... 64); a value <= 0 leaves that setting as it is.  The previous settings go to
+// prev[3] when given.
+int hg_internal_host_stage_config(int64_t ring_bytes, int depth, int threads, int64_t* prev) {
+    StageConfig& c = stage_config();
+    if (prev) {
+        prev[0] = c.ring_bytes.load();
+        prev[1] = c.depth.load();
+        prev[2] = copy_pool().threads();
+    }
+    if ((ring_bytes > 0 && ring_bytes < (64 << 10)) || depth > 16 || threads > 64) return kInvalid;
+    if (ring_bytes > 0) c.ring_bytes = ring_bytes / (int64_t)hg::host::kStageAlign *
+                                       (int64_t)hg::host::kStageAlign;
+    if (depth > 0) c.depth = depth;
+    if (threads > 0) copy_pool().set_threads(threads);
+    return 0;
+}
+
+// {stages allocated, staged calls, chunks solved, stages withheld after a failed stream,
+// calls that took ring stages (not the small stage), ns in host copies, ns waiting for the
+// GPU, bytes copied by the host} -- out[8].
+int hg_internal_host_stage_stats(int64_t* out) {
+    if (!out) return kInvalid;
+    StageStats& s = stage_stats();
+    out[0] = s.made.load();
+    out[1] = s.calls.load();
+    out[2] = s.chunks.load();
+    out[3] = s.leaked.load();
+    out[4] = s.ring_calls.load();
+    out[5] = s.copy_ns.load();
+    out[6] = s.wait_ns.load();
+    out[7] = s.copy_bytes.load();
     return 0;
 }
 

@@ -981,6 +981,6 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
     return hg::launch(hg::aten_sum_l4, (unsigned)rows, 64, 0, s, a, threads, lanes, out);
 }
 
-const char* hg_version(void) { return "sks-homography-amd 0.2 (gfx950)"; }
+const char* hg_version(void) { return "sks-homography-amd 0.3 (gfx950)"; }
 
 }  // extern "C"

@@ -188,7 +188,7 @@ int solve_one(T* src, T* tar, T* result) {
 
 // Batches: device-visible buffers (device, managed or pinned host memory) are solved
 // asynchronously on `stream`; a batch with any pageable host buffer goes through
-// hg_solve_host_* (registered for the call, zero-copy, synchronous).
+// hg_solve_host_* (staged through library-owned pinned memory, synchronous).
 bool is_pageable(const void* p) {
     hipPointerAttribute_t attr;
     if (hipPointerGetAttributes(&attr, p) != hipSuccess) {

@@ -90,12 +90,17 @@ def solve(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = Tru
 
 def solve_host(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool = True,
                layout: str = "aos", out: Optional[torch.Tensor] = None,
-               device: Union[int, str, torch.device, None] = None) -> torch.Tensor:
-    """``solve`` for a batch that lives in HOST memory (CPU tensors, pinned or not): the
-    GPU kernel reads src/tar over PCIe and writes H into the host tensor directly
-    (hg_solve_host_*, zero-copy; pageable tensors are registered for the call).  Returns
-    when H is complete.  ``device`` picks the GPU (default: the current one).  The
-    computation is the same HIP kernel with the same bits -- there is no CPU solver."""
+               device: Union[int, str, torch.device, None] = None,
+               register: bool = False) -> torch.Tensor:
+    """``solve`` for a batch that lives in HOST memory (CPU tensors, pinned or not)
+    (hg_solve_host_*).  Pinned tensors are read and written by the GPU kernel in place over
+    PCIe (zero-copy); pageable tensors go through the library's ring of pinned stages, copied
+    by host threads, so their pages are never mapped for the GPU.  ``register=True``
+    (HG_FLAG_HOST_REGISTER) registers pageable tensors for the call instead -- zero-copy, but
+    the driver keeps those pages GPU-mapped afterwards: only for memory that is never handed
+    back to the heap.  Returns when H is complete.  ``device``
+    picks the GPU (default: the current one).  The computation is the same HIP kernel with
+    the same bits -- there is no CPU solver."""
     algo_id = _ALGO_ID.get(algo)
     if algo_id is None:
         raise ValueError(f"algo must be 'aca', 'sks', 'ge' or 'gpt', got {algo!r}")
@@ -131,7 +136,8 @@ def solve_host(algo: str, src: torch.Tensor, tar: torch.Tensor, normalize: bool 
     fn = "hg_solve_host_f32" if src.dtype is torch.float32 else "hg_solve_host_f64"
     with _guard(dev):
         _lib.call(fn, algo_id, src.data_ptr(), tar.data_ptr(), out.data_ptr(), n, lay,
-                  _lib.HG_FLAG_NORMALIZE if normalize else 0, None)
+                  (_lib.HG_FLAG_NORMALIZE if normalize else 0)
+                  | (_lib.HG_FLAG_HOST_REGISTER if register else 0), None)
     return out
 
 

@@ -11,7 +11,7 @@ collects every H block on one rank, both as paired send/recv over RCCL
 
 A batch that lives in HOST memory needs neither: SharedHostBatch puts src/tar/H in one
 shared-memory file every rank maps, and each rank's GPU reads its block and writes its H
-rows over its own PCIe link (ops.solve_host, zero-copy) -- N links in parallel, no xGMI
+rows over its own PCIe link (ops.solve_host with register=True, zero-copy) -- N links in parallel, no xGMI
 traffic, no rank-0 bottleneck.
 """
 from __future__ import annotations
@@ -197,13 +197,16 @@ class SharedHostBatch:
 
     def solve_block(self, world: int, algo: str = "aca", normalize: bool = True,
                     device=None) -> Tuple[int, int]:
-        """Solves this rank's block in place (H rows of the shared file); returns it."""
+        """Solves this rank's block in place (H rows of the shared file); returns it.  The
+        pages are registered for the call (zero-copy, HG_FLAG_HOST_REGISTER): they belong to
+        this object's own shared-memory mapping, never to the heap, and the driver drops any
+        GPU mapping of them when close() unmaps the file."""
         from .ops import solve_host
 
         lo, hi = self.block(world)
         if hi > lo:
             solve_host(algo, self.src[lo:hi], self.tar[lo:hi], normalize=normalize,
-                       out=self.H[lo:hi], device=device)
+                       out=self.H[lo:hi], device=device, register=True)
         return lo, hi
 
     def close(self) -> None:

@@ -15,7 +15,9 @@ os.environ.setdefault("AMD_LOG_LEVEL", "1")
 # mappings after the copy; every GPU fault this suite ever had was such a copy writing a heap
 # page.  The tests' own .cpu() / .to() copies go through HIP's staging
 # buffers instead (the runtime reads this before it starts): no heap page of the test process
-# is mapped for the GPU except by the library's own host-memory calls, which are under test.
+# is mapped for the GPU except by the library's HG_FLAG_HOST_REGISTER calls under test (its
+# default host path maps none -- tests/test_gpu_host_nomap.py checks that in a child process
+# that runs WITHOUT this setting).
 os.environ.setdefault("GPU_PINNED_MIN_XFER_SIZE", "65536")  # MiB
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -56,7 +58,7 @@ _PARITY_FILES = [
     "test_gpu_ransac.py", "test_gpu_mrg32k3a.py", "test_gpu_aten_sum.py", "test_gpu_rocm_sum.py",
     "test_gpu_refcu.py", "test_gpu_config5.py", "test_gpu_multi.py",
 ]
-_PROGRAM_FILES = ["test_gpu_bench_contract.py", "test_gpu_cpp_api.py"]
+_PROGRAM_FILES = ["test_gpu_bench_contract.py", "test_gpu_cpp_api.py", "test_gpu_host_nomap.py"]
 _STRESS_FILES = ["test_gpu_grouped.py", "test_gpu_errors.py", "test_gpu_host.py"]
 _STRESS_TESTS = [  # plumbing tests inside the parity file: threads, host pointers, graphs
     ("test_gpu_parity.py", "test_cpp_api_single_problem_host_and_device"),

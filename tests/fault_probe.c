@@ -112,3 +112,26 @@ int hg_fault_probe_svm(uint64_t va, uint64_t bytes, uint64_t* access, uint64_t* 
     if (global_flag) *global_flag = at[2].value;
     return 0;
 }
+
+/* Walks [va, va + bytes) page by page (page bytes each) with the query above and counts the
+ * pages whose first-GPU access is not `want` (0x202: no access); the first such page's address
+ * and access go to *bad_va / *bad_access.  Returns the count, or -(HSA status) on a failed
+ * query.  For the host-entry test (tests/test_gpu_host_nomap.py): after a library call, the
+ * caller's pages must carry no GPU mapping. */
+int64_t hg_fault_probe_svm_pages(uint64_t va, uint64_t bytes, uint64_t page, uint64_t want,
+                                 uint64_t* bad_va, uint64_t* bad_access) {
+    int64_t bad = 0;
+    if (!page) return -1;
+    for (uint64_t p = va / page * page; p < va + bytes; p += page) {
+        uint64_t acc = 0;
+        const int rc = hg_fault_probe_svm(p, page, &acc, NULL, NULL);
+        if (rc) return -(int64_t)rc;
+        if (acc != want) {
+            if (bad++ == 0) {
+                if (bad_va) *bad_va = p;
+                if (bad_access) *bad_access = acc;
+            }
+        }
+    }
+    return bad;
+}

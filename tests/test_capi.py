@@ -189,7 +189,8 @@ def test_other_entry_validation(pkg):
         assert f(0, None, None, None, 5, 0, 1, None) == 1                       # NULL
         assert f(-1, None, None, None, 0, 0, 1, None) == 1                      # algo
         assert f(0, None, None, None, 0, 2, 1, None) == 1                       # layout
-        assert f(0, None, None, None, 0, 0, 2, None) == 1                       # flags
+        assert f(0, None, None, None, 0, 0, 4, None) == 1                       # flags
+        assert f(0, None, None, None, 0, 0, 1 | 2, None) == 0                   # HOST_REGISTER ok
     assert lib.hg_solve_host_f32(3, None, None, None, 0, 0, 1, None) == 1       # GPT: f64 only
     assert lib.hg_solve_host_f64(3, None, None, None, 0, 0, 1, None) == 0
     assert lib.hg_solve_host_f64(4, None, None, None, 0, 0, 1, None) == 1

@@ -6,10 +6,10 @@ such a copy writing a reused heap page.  tests/conftest.py keeps this process's 
 staged path (GPU_PINNED_MIN_XFER_SIZE, read when the runtime starts).  These tests check that
 the setting took: after .cpu() / .to() copies of 2-64 MB, KFD reports the copied pages as not
 accessible to the GPU (tests/fault_probe.c asks hsa_amd_svm_attributes_get, a host-side
-query).  The library's own host entry, by contrast, maps the caller's pages for its call --
-that is hg_solve_host's contract, and KFD keeps those pages mapped after the call too, so this
-file runs before any library host call (tests/conftest.py orders it with the first tier) --
-and its bits are checked in tests/test_gpu_host.py."""
+query).  The library's own host entry maps none of the caller's pages (it stages pageable
+memory through its own pinned buffers; tests/test_gpu_host_nomap.py checks that without the
+knob) except with HG_FLAG_HOST_REGISTER, whose pages KFD keeps mapped after the call, so this
+file runs before any library host call (tests/conftest.py orders it with the first tier)."""
 import ctypes
 import os
 

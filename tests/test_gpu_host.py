@@ -1,8 +1,12 @@
-"""Host-resident batches (hg_solve_host_f32/_f64, ops.solve_host): the kernel reads src/tar
-from host memory and writes H there.  Pinned and pageable buffers, every solver, both
-layouts, buffers cut from one allocation (sharing pages), misaligned views, threads at
-once -- each bit-identical to the device-resident solve, which tests/test_gpu_parity.py
-pins to the oracle; a small batch is also checked against the oracle directly."""
+"""Host-resident batches (hg_solve_host_f32/_f64, ops.solve_host): pinned buffers are read and
+written by the kernel in place; pageable ones go through the library's ring of pinned stages
+(the default) or, with HG_FLAG_HOST_REGISTER (register=True), are registered for the call.
+Pinned and pageable buffers, every solver, both layouts, one chunk and many (a small ring
+configured through hg_internal_host_stage_config), pinned, device and pageable buffers mixed,
+buffers cut from one allocation (sharing pages), misaligned views, threads at once -- each
+bit-identical to the device-resident solve, which tests/test_gpu_parity.py pins to the
+oracle; a small batch is also checked against the oracle directly.  That the staged path
+leaves the caller's pages unmapped is tests/test_gpu_host_nomap.py."""
 import ctypes
 import os
 import threading
@@ -37,6 +41,34 @@ def _inputs(pkg, dev, n, dtype, layout, off=0):
 
 def _bits(x):
     return x.view(torch.int32 if x.dtype is torch.float32 else torch.int64)
+
+
+def _internal(lib):
+    """Signatures of the library-internal stage hooks (hg_host.cpp; not in the header)."""
+    p64 = ctypes.POINTER(ctypes.c_int64)
+    lib.hg_internal_host_stage_config.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, p64]
+    lib.hg_internal_host_stage_config.restype = ctypes.c_int
+    lib.hg_internal_host_stage_stats.argtypes = [p64]
+    lib.hg_internal_host_stage_stats.restype = ctypes.c_int
+    return lib
+
+
+def _stage_stats(lib):
+    _internal(lib)
+    st = (ctypes.c_int64 * 8)()
+    assert lib.hg_internal_host_stage_stats(st) == 0
+    return list(st)
+
+
+@pytest.fixture
+def small_ring(pkg):
+    """A 64 KiB ring stage, 3 deep, 4 copy threads: every batch below of more than a few
+    hundred problems runs in many chunks.  The library's settings are restored after."""
+    lib = _internal(pkg.lib())
+    prev = (ctypes.c_int64 * 3)()
+    assert lib.hg_internal_host_stage_config(64 << 10, 3, 4, prev) == 0
+    yield lib
+    assert lib.hg_internal_host_stage_config(prev[0], prev[1], prev[2], None) == 0
 
 
 def _hip():
@@ -76,10 +108,11 @@ def test_host_batch_vs_oracle(pkg, dev, oracle):
         assert np.array_equal(got.numpy().view(np.uint32), want.view(np.uint32)), algo
 
 
-def test_host_buffers_sharing_pages_and_misaligned(pkg, dev):
+@pytest.mark.parametrize("register", [False, True])
+def test_host_buffers_sharing_pages_and_misaligned(pkg, dev, register):
     """src, tar and H carved out of ONE pageable allocation (neighbours share pages, so
-    the registrations must merge), H at a 4-B offset (not 16-B aligned: the generic
-    kernel), and the registration gone afterwards."""
+    registrations must merge), H at a 4-B offset (not 16-B aligned: the generic
+    kernel), and no registration left afterwards -- staged and registered."""
     n = 30011
     ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=77)
     want = pkg.solve("aca", ds, dt, normalize=True).cpu()
@@ -89,7 +122,7 @@ def test_host_buffers_sharing_pages_and_misaligned(pkg, dev):
     h = buf[n * 16 + 1:].view(n, 9)  # 4 B past a 16-B boundary
     s.copy_(ds.cpu())
     t.copy_(dt.cpu())
-    pkg.solve_host("aca", s, t, out=h)
+    pkg.solve_host("aca", s, t, out=h, register=register)
     assert torch.equal(_bits(h), _bits(want))
     assert torch.equal(_bits(s), _bits(ds.cpu()))  # inputs untouched
     # unregistered again: a second registration of the same pages succeeds
@@ -98,7 +131,7 @@ def test_host_buffers_sharing_pages_and_misaligned(pkg, dev):
     rc = hip.hipPointerGetAttributes(attrs, ctypes.c_void_p(buf.data_ptr()))
     hip.hipGetLastError()
     assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the call"
-    pkg.solve_host("aca", s, t, out=h)
+    pkg.solve_host("aca", s, t, out=h, register=register)
     assert torch.equal(_bits(h), _bits(want))
 
 
@@ -142,7 +175,8 @@ def test_host_threads_at_once(pkg, dev):
     assert not bad
 
 
-def test_host_threads_share_one_pageable_allocation(pkg, dev):
+@pytest.mark.parametrize("register", [False, True])
+def test_host_threads_share_one_pageable_allocation(pkg, dev, register):
     """threads solving slices of ONE pageable allocation.  Neighbouring
     slices share the pages at their boundaries, so one call finds pages another call
     registered (they read as pinned memory); the library must treat them as its own
@@ -164,11 +198,11 @@ def test_host_threads_share_one_pageable_allocation(pkg, dev):
             # alternate the slice shape so registrations overlap in changing ways: the
             # whole slice, then its two halves in turn
             if it % 3 == 0:
-                pkg.solve_host("aca", src[lo:hi], tar[lo:hi], out=H[lo:hi])
+                pkg.solve_host("aca", src[lo:hi], tar[lo:hi], out=H[lo:hi], register=register)
             else:
                 mid = lo + n // 2 + (it % 2)
-                pkg.solve_host("aca", src[lo:mid], tar[lo:mid], out=H[lo:mid])
-                pkg.solve_host("aca", src[mid:hi], tar[mid:hi], out=H[mid:hi])
+                pkg.solve_host("aca", src[lo:mid], tar[lo:mid], out=H[lo:mid], register=register)
+                pkg.solve_host("aca", src[mid:hi], tar[mid:hi], out=H[mid:hi], register=register)
             if not torch.equal(_bits(H[lo:hi]), _bits(want[lo:hi])):
                 bad.append((i, it))
 
@@ -187,7 +221,8 @@ def test_host_threads_share_one_pageable_allocation(pkg, dev):
         assert rc != 0 or attrs.raw[:4] == b"\0\0\0\0", "pages still registered after the calls"
 
 
-def test_host_threads_random_overlapping_slices(pkg, dev):
+@pytest.mark.parametrize("register", [False, True])
+def test_host_threads_random_overlapping_slices(pkg, dev, register):
     """Stress of the shared registrations: 6 threads, each solving 40 random (possibly
     overlapping in pages, never in rows) slices of one pageable allocation, sizes from 1
     problem to 40 K, f32 AoS; every row written equals the device solve, untouched rows
@@ -208,7 +243,7 @@ def test_host_threads_random_overlapping_slices(pkg, dev):
         for _ in range(40):
             a = rng.randrange(lo0, hi0)
             b = min(hi0, a + rng.choice((1, 7, 100, 4096, 40_000)))
-            pkg.solve_host("aca", src[a:b], tar[a:b], out=H[a:b])
+            pkg.solve_host("aca", src[a:b], tar[a:b], out=H[a:b], register=register)
             if not torch.equal(_bits(H[a:b]), _bits(want[a:b])):
                 bad.append((i, a, b))
 
@@ -240,17 +275,17 @@ def test_host_full_size(pkg, dev):
 
 @pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
 @pytest.mark.parametrize("layout", ["aos", "soa"])
-def test_small_pageable_batches_are_staged(pkg, dev, dtype, layout):
-    """Batches whose pageable buffers fit the library's 128 KiB stage (hg_host.cpp kStageBytes)
-    are copied through library-owned pinned memory, not registered: bits equal the device
-    solve for every solver, ragged sizes up to the stage's edge and just past it, H at a 4-B
-    offset; the staged calls make no page registration at all."""
+def test_pageable_batches_are_staged_never_registered(pkg, dev, dtype, layout):
+    """Pageable batches go through library-owned pinned stages and are never registered: bits
+    equal the device solve for every solver, ragged sizes up to the 128 KiB small stage's
+    edge, just past it (a ring stage) and well past it, H at a 4-B offset; no call makes a
+    page registration, and batches past the small stage's edge take ring stages."""
     lib = pkg.lib()
     stats = (ctypes.c_int64 * 4)()
     algos = ["aca", "sks", "ge"] + (["gpt"] if dtype is torch.float64 else [])
     per = 100 if dtype is torch.float32 else 200  # bytes a problem stages (src + tar + H)
     edge = (128 << 10) // per - 16
-    for n in (1, 2, 7, 64, 100, 1000 if dtype is torch.float32 else 500, edge, edge + 40):
+    for n in (1, 2, 7, 64, 100, 1000 if dtype is torch.float32 else 500, edge, edge + 40, 200_003):
         ds, dt = _inputs(pkg, dev, n, dtype, layout, off=n)
         hs, ht = ds.cpu(), dt.cpu()
         for algo in algos:
@@ -259,17 +294,83 @@ def test_small_pageable_batches_are_staged(pkg, dev, dtype, layout):
             out = buf[1:].view(want.shape)  # one element past the allocation's start
             assert lib.hg_internal_host_registry_stats(stats) == 0
             made = stats[1]
+            ring = _stage_stats(lib)[4]
             got = pkg.solve_host(algo, hs, ht, normalize=True, layout=layout, out=out)
             assert got is out
             assert torch.equal(_bits(got), _bits(want)), (n, algo)
             assert lib.hg_internal_host_registry_stats(stats) == 0
-            staged = n <= edge
-            assert (stats[1] == made) == staged, (n, "staged" if staged else "registered", stats[1] - made)
+            assert stats[1] == made, (n, "registered")
+            assert (_stage_stats(lib)[4] > ring) == (n > edge), (n, "ring stage use")
+            assert torch.equal(_bits(hs), _bits(ds.cpu()))  # inputs untouched
+
+
+@pytest.mark.parametrize("dtype", [torch.float32, torch.float64])
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_staged_ring_many_chunks(pkg, dev, small_ring, dtype, layout):
+    """The ring at work: a 64 KiB stage, 3 deep, so a ragged 70001-problem batch runs in
+    about 110 chunks (the last one short) -- every solver, normalised and not, bits equal to
+    the device solve; pageable inputs untouched; no registration."""
+    lib = small_ring
+    n = 70001
+    algos = ["aca", "sks", "ge"] + (["gpt"] if dtype is torch.float64 else [])
+    ds, dt = _inputs(pkg, dev, n, dtype, layout, off=31)
+    hs, ht = ds.cpu(), dt.cpu()
+    stats = (ctypes.c_int64 * 4)()
+    assert lib.hg_internal_host_registry_stats(stats) == 0
+    made = stats[1]
+    for algo in algos:
+        for norm in (True, False):
+            want = pkg.solve(algo, ds, dt, normalize=norm, layout=layout).cpu()
+            out = torch.full(want.shape, float("nan"), dtype=dtype)
+            c0 = _stage_stats(lib)[2]
+            pkg.solve_host(algo, hs, ht, normalize=norm, layout=layout, out=out)
+            assert torch.equal(_bits(out), _bits(want)), (algo, norm)
+            assert _stage_stats(lib)[2] - c0 > 50, "expected many chunks"
+    assert torch.equal(_bits(hs), _bits(ds.cpu())) and torch.equal(_bits(ht), _bits(dt.cpu()))
+    assert lib.hg_internal_host_registry_stats(stats) == 0 and stats[1] == made
+
+
+@pytest.mark.parametrize("layout", ["aos", "soa"])
+def test_staged_ring_mixed_memory(pkg, dev, small_ring, layout):
+    """Pageable buffers beside pinned and device ones, in many chunks: in AoS the pinned and
+    device buffers are used in place at each chunk's offset; in SoA a chunk is C-wide rows,
+    so the pinned ones are copied by the host threads and the device ones by the DMA engines
+    (hipMemcpy2DAsync) through the stage too.  Every combination, f64 SKS, bits equal."""
+    lib = small_ring
+    n = 40007
+    ds, dt = _inputs(pkg, dev, n, torch.float64, layout, off=5)
+    want = pkg.solve("sks", ds, dt, normalize=True, layout=layout)
+    kinds = {"pageable": lambda x: x.cpu(), "pinned": lambda x: x.cpu().pin_memory(),
+             "device": lambda x: x.clone()}
+    combos = [("pageable", "pinned", "pageable"), ("pinned", "pageable", "pinned"),
+              ("device", "pageable", "pageable"), ("pageable", "device", "device"),
+              ("pinned", "device", "pageable"), ("device", "device", "pageable")]
+    for ks, kt, kh in combos:
+        s, t = kinds[ks](ds), kinds[kt](dt)
+        h = kinds[kh](torch.full(want.shape, float("nan"), dtype=torch.float64, device=dev))
+        rc = lib.hg_solve_host_f64(1, s.data_ptr(), t.data_ptr(), h.data_ptr(), n,
+                                   0 if layout == "aos" else 1, 1, None)
+        assert rc == 0, (ks, kt, kh, rc)
+        assert torch.equal(_bits(h.cpu()), _bits(want.cpu())), (ks, kt, kh)
+
+
+def test_staged_ring_settings_validated(pkg, dev):
+    lib = _internal(pkg.lib())
+    prev = (ctypes.c_int64 * 3)()
+    assert lib.hg_internal_host_stage_config(0, 0, 0, prev) == 0  # a query
+    assert prev[0] >= 64 << 10 and 1 <= prev[1] <= 16 and 1 <= prev[2] <= 64
+    assert lib.hg_internal_host_stage_config(1024, 0, 0, None) == 1
+    assert lib.hg_internal_host_stage_config(0, 17, 0, None) == 1
+    assert lib.hg_internal_host_stage_config(0, 0, 65, None) == 1
+    now = (ctypes.c_int64 * 3)()
+    assert lib.hg_internal_host_stage_config(0, 0, 0, now) == 0
+    assert list(now) == list(prev)
 
 
 def test_small_pageable_batches_from_threads(pkg, dev):
     """Eight threads, each 60 small pageable calls (staged through pooled stages), one of them
-    with pinned inputs and a pageable H: every result bit-exact, no registration made."""
+    with pinned inputs and a pageable H: every result bit-exact, no registration made, no
+    stage withheld."""
     lib = pkg.lib()
     stats = (ctypes.c_int64 * 4)()
     jobs = []
@@ -299,6 +400,7 @@ def test_small_pageable_batches_from_threads(pkg, dev):
     assert not bad, bad
     assert lib.hg_internal_host_registry_stats(stats) == 0
     assert stats[1] == made, f"{stats[1] - made} registrations made by staged calls"
+    assert _stage_stats(lib)[3] == 0
 
 
 def test_host_entry_errors(pkg, dev):

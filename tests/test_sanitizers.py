@@ -8,7 +8,9 @@
 * A negative control: an out-of-bounds oracle call in the same setup must be caught, which
   shows the instrumented libraries are the ones loaded.
 * hg_host_ranges.hpp -- the page-range merge and registration plan of hg_solve_host_*
-  (csrc/hg_host.cpp) -- in a pure C++ unit check (tests/host_ranges_check.cpp).
+  (csrc/hg_host.cpp) -- and hg_host_stage.hpp -- the staged ring of its pageable path and the
+  copy thread pool -- in a pure C++ unit check (tests/host_ranges_check.cpp), also under
+  ThreadSanitizer.
 """
 import os
 import shutil
@@ -126,3 +128,18 @@ def test_host_ranges_under_asan_ubsan(tmp_path):
     r = subprocess.run([str(exe)], capture_output=True, text=True, timeout=120,
                        env=dict(os.environ, ASAN_OPTIONS="detect_leaks=1"))
     assert r.returncode == 0 and "host ranges ok" in r.stdout, r.stdout + r.stderr
+
+
+def test_host_stage_under_tsan(tmp_path):
+    """The copy thread pool and the staged ring (hg_host_stage.hpp) under ThreadSanitizer:
+    several callers sharing one pool's helpers, lists handed over and retired while helpers
+    still hold them."""
+    if not shutil.which("g++") or not _runtime("libtsan.so"):
+        pytest.skip("g++ or the ThreadSanitizer runtime not available")
+    exe = tmp_path / "host_stage_tsan"
+    subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fsanitize=thread",
+                    f"-I{ROOT}/sks-homography_amd/csrc", os.path.join(HERE, "host_ranges_check.cpp"),
+                    "-o", str(exe), "-lpthread"], check=True)
+    r = subprocess.run([str(exe), "30"], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, TSAN_OPTIONS="halt_on_error=1"))
+    assert r.returncode == 0 and "host ranges ok" in r.stdout, r.stdout + r.stderr[-4000:]
