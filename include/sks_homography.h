@@ -122,6 +122,18 @@ int hg_tensor_aca_rect_backward_terms_f32(const float* src, const float* tar, co
                                           float* grad_src, float* grad_tar, float* grad_terms,
                                           void* stream);
 
+/* The all-gradient backward for a batch-uniform (one-value) scale / div, their gradients
+ * summed in ATen-CPU's order: the bits of hg_tensor_aca_rect_backward_terms_f32 followed by
+ * hg_sum_aten_f32(workspace, 2, 3B, 3B, 1, lanes, threads, grad_sd) -- grad_sd[0] = dL/dscale,
+ * grad_sd[1] = dL/ddiv -- with the sum's first level folded into the backward kernel, so the
+ * 24 B of terms a problem has are never written out and read back.
+ * workspace: 6B floats of device scratch.  grad_src may be NULL (not wanted).  lanes and
+ * threads as for hg_sum_aten_f32.  New in 0.3 (hg_version). */
+int hg_tensor_aca_rect_backward_sum_f32(const float* src, const float* tar, const float* grad_H,
+                                        int64_t B, const float* scale, const float* div,
+                                        float* grad_src, float* grad_tar, float* workspace,
+                                        int lanes, int threads, float* grad_sd, void* stream);
+
 /* TensorACA with scale / div broadcast the way the reference composition broadcasts them
  * (Modules_Runtime_Test.py:301-302: torch.mul(div, X) and scale * h_temp, X and h_temp
  * (B,3,1)): any shape broadcastable to (B,3,1) -- one value, one per problem ((B,1,1)),

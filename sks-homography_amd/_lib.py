@@ -38,6 +38,7 @@ SIGNATURES = {
                                            _vp], _int),
     "hg_tensor_aca_rect_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
     "hg_tensor_aca_rect_backward_terms_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _vp], _int),
+    "hg_tensor_aca_rect_backward_sum_f32": ([_vp, _vp, _vp, _i64, _vp, _vp, _vp, _vp, _vp, _int, _int, _vp, _vp], _int),
     "hg_tensor_aca_rect_bcast_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64, _i64, _vp],
                                      _int),
     "hg_tensor_aca_rect_bcast_backward_f32": ([_vp, _vp, _vp, _i64, _vp, _i64, _i64, _vp, _i64,

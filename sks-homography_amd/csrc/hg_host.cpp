@@ -244,6 +244,7 @@ constexpr int kDevSlots = 64;
 struct StageConfig {
     std::atomic<int64_t> ring_bytes{8 << 20};  // one ring stage
     std::atomic<int> depth{4};                 // ring stages a call cycles through
+    std::atomic<int> coherent{1};              // stage memory fine-grained (1) or not (0)
 };
 
 StageConfig& stage_config() {
@@ -264,8 +265,9 @@ host::CopyPool& copy_pool() {
 }
 
 struct Stage {
-    char* host = nullptr;  // pinned, mapped, coherent, portable
+    char* host = nullptr;  // pinned, mapped, portable; coherent or not (StageConfig)
     size_t bytes = 0;
+    int coherent = 1;
     char* dev[kDevSlots] = {};  // its address on device d (filled on first use there)
 };
 
@@ -289,12 +291,12 @@ struct StagePool {
     std::mutex mu;
     std::vector<Stage*> idle;
 
-    // An idle stage of exactly `bytes`, or a new one.
-    int take(size_t bytes, Stage*& out) {
+    // An idle stage of exactly `bytes` and kind, or a new one.
+    int take(size_t bytes, int coherent, Stage*& out) {
         {
             std::lock_guard<std::mutex> lock(mu);
             for (size_t i = idle.size(); i-- > 0;) {
-                if (idle[i]->bytes != bytes) continue;
+                if (idle[i]->bytes != bytes || idle[i]->coherent != coherent) continue;
                 out = idle[i];
                 idle.erase(idle.begin() + (long)i);
                 return 0;
@@ -303,14 +305,16 @@ struct StagePool {
         auto* st = new Stage();
         // coherent (fine-grained): the GPU never holds a stale line of a stage another call
         // refilled; portable: a stage serves calls on any device of the process
-        const hipError_t e = hipHostMalloc(reinterpret_cast<void**>(&st->host), bytes,
-                                           hipHostMallocMapped | hipHostMallocCoherent |
-                                               hipHostMallocPortable);
+        const hipError_t e = hipHostMalloc(
+            reinterpret_cast<void**>(&st->host), bytes,
+            hipHostMallocMapped | hipHostMallocPortable |
+                (coherent ? hipHostMallocCoherent : hipHostMallocNonCoherent));
         if (e != hipSuccess) {  // nothing half-made is kept
             delete st;
             return (int)e;
         }
         st->bytes = bytes;
+        st->coherent = coherent;
         ++stage_stats().made;
         out = st;
         return 0;
@@ -376,7 +380,40 @@ int launch(int algo, const T* s, const T* t, T* h, int64_t n, int layout, int fl
     }
 }
 
-// The staged solve of a batch with at least one pageable buffer (v[i].dev == nullptr).
+// Streams of the ring, per device: created on first need, never destroyed (no HIP call at
+// exit), handed to one call at a time.  Consecutive chunks run on different streams, so their
+// kernels overlap: one chunk's kernel alone cannot keep both PCIe directions busy through its
+// ramp-up and drain (profiles/r06: 145 us per 8 MiB chunk on one stream, the link's rate only
+// with several in flight).
+struct StreamPool {
+    std::mutex mu;
+    std::vector<std::pair<int, hipStream_t>> idle;
+
+    int take(int dev, hipStream_t& out) {
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            for (size_t i = idle.size(); i-- > 0;) {
+                if (idle[i].first != dev) continue;
+                out = idle[i].second;
+                idle.erase(idle.begin() + (long)i);
+                return 0;
+            }
+        }
+        return (int)hipStreamCreateWithFlags(&out, hipStreamNonBlocking);
+    }
+    void give_back(int dev, hipStream_t x) {
+        std::lock_guard<std::mutex> lock(mu);
+        idle.push_back({dev, x});
+    }
+};
+
+StreamPool& stream_pool() {
+    static StreamPool* p = new StreamPool();  // never destroyed
+    return *p;
+}
+
+// The staged solve of a batch with at least one pageable buffer (v[i].dev == nullptr).  `s` is
+// the caller's stream: device-memory buffers are ordered after the work queued on it.
 template <typename T>
 int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipStream_t s) {
     host::StagePlan p;
@@ -398,20 +435,35 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
             if (p.mode[i] == host::kDirect) p.mode[i] = v[i].in_host ? host::kCpu : host::kDma;
         if (!host::plan_chunks(p, cap)) return kInvalid;
     }
+    const bool device_data = !v[0].in_host || !v[1].in_host || !v[2].in_host;
     const int64_t K = p.chunks;
     const int D = (int)std::min<int64_t>(K, std::max(1, stage_config().depth.load()));
+    // one chunk: the caller's stream; several: a ring stream per stage
+    const bool ring = K > 1;
     std::vector<Stage*> st((size_t)D, nullptr);
     std::vector<char*> sd((size_t)D, nullptr);
+    std::vector<hipStream_t> ss((size_t)D, s);
+    std::vector<bool> own((size_t)D, false);
     std::vector<hipEvent_t> ev;
-    int rc = 0;
+    int rc = 0, dev = 0;
+    const int coherent = stage_config().coherent.load();
     for (int j = 0; j < D && !rc; ++j) {
-        rc = stage_pool().take(cap, st[(size_t)j]);
+        rc = stage_pool().take(cap, coherent, st[(size_t)j]);
         if (!rc) rc = stage_dev(st[(size_t)j], sd[(size_t)j]);
     }
-    if (!rc && K > 1) {
-        ev.assign((size_t)D, nullptr);
-        for (int j = 0; j < D && !rc; ++j)
+    if (!rc && ring) {
+        rc = (int)hipGetDevice(&dev);
+        for (int j = 0; j < D && !rc; ++j) {
+            rc = stream_pool().take(dev, ss[(size_t)j]);
+            own[(size_t)j] = rc == 0;
+        }
+        ev.assign((size_t)D + 1, nullptr);
+        for (int j = 0; j <= D && !rc; ++j)
             rc = (int)hipEventCreateWithFlags(&ev[(size_t)j], hipEventDisableTiming);
+        if (!rc && device_data) {  // the ring streams start after the caller's queued work
+            rc = (int)hipEventRecord(ev[(size_t)D], s);
+            for (int j = 0; j < D && !rc; ++j) rc = (int)hipStreamWaitEvent(ss[(size_t)j], ev[(size_t)D], 0);
+        }
     }
     ++stage_stats().calls;
     if (!small) ++stage_stats().ring_calls;
@@ -439,16 +491,39 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
         for (const host::Piece& x : pieces) b += (int64_t)x.bytes;
         stats.copy_bytes += b;
     };
+    // chunks launched whose H has not been copied out yet, oldest first (chunk k is in stage
+    // k % D); H leaves as soon as a chunk is done, so only the last chunk's copy is exposed
+    int64_t out_next = 0;
+    auto take_done = [&](int64_t upto, bool wait_first) -> int {  // copy out chunks < upto that are done
+        while (out_next < upto) {
+            const int j = (int)(out_next % D);
+            if (ring) {
+                if (wait_first) {
+                    const int64_t t0 = now_ns();
+                    const int e = (int)hipEventSynchronize(ev[(size_t)j]);
+                    stats.wait_ns += now_ns() - t0;
+                    if (e) return e;
+                    wait_first = false;
+                } else {
+                    const hipError_t q = hipEventQuery(ev[(size_t)j]);
+                    if (q == hipErrorNotReady) break;
+                    if (q != hipSuccess) return (int)q;
+                }
+            }
+            copy_out(out_next, j);
+            ++out_next;
+        }
+        return 0;
+    };
     for (int64_t k = 0; k < K && !rc; ++k) {
         const int j = (int)(k % D);
+        hipStream_t q = ss[(size_t)j];
         pieces.clear();
-        if (k >= D) {  // stage j still holds chunk k - D: wait for its kernel, take its H out
-            const int64_t t0 = now_ns();
-            rc = (int)hipEventSynchronize(ev[(size_t)j]);
-            stats.wait_ns += now_ns() - t0;
-            if (rc) break;
-            copy_out(k - D, j);
-        }
+        // stage j still holds chunk k - D: it (and any chunk before it) must be out first;
+        // chunks after it that are already done leave too
+        rc = take_done(k - D + 1, k >= D && out_next <= k - D);
+        if (!rc) rc = take_done(k, false);
+        if (rc) break;
         copy_in(k, j);
         run_pieces();
         const int64_t lo = p.lo(k), c = p.count(k);
@@ -464,34 +539,49 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
                 rc = (int)hipMemcpy2DAsync(st[(size_t)j]->host + p.off[i], (size_t)c * E,
                                            static_cast<const char*>(v[i].dev) + (size_t)lo * E,
                                            (size_t)n * E, (size_t)c * E, (size_t)p.rows[i],
-                                           hipMemcpyDeviceToHost, s);
+                                           hipMemcpyDeviceToHost, q);
         if (!rc)
             rc = launch<T>(algo, reinterpret_cast<const T*>(ptr[0]),
                            reinterpret_cast<const T*>(ptr[1]), reinterpret_cast<T*>(ptr[2]), c,
-                           layout, flags, s, true);
+                           layout, flags, q, true);
         if (!rc && p.mode[2] == host::kDma)
             rc = (int)hipMemcpy2DAsync(static_cast<char*>(v[2].dev) + (size_t)lo * E,
                                        (size_t)n * E, st[(size_t)j]->host + p.off[2],
                                        (size_t)c * E, (size_t)c * E, (size_t)p.rows[2],
-                                       hipMemcpyHostToDevice, s);
-        if (!rc && K > 1) rc = (int)hipEventRecord(ev[(size_t)j], s);
-        ++stage_stats().chunks;
+                                       hipMemcpyHostToDevice, q);
+        if (!rc && ring) rc = (int)hipEventRecord(ev[(size_t)j], q);
+        ++stats.chunks;
     }
-    // every stage's last chunk: H out once the stream has drained
+    // the chunks still out, in order, each copied as soon as it is done
+    if (ring) {
+        while (!rc && out_next < K) {
+            pieces.clear();
+            rc = take_done(out_next + 1, true);
+            if (!rc) rc = take_done(K, false);
+            if (!rc) run_pieces();
+        }
+    }
+    // every stream drained (also after an error: no stage is reused under a running kernel)
     const int64_t t_drain = now_ns();
-    const hipError_t e = hipStreamSynchronize(s);
+    hipError_t e = hipSuccess;
+    for (int j = 0; j < (ring ? D : 1); ++j) {
+        const hipError_t x = hipStreamSynchronize(ss[(size_t)j]);
+        if (e == hipSuccess) e = x;
+    }
     stats.wait_ns += now_ns() - t_drain;
-    if (!rc && e == hipSuccess) {
+    if (!ring && !rc && e == hipSuccess) {  // one chunk: H out now
         pieces.clear();
-        for (int64_t k = std::max<int64_t>(0, K - D); k < K; ++k) copy_out(k, (int)(k % D));
+        copy_out(0, 0);
         run_pieces();
     }
     for (hipEvent_t x : ev)
         if (x) (void)hipEventDestroy(x);
+    // a stream that did not drain may still have a kernel reading or writing a stage: neither
+    // is handed to another call
+    for (int j = 0; j < D; ++j)
+        if (own[(size_t)j] && e == hipSuccess) stream_pool().give_back(dev, ss[(size_t)j]);
     for (Stage* x : st) {
         if (!x) continue;
-        // a stream that did not drain may still have a kernel reading or writing the stage:
-        // it is never handed to another call
         if (e == hipSuccess) stage_pool().give_back(x);
         else ++stage_stats().leaked;
     }
@@ -607,6 +697,15 @@ int hg_internal_host_stage_config(int64_t ring_bytes, int depth, int threads, in
     if (depth > 0) c.depth = depth;
     if (threads > 0) copy_pool().set_threads(threads);
     return 0;
+}
+
+// Library-internal (tools/ring_probe.py): stage memory fine-grained (1, coherent) or coarse-
+// grained (0, non-coherent) from now on; -1 only queries.  Returns the previous setting.
+int hg_internal_host_stage_coherent(int coherent) {
+    StageConfig& c = stage_config();
+    const int prev = c.coherent.load();
+    if (coherent == 0 || coherent == 1) c.coherent = coherent;
+    return prev;
 }
 
 // {stages allocated, staged calls, chunks solved, stages withheld after a failed stream,

@@ -18,6 +18,7 @@
 #include <cstdint>
 #include <cstring>
 #include <deque>
+#include <emmintrin.h>
 #include <mutex>
 #include <thread>
 #include <vector>
@@ -127,6 +128,37 @@ inline void chunk_pieces(const StagePlan& p, int i, int64_t k, const char* user_
     }
 }
 
+// One piece's copy with streaming (non-temporal) stores: the destination -- a stage the GPU
+// reads next over PCIe, or the caller's H, read by nobody before the call returns -- is not
+// read first (no read-for-ownership) and does not evict the copy threads' caches.  Measured on
+// the MI355X box's EPYC host (tools/ring_probe.py, profiles/r06): the copies share the host's
+// memory with the GPU's PCIe reads of the stages, and the read-for-ownership traffic of
+// ordinary stores was what the ring ran short of.  Short or unaligned ends go through memcpy.
+inline void copy_streaming(char* dst, const char* src, size_t bytes) {
+    const size_t head = (64 - (reinterpret_cast<uintptr_t>(dst) & 63)) & 63;
+    if (bytes < head + 256) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    std::memcpy(dst, src, head);
+    dst += head;
+    src += head;
+    bytes -= head;
+    const size_t body = bytes & ~(size_t)63;
+    for (size_t i = 0; i < body; i += 64) {
+        const __m128i a = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i));
+        const __m128i b = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 16));
+        const __m128i c = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 32));
+        const __m128i d = _mm_loadu_si128(reinterpret_cast<const __m128i*>(src + i + 48));
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i), a);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 16), b);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 32), c);
+        _mm_stream_si128(reinterpret_cast<__m128i*>(dst + i + 48), d);
+    }
+    std::memcpy(dst + body, src + body, bytes - body);
+    _mm_sfence();  // the streamed lines are globally visible before the caller goes on
+}
+
 // Runs lists of copies on the calling thread and up to threads-1 helper threads.  Helpers
 // are started on first need and never exit (no thread, and no library state, is torn down at
 // process exit: the pool itself is never destroyed -- hg_host.cpp).  Each caller works on its
@@ -182,7 +214,7 @@ class CopyPool {
 
     static void work_on(Job& job) {
         for (size_t i = job.next.fetch_add(1); i < job.n; i = job.next.fetch_add(1))
-            std::memcpy(job.p[i].dst, job.p[i].src, job.p[i].bytes);
+            copy_streaming(job.p[i].dst, job.p[i].src, job.p[i].bytes);
     }
 
     void helper() {

@@ -15,12 +15,14 @@
 // is HBM bandwidth, not VALU.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdint>
 
 #include "hg_aos.hpp"
 #include "hg_launch.hpp"
 #include "hg_rect.hpp"
 #include "hg_reduce.hpp"
+#include "hg_rect_sum.hpp"
 #include "hg_soa.hpp"
 #include "hg_solvers.hpp"
 #include "sks_homography.h"
@@ -939,46 +941,112 @@ int hg_sum_rocm_f32(const float* x, int64_t B, int kind, float* out, float* work
                       static_cast<const float*>(workspace), out);
 }
 
-int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
-                    int lanes, int threads, float* out, void* stream) {
-    if (rows < 0 || m < 0 || lanes < 1 || lanes > hg::kAtenMaxLanes || threads < 1 ||
-        threads > hg::kAtenMaxThreads || (threads > 1 && lanes < 4))
-        return hg::kErrInvalid;
-    if (rows == 0) return 0;
-    if (!out || (m > 0 && !x)) return hg::kErrInvalid;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-    const int64_t want = hg::ceil_div(m, hg::kAtenGrain);
-    const int64_t chunks = threads > 1 && m >= hg::kAtenGrain ? (want < threads ? want : threads) : 1;
-    const int64_t runs = rows * chunks;
-    if (runs > 65535) return hg::kErrInvalid;
-    const hg::AtenSum a{x, row_stride, elem_stride, m, chunks > 1 ? hg::ceil_div(m, chunks) : m,
-                        (int)chunks, lanes};
+}  // extern "C"
+
+namespace hg {
+// The ATen-order sum's runs of rows x m floats (hg_sum_aten_f32's chunking: min(T, ceil(m /
+// 32768)) chunks of ceil(m / chunks) with T threads and m >= 32768, else one).
+inline AtenSum aten_sum_of(float* x, int64_t m, int64_t row_stride, int64_t elem_stride,
+                           int lanes, int threads) {
+    const int64_t want = ceil_div(m, kAtenGrain);
+    const int64_t chunks = threads > 1 && m >= kAtenGrain ? (want < threads ? want : threads) : 1;
+    return AtenSum{x, row_stride, elem_stride, m, chunks > 1 ? ceil_div(m, chunks) : m,
+                   (int)chunks, lanes};
+}
+
+// Levels 1 ... 4 of the sum over `rows` rows of a; `blocks_done`: level 0 already folded
+// in place (rect_backward_sum_l0), so level 1 reads block sums (aten_sum_l1_blocks).
+inline int aten_sum_launch(const AtenSum& a, int64_t rows, int threads, int lanes, float* out,
+                           hipStream_t s, bool blocks_done) {
+    const int64_t runs = rows * a.chunks;
+    if (runs > 65535) return kErrInvalid;
     // The grids cover the largest extent over EVERY run: a shorter run (the last chunk) may
     // take a smaller level step and so have more super-blocks / level-2 groups than run 0.
     int64_t g1_max = -1, l2_max = 0, step_max = 0;
     for (int64_t run = 0; run < runs; ++run) {
-        const hg::AtenRun r(a, (int)run);
-        if (r.step > hg::kAtenMaxStep) return hg::kErrInvalid;  // a run of > 2^35 rows per stream
+        const AtenRun r(a, (int)run);
+        if (r.step > kAtenMaxStep) return kErrInvalid;  // a run of > 2^35 rows per stream
         if (r.nb > 0 && r.g1 > g1_max) g1_max = r.g1;
         if (r.g1 > 0 && (r.g2 + 1) * r.S > l2_max) l2_max = (r.g2 + 1) * r.S;
         if (r.step * r.S > step_max) step_max = r.step * r.S;
     }
     if (g1_max >= 0) {
         const int64_t bx = g1_max + 1;  // one block per super-block (the last may be partial)
-        if (bx > 0x7fffffffLL) return hg::kErrInvalid;
-        const int rc = hg::launch(hg::aten_sum_l1, dim3((unsigned)bx, (unsigned)runs),
-                                  hg::kAtenL1Threads, (size_t)step_max * sizeof(float), s, a);
+        if (bx > 0x7fffffffLL) return kErrInvalid;
+        const int rc = blocks_done
+                           ? launch(aten_sum_l1_blocks, dim3((unsigned)bx, (unsigned)runs), 64, 0, s, a)
+                           : launch(aten_sum_l1, dim3((unsigned)bx, (unsigned)runs), kAtenL1Threads,
+                                    (size_t)step_max * sizeof(float), s, a);
         if (rc) return rc;
     }
     if (l2_max > 0) {
-        const int64_t bx = hg::ceil_div(l2_max, (int64_t)256);
-        if (bx > 0x7fffffffLL) return hg::kErrInvalid;
-        const int rc = hg::launch(hg::aten_sum_l2, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
+        const int64_t bx = ceil_div(l2_max, (int64_t)256);
+        if (bx > 0x7fffffffLL) return kErrInvalid;
+        const int rc = launch(aten_sum_l2, dim3((unsigned)bx, (unsigned)runs), 256, 0, s, a);
         if (rc) return rc;
     }
-    const int rc = hg::launch(hg::aten_sum_l3, (unsigned)runs, 64, 0, s, a, out);
-    if (rc || chunks == 1) return rc;
-    return hg::launch(hg::aten_sum_l4, (unsigned)rows, 64, 0, s, a, threads, lanes, out);
+    const int rc = launch(aten_sum_l3, (unsigned)runs, 64, 0, s, a, out);
+    if (rc || a.chunks == 1) return rc;
+    return launch(aten_sum_l4, (unsigned)rows, 64, 0, s, a, threads, lanes, out);
+}
+
+inline bool aten_sum_args_ok(int lanes, int threads) {
+    return lanes >= 1 && lanes <= kAtenMaxLanes && threads >= 1 && threads <= kAtenMaxThreads &&
+           (threads == 1 || lanes >= 4);
+}
+}  // namespace hg
+
+extern "C" {
+
+int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64_t elem_stride,
+                    int lanes, int threads, float* out, void* stream) {
+    if (rows < 0 || m < 0 || !hg::aten_sum_args_ok(lanes, threads)) return hg::kErrInvalid;
+    if (rows == 0) return 0;
+    if (!out || (m > 0 && !x)) return hg::kErrInvalid;
+    const hg::AtenSum a = hg::aten_sum_of(x, m, row_stride, elem_stride, lanes, threads);
+    return hg::aten_sum_launch(a, rows, threads, lanes, out, reinterpret_cast<hipStream_t>(stream),
+                               false);
+}
+
+int hg_tensor_aca_rect_backward_sum_f32(const float* src, const float* tar, const float* grad_H,
+                                        int64_t B, const float* scale, const float* div,
+                                        float* grad_src, float* grad_tar, float* workspace,
+                                        int lanes, int threads, float* grad_sd, void* stream) {
+    if (B < 0 || !hg::aten_sum_args_ok(lanes, threads)) return hg::kErrInvalid;
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+    if (!grad_sd) return hg::kErrInvalid;
+    if (B == 0) return (int)hipMemsetAsync(grad_sd, 0, 2 * sizeof(float), s);  // sums of nothing
+    if (!src || !tar || !grad_H || !scale || !div || !grad_tar || !workspace) return hg::kErrInvalid;
+    if (B > (int64_t)1 << 40) return hg::kErrInvalid;
+    const int64_t m = 3 * B;
+    const hg::AtenSum a = hg::aten_sum_of(workspace, m, m, 1, lanes, threads);
+    const bool aligned = hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(grad_tar) &&
+                         (!grad_src || hg::aligned16(grad_src));
+    if (!aligned) {  // the two-launch form: the same bits
+        int rc = hg::launch_rect_backward<hg::kAtenCpu, hg::kSdTerms>(
+            src, tar, grad_H, B, scale, div, grad_src, grad_tar, workspace, s);
+        if (rc) return rc;
+        return hg::aten_sum_launch(a, 2, threads, lanes, grad_sd, s, false);
+    }
+    int64_t units = 0, lds_floats = 0;
+    for (int c = 0; c < a.chunks; ++c) {
+        const hg::AtenRun r(a, c);
+        if (r.step > hg::kAtenMaxStep) return hg::kErrInvalid;
+        units = std::max(units, hg::rect_sum_units(r));
+        lds_floats = std::max(lds_floats, hg::rect_sum_group(r) * r.step * r.S);
+    }
+    if (units > 0x7fffffffLL) return hg::kErrInvalid;
+    const size_t lds = 2 * (size_t)lds_floats * sizeof(float);  // <= 2 x 8192 floats (step 256)
+    const dim3 grid((unsigned)units, (unsigned)a.chunks);
+    const bool nt = B * 232 > hg::kMallResidentBytes;
+#define HG_RS(W, NT)                                                                          \
+    hg::launch(hg::rect_backward_sum_l0<W, NT>, grid, hg::kRectSumThreads, lds, s, src, tar, \
+               grad_H, scale, div, grad_src, grad_tar, a)
+    const int rc = grad_src ? (nt ? HG_RS(true, true) : HG_RS(true, false))
+                            : (nt ? HG_RS(false, true) : HG_RS(false, false));
+#undef HG_RS
+    if (rc) return rc;
+    return hg::aten_sum_launch(a, 2, threads, lanes, grad_sd, s, true);
 }
 
 const char* hg_version(void) { return "sks-homography-amd 0.3 (gfx950)"; }

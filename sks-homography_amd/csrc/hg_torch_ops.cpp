@@ -261,6 +261,18 @@ std::tuple<at::Tensor, at::Tensor, at::Tensor, at::Tensor> rect_backward(
         at::Tensor part = need_scale_div ? at::empty({2, 3 * B}, tar.options()) : none;
         float* gs = need_src && B ? g_src.data_ptr<float>() : nullptr;
         float* pp = need_scale_div && B ? part.data_ptr<float>() : nullptr;
+        if (order == HG_ORDER_ATEN_CPU && need_scale_div) {
+            // the backward and ATen's batch sum in one pass over the terms (the bits of the
+            // terms kernel + hg_sum_aten_f32 below)
+            at::Tensor g_sd = at::empty({2}, tar.options());
+            hip_ok(hg_tensor_aca_rect_backward_sum_f32(
+                       src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
+                       scale_.data_ptr<float>(), div_.data_ptr<float>(), gs,
+                       g_tar.data_ptr<float>(), pp, kAtenLanes, threads, g_sd.data_ptr<float>(), st),
+                   "hg_tensor_aca_rect_backward_sum_f32");
+            return {g_src, g_tar, g_sd.slice(0, 0, 1).reshape(scale_.sizes()),
+                    g_sd.slice(0, 1, 2).reshape(div_.sizes())};
+        }
         if (order == HG_ORDER_ATEN_CPU)
             hip_ok(hg_tensor_aca_rect_backward_terms_f32(
                        src.data_ptr<float>(), tar.data_ptr<float>(), grad.data_ptr<float>(), B,
