@@ -890,6 +890,11 @@ RECT_LAYOUT_MIN_BYTES = 132
 # terms 24 out.  PMC reads 183.7 / 256.2 B (profiles/pmc_traffic.json)
 RECT_BWD_TAR_LAYOUT_MIN_BYTES = 180
 RECT_BWD_ALL_LAYOUT_MIN_BYTES = 252
+# the fused all-gradient op (round 6: hg_tensor_aca_rect_backward_sum_f32) writes no terms:
+# algorithmic src M 8 + tar 48 + dL/dH 36 in, dL/dtar 48 + dL/dsrc 48 out; layout floor with
+# src's whole 48-B records (the level-0 block sums it leaves are 24 / step B, ~1.5 B)
+RECT_BWD_SUM_BYTES = 188
+RECT_BWD_SUM_LAYOUT_MIN_BYTES = 228
 
 # imgs/GPU-runtime.png (Table 8), N = 1M, FP64 SoA, unnamed CUDA GPU
 TABLE8_US = {"aca": 245.0, "sks": 436.0, "gpt": 8390.0, "ge": 589.0}
@@ -1814,26 +1819,44 @@ def main():
                 f_ba()
             _, ms_bt = timed_region(d, f_bt, 20)
             _, ms_ba = timed_region(d, f_ba, 20)
-            # the all-gradient backward kernel alone (the raw C ABI: no batch sum, no allocation)
+            # the all-gradient op's kernels apart (raw C ABI, no allocation): the fused backward
+            # kernel alone (rect_backward_sum_l0: gradients + the sum's level 0), and the round-5
+            # two-launch form (the terms kernel, then hg_sum_aten_f32 over its 24 B of terms)
             gs_k, gt_k = torch.empty_like(bs_h), torch.empty_like(bt_h)
             terms_k = torch.empty((2, big, 3), device=d.dev)
+            sd_k = torch.empty(2, device=d.dev)
             stream_k = torch.cuda.current_stream(d.dev).cuda_stream
-            f_bk = lambda: pkg._lib.call(  # noqa: E731
-                "hg_tensor_aca_rect_backward_terms_f32", bs_h.data_ptr(), bt_h.data_ptr(),
-                gHb.data_ptr(), big, bsc.data_ptr(), bdv.data_ptr(), gs_k.data_ptr(),
-                gt_k.data_ptr(), terms_k.data_ptr(), stream_k)
+            T_bw = torch.get_num_threads()
+            import ctypes
+            lib_k = pkg.lib()
+            lib_k.hg_internal_rect_backward_sum_l0.argtypes = (
+                [ctypes.c_void_p] * 3 + [ctypes.c_int64] + [ctypes.c_void_p] * 5
+                + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p])
+            f_bk = lambda: lib_k.hg_internal_rect_backward_sum_l0(  # noqa: E731
+                bs_h.data_ptr(), bt_h.data_ptr(), gHb.data_ptr(), big, bsc.data_ptr(),
+                bdv.data_ptr(), gs_k.data_ptr(), gt_k.data_ptr(), terms_k.data_ptr(), 8, T_bw,
+                stream_k)
+
+            def f_b2():
+                pkg._lib.call("hg_tensor_aca_rect_backward_terms_f32", bs_h.data_ptr(),
+                              bt_h.data_ptr(), gHb.data_ptr(), big, bsc.data_ptr(), bdv.data_ptr(),
+                              gs_k.data_ptr(), gt_k.data_ptr(), terms_k.data_ptr(), stream_k)
+                pkg._lib.call("hg_sum_aten_f32", terms_k.data_ptr(), 2, 3 * big, 3 * big, 1, 8,
+                              T_bw, sd_k.data_ptr(), stream_k)
             for _ in range(5):
                 f_bk()
+                f_b2()
             _, ms_bk = timed_region(d, f_bk, 20)
-            del gs_k, gt_k, terms_k
-            # a plain copy of the same 252 B per problem (half read, half written): what the
+            _, ms_b2 = timed_region(d, f_b2, 20)
+            del gs_k, gt_k, terms_k, sd_k
+            # a plain copy of the same 228 B per problem (half read, half written): what the
             # box's HBM gives this read/write mix with two streams instead of the layout's seven
-            cpy_src = torch.empty(big * RECT_BWD_ALL_LAYOUT_MIN_BYTES // 8, dtype=torch.float32,
+            cpy_src = torch.empty(big * RECT_BWD_SUM_LAYOUT_MIN_BYTES // 8, dtype=torch.float32,
                                   device=d.dev)
             cpy_dst = torch.empty_like(cpy_src)
             f_cp = lambda: pkg._lib.call(  # noqa: E731
                 "hg_stream_copy", cpy_src.data_ptr(), cpy_dst.data_ptr(),
-                big * RECT_BWD_ALL_LAYOUT_MIN_BYTES // 2, stream_k)
+                big * RECT_BWD_SUM_LAYOUT_MIN_BYTES // 2, stream_k)
             for _ in range(5):
                 f_cp()
             _, ms_cp = timed_region(d, f_cp, 20)
@@ -1857,21 +1880,26 @@ def main():
                 "large_backward_tar_us": round(ms_bt * 1e3, 2),
                 "large_backward_tar_frac": round(big * 140 / (ms_bt * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "large_backward_tar_traffic": pmc_detail("rect_backward_tar"),
+                # everything (dL/dsrc, dL/dtar, the (1,) scale / div in ATen-CPU's order): one
+                # fused backward kernel (the sum's level 0 in LDS) + the sum's small upper levels
                 "large_backward_all_us": round(ms_ba * 1e3, 2),
-                "large_backward_all_frac": round(big * 212 / (ms_ba * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                "large_backward_all_frac": round(big * RECT_BWD_SUM_BYTES / (ms_ba * 1e-3) / 1e9
+                                                 / HBM_PEAK_GBPS, 4),
                 "large_backward_all_traffic": pmc_detail(
-                    "rect_backward_all", "the backward kernel alone; the scale / div sum "
-                    "(hg_sum_aten_f32) is in large_backward_all_us"),
+                    "rect_backward_sum", "the fused backward kernel alone (rect_backward_sum_l0)"),
+                "large_backward_all_kernel_us": round(ms_bk * 1e3, 2),
+                "large_backward_all_op_over_kernel": round(ms_ba / ms_bk, 4),
+                "large_backward_all_two_launch_us": round(ms_b2 * 1e3, 2),
+                "large_backward_all_aten_threads": T_bw,
                 # against the (B,3,4) layout's own floors (RECT_BWD_*_LAYOUT_MIN_BYTES)
                 "large_backward_tar_layout_min_bytes_per_problem": RECT_BWD_TAR_LAYOUT_MIN_BYTES,
                 "large_backward_tar_layout_min_frac": round(
                     big * RECT_BWD_TAR_LAYOUT_MIN_BYTES / (ms_bt * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "large_backward_all_layout_min_bytes_per_problem": RECT_BWD_ALL_LAYOUT_MIN_BYTES,
+                "large_backward_all_layout_min_bytes_per_problem": RECT_BWD_SUM_LAYOUT_MIN_BYTES,
                 "large_backward_all_layout_min_frac": round(
-                    big * RECT_BWD_ALL_LAYOUT_MIN_BYTES / (ms_ba * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
-                "large_backward_all_kernel_us": round(ms_bk * 1e3, 2),
+                    big * RECT_BWD_SUM_LAYOUT_MIN_BYTES / (ms_ba * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "large_backward_all_kernel_layout_min_frac": round(
-                    big * RECT_BWD_ALL_LAYOUT_MIN_BYTES / (ms_bk * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                    big * RECT_BWD_SUM_LAYOUT_MIN_BYTES / (ms_bk * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
                 "large_backward_all_copy_yardstick_us": round(ms_cp * 1e3, 2),
                 # > 1: the kernel moves its layout's bytes faster than a plain copy of them
                 "large_backward_all_kernel_vs_copy": round(ms_cp / ms_bk, 4),

@@ -241,9 +241,13 @@ Registry& registry() {
 constexpr size_t kSmallStageBytes = 128 << 10;
 constexpr int kDevSlots = 64;
 
+// Ring shape: 32 MiB stages, 6 deep (192 MiB of pinned memory while a large call runs).  At 10 M
+// f32 AoS from pageable memory, 8 copy threads (tools/ring_probe.py, profiles/r06/ring_*.json):
+// 8 MiB x 4 18.8 ms, 16 x 6 17.2, 32 x 6 16.1, 64 x 6 14.6 -- larger stages keep more of the
+// PCIe link busy per kernel but hold more pinned memory and lengthen the ring's fill and drain.
 struct StageConfig {
-    std::atomic<int64_t> ring_bytes{8 << 20};  // one ring stage
-    std::atomic<int> depth{4};                 // ring stages a call cycles through
+    std::atomic<int64_t> ring_bytes{32 << 20};  // one ring stage
+    std::atomic<int> depth{6};                  // ring stages (and streams) a call cycles through
     std::atomic<int> coherent{1};              // stage memory fine-grained (1) or not (0)
 };
 
@@ -319,9 +323,21 @@ struct StagePool {
         out = st;
         return 0;
     }
+    // Idle stages are kept up to kIdleCap bytes (so a burst of concurrent large calls does not
+    // pin its peak for the process's life); a stage past the cap is freed here, in the call.
+    static constexpr size_t kIdleCap = (size_t)1 << 30;
     void give_back(Stage* st) {
-        std::lock_guard<std::mutex> lock(mu);
-        idle.push_back(st);
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            size_t held = 0;
+            for (const Stage* x : idle) held += x->bytes;
+            if (held + st->bytes <= kIdleCap) {
+                idle.push_back(st);
+                return;
+            }
+        }
+        (void)hipHostFree(st->host);
+        delete st;
     }
 };
 

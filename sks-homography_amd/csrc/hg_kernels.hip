@@ -1008,12 +1008,47 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
                                false);
 }
 
+}  // extern "C"
+
+namespace hg {
+// level0_only: the fused backward kernel alone (its block sums left in the workspace) -- for
+// the bench's op-over-kernel figure (hg_internal_rect_backward_sum_l0).
+inline int rect_backward_sum(const float* src, const float* tar, const float* grad_H, int64_t B,
+                             const float* scale, const float* div, float* grad_src,
+                             float* grad_tar, float* workspace, int lanes, int threads,
+                             float* grad_sd, hipStream_t s, bool level0_only);
+}  // namespace hg
+
+extern "C" {
+
+// Library-internal (bench.py): rect_backward_sum_l0 alone, as hg_tensor_aca_rect_backward_sum_f32
+// launches it (aligned tensors only).
+int hg_internal_rect_backward_sum_l0(const float* src, const float* tar, const float* grad_H,
+                                     int64_t B, const float* scale, const float* div,
+                                     float* grad_src, float* grad_tar, float* workspace, int lanes,
+                                     int threads, void* stream) {
+    float dummy = 0.f;
+    return hg::rect_backward_sum(src, tar, grad_H, B, scale, div, grad_src, grad_tar, workspace,
+                                 lanes, threads, &dummy, reinterpret_cast<hipStream_t>(stream), true);
+}
+
 int hg_tensor_aca_rect_backward_sum_f32(const float* src, const float* tar, const float* grad_H,
                                         int64_t B, const float* scale, const float* div,
                                         float* grad_src, float* grad_tar, float* workspace,
                                         int lanes, int threads, float* grad_sd, void* stream) {
+    return hg::rect_backward_sum(src, tar, grad_H, B, scale, div, grad_src, grad_tar, workspace,
+                                 lanes, threads, grad_sd, reinterpret_cast<hipStream_t>(stream),
+                                 false);
+}
+
+}  // extern "C"
+
+namespace hg {
+inline int rect_backward_sum(const float* src, const float* tar, const float* grad_H, int64_t B,
+                             const float* scale, const float* div, float* grad_src,
+                             float* grad_tar, float* workspace, int lanes, int threads,
+                             float* grad_sd, hipStream_t s, bool level0_only) {
     if (B < 0 || !hg::aten_sum_args_ok(lanes, threads)) return hg::kErrInvalid;
-    hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     if (!grad_sd) return hg::kErrInvalid;
     if (B == 0) return (int)hipMemsetAsync(grad_sd, 0, 2 * sizeof(float), s);  // sums of nothing
     if (!src || !tar || !grad_H || !scale || !div || !grad_tar || !workspace) return hg::kErrInvalid;
@@ -1023,6 +1058,7 @@ int hg_tensor_aca_rect_backward_sum_f32(const float* src, const float* tar, cons
     const bool aligned = hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(grad_tar) &&
                          (!grad_src || hg::aligned16(grad_src));
     if (!aligned) {  // the two-launch form: the same bits
+        if (level0_only) return hg::kErrInvalid;
         int rc = hg::launch_rect_backward<hg::kAtenCpu, hg::kSdTerms>(
             src, tar, grad_H, B, scale, div, grad_src, grad_tar, workspace, s);
         if (rc) return rc;
@@ -1045,9 +1081,12 @@ int hg_tensor_aca_rect_backward_sum_f32(const float* src, const float* tar, cons
     const int rc = grad_src ? (nt ? HG_RS(true, true) : HG_RS(true, false))
                             : (nt ? HG_RS(false, true) : HG_RS(false, false));
 #undef HG_RS
-    if (rc) return rc;
+    if (rc || level0_only) return rc;
     return hg::aten_sum_launch(a, 2, threads, lanes, grad_sd, s, true);
 }
+}  // namespace hg
+
+extern "C" {
 
 const char* hg_version(void) { return "sks-homography-amd 0.3 (gfx950)"; }
 

@@ -40,9 +40,9 @@ KEYS = {
     "tensor_aca_rect_bcast": ("void hg::tensor_aca_rect_bcast_staged<true, 0>", M16 * 100),
     # dL/dtar alone: src M 8 + tar 48 + dL/dH 36 in, dL/dtar 48 out
     "rect_backward_tar": ("void hg::tensor_aca_rect_backward_staged<false, 0, true, 0, false>", M16 * 140),
-    # + dL/dsrc 48 and the (problem, row) scale / div terms 24 out
-    "rect_backward_all": ("void hg::tensor_aca_rect_backward_staged<true, 2, true, 0, false>", M16 * 212),
     "aten_sum_l1": ("hg::aten_sum_l1", None),
+    # the fused all-gradient backward (round 6): no terms out, the sum's level 0 in LDS
+    "rect_backward_sum": ("void hg::rect_backward_sum_l0<true, true>", M16 * 188),
     "tensor_aca_offsets": ("void hg::tensor_aca_offsets_kernel", M16 * 76),
     # corner 8 + offsets 32 + dL/dH 36 in, dL/doffsets 32 out
     "offsets_backward": ("void hg::tensor_aca_offsets_backward_staged<false, true>", M16 * 108),

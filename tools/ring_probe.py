@@ -40,6 +40,9 @@ def main():
     ap.add_argument("--out", default="gpurun_out/ring_probe.json")
     ap.add_argument("--quick", action="store_true")
     ap.add_argument("--no-numa", action="store_true")
+    ap.add_argument("--stages", default="", help="MiB list, e.g. 16,32,64")
+    ap.add_argument("--depths", default="")
+    ap.add_argument("--threads", default="")
     a = ap.parse_args()
     import bench  # the bench's own NUMA binding, before anything touches the GPU
     numa = bench.bind_numa(0) if not a.no_numa else None
@@ -77,6 +80,12 @@ def main():
     stages = [4 << 20, 8 << 20, 16 << 20] if a.quick else [2 << 20, 4 << 20, 8 << 20, 16 << 20, 32 << 20]
     depths = [3, 4] if a.quick else [2, 3, 4, 6]
     threads = [4, 8, 12] if a.quick else [1, 2, 4, 8, 12, 16]
+    if a.stages:
+        stages = [int(x) << 20 for x in a.stages.split(",")]
+    if a.depths:
+        depths = [int(x) for x in a.depths.split(",")]
+    if a.threads:
+        threads = [int(x) for x in a.threads.split(",")]
     for sb, dp, th in itertools.product(stages, depths, threads):
         assert lib.hg_internal_host_stage_config(sb, dp, th, None) == 0
         qH.fill_(float("nan"))
