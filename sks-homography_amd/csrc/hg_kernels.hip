@@ -1011,6 +1011,10 @@ int hg_sum_aten_f32(float* x, int64_t rows, int64_t m, int64_t row_stride, int64
 }  // extern "C"
 
 namespace hg {
+// The fused kernel's shape (hg_internal_rect_sum_config; tools/kbench_rect_sum.py): floats of
+// each parameter's terms per workgroup.
+inline int g_rect_sum_budget = kRectSumBudget;
+
 // level0_only: the fused backward kernel alone (its block sums left in the workspace) -- for
 // the bench's op-over-kernel figure (hg_internal_rect_backward_sum_l0).
 inline int rect_backward_sum(const float* src, const float* tar, const float* grad_H, int64_t B,
@@ -1020,6 +1024,20 @@ inline int rect_backward_sum(const float* src, const float* tar, const float* gr
 }  // namespace hg
 
 extern "C" {
+
+// Library-internal (tools/kbench_rect_sum.py): the fused kernel's unit -- floats of each
+// parameter's terms a workgroup stages (512 ... 4096, a power of two); a value < 0 leaves it.
+// prev[2] receives the settings before (prev[1]: 0, unused).
+int hg_internal_rect_sum_config(int budget, int unused, int* prev) {
+    (void)unused;
+    if (prev) {
+        prev[0] = hg::g_rect_sum_budget;
+        prev[1] = 0;
+    }
+    if (budget >= 0 && (budget < 512 || budget > 4096 || (budget & (budget - 1)))) return hg::kErrInvalid;
+    if (budget >= 0) hg::g_rect_sum_budget = budget;
+    return 0;
+}
 
 // Library-internal (bench.py): rect_backward_sum_l0 alone, as hg_tensor_aca_rect_backward_sum_f32
 // launches it (aligned tensors only).
@@ -1055,29 +1073,32 @@ inline int rect_backward_sum(const float* src, const float* tar, const float* gr
     if (B > (int64_t)1 << 40) return hg::kErrInvalid;
     const int64_t m = 3 * B;
     const hg::AtenSum a = hg::aten_sum_of(workspace, m, m, 1, lanes, threads);
-    const bool aligned = hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(grad_tar) &&
-                         (!grad_src || hg::aligned16(grad_src));
-    if (!aligned) {  // the two-launch form: the same bits
+    bool fused = hg::aligned16(src) && hg::aligned16(tar) && hg::aligned16(grad_H) &&
+                 hg::aligned16(grad_tar) && (!grad_src || hg::aligned16(grad_src));
+    for (int c = 0; c < a.chunks && fused; ++c)
+        fused = hg::AtenRun(a, c).step <= hg::kRectSumMaxStep;
+    if (!fused) {  // the two-launch form: the same bits
         if (level0_only) return hg::kErrInvalid;
         int rc = hg::launch_rect_backward<hg::kAtenCpu, hg::kSdTerms>(
             src, tar, grad_H, B, scale, div, grad_src, grad_tar, workspace, s);
         if (rc) return rc;
         return hg::aten_sum_launch(a, 2, threads, lanes, grad_sd, s, false);
     }
+    const int budget = g_rect_sum_budget;
     int64_t units = 0, lds_floats = 0;
     for (int c = 0; c < a.chunks; ++c) {
         const hg::AtenRun r(a, c);
         if (r.step > hg::kAtenMaxStep) return hg::kErrInvalid;
-        units = std::max(units, hg::rect_sum_units(r));
-        lds_floats = std::max(lds_floats, hg::rect_sum_group(r) * r.step * r.S);
+        units = std::max(units, hg::rect_sum_units(r, budget));
+        lds_floats = std::max(lds_floats, hg::rect_sum_group(r, budget) * r.step * r.S);
     }
     if (units > 0x7fffffffLL) return hg::kErrInvalid;
-    const size_t lds = 2 * (size_t)lds_floats * sizeof(float);  // <= 2 x 8192 floats (step 256)
+    const size_t lds = 2 * (size_t)lds_floats * sizeof(float);  // <= 2 x 4096 floats (step 128)
     const dim3 grid((unsigned)units, (unsigned)a.chunks);
     const bool nt = B * 232 > hg::kMallResidentBytes;
 #define HG_RS(W, NT)                                                                          \
     hg::launch(hg::rect_backward_sum_l0<W, NT>, grid, hg::kRectSumThreads, lds, s, src, tar, \
-               grad_H, scale, div, grad_src, grad_tar, a)
+               grad_H, B, scale, div, grad_src, grad_tar, a, budget)
     const int rc = grad_src ? (nt ? HG_RS(true, true) : HG_RS(true, false))
                             : (nt ? HG_RS(false, true) : HG_RS(false, false));
 #undef HG_RS

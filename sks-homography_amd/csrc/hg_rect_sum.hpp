@@ -20,35 +20,48 @@
 
 namespace hg {
 
-constexpr int kRectSumBudget = 4096;  // floats of each parameter's terms a workgroup stages
-constexpr int kRectSumThreads = 256;
+constexpr int kRectSumBudget = 4096;  // floats of each parameter's terms a workgroup stages (default)
+constexpr int kRectSumThreads = 256;  // kWavesPerBlock waves
+constexpr int64_t kRectSumMaxStep = 128;  // larger level steps (runs of > 2^31 rows): two launches
+// LDS: the four waves' slabs (21 KiB) + 2 x max(budget, step S) floats (32 KiB at 4096 / step 128)
 
 // Level-0 blocks per workgroup for a run, and its workgroups: ceil(nb / G) summing ones plus
 // one for the raw remainder.  The same function on host (grid, LDS) and device.
-__host__ __device__ inline int64_t rect_sum_group(const AtenRun& R) {
+__host__ __device__ inline int64_t rect_sum_group(const AtenRun& R, int budget) {
     const int64_t per = R.step * R.S;
-    return per >= kRectSumBudget ? 1 : kRectSumBudget / per;
+    return per >= budget ? 1 : budget / per;
 }
-__host__ __device__ inline int64_t rect_sum_units(const AtenRun& R) {
-    const int64_t G = rect_sum_group(R);
+__host__ __device__ inline int64_t rect_sum_units(const AtenRun& R, int budget) {
+    const int64_t G = rect_sum_group(R, budget);
     return (R.nb + G - 1) / G + 1;
 }
 
 // Grid (units, chunks): workgroup (u, c) serves run c of both rows of the (2, 3B) scratch
 // a.x (row 0 dL/dscale's terms, row 1 dL/ddiv's; a.es == 1).  Every problem is computed by
 // the workgroups whose float ranges hold one of its three terms and written (dL/dtar, dL/dsrc)
-// by the one holding its first.  16-B aligned src / tar / grad_src / grad_tar (the launcher
-// checks).  The arithmetic is tensor_aca_rect_grad_rows<kAtenCpu>: the terms' bits are those of
+// by the one holding its first.  The waves take tiles of 64 problems from a 4-aligned start as
+// tensor_aca_rect_backward_staged does -- tar and dL/dH slabs by LDS-DMA, dL/dtar and dL/dsrc
+// leaving as contiguous slabs when the workgroup owns the whole tile, per lane at the range's
+// edges -- and each lane puts the terms of its problem that fall in the range into LDS; then
+// task (param, block, stream) sums its block's rows from 0 in order.  16-B aligned src / tar /
+// grad_H / grad_src / grad_tar (the launcher checks).  The arithmetic is
+// tensor_aca_rect_grad_rows<kAtenCpu>: the terms' bits are those of
 // tensor_aca_rect_backward_staged<..., kSdTerms>.
+// Measured at B = 16 M, T = 16 (tools/kbench_rect_sum.py, profiles/r06): a 4096-float budget
+// 713 us for this kernel (2048: 746, 1024: 790; dL/dH per lane instead of by DMA +20 us);
+// a variant with no workgroup-wide LDS -- each wave walking its own unit tile after tile and
+// adding its streams in registers -- 808 us: one wave's tiles in series expose their latency.
 template <bool WANT_SRC, bool NT>
 __global__ __launch_bounds__(kRectSumThreads) void rect_backward_sum_l0(
     const float* __restrict__ src, const float* __restrict__ tar, const float* __restrict__ gH,
-    const float* __restrict__ scale_p, const float* __restrict__ div_p,
-    float* __restrict__ gsrc, float* __restrict__ gtar, AtenSum a) {
+    int64_t B, const float* __restrict__ scale_p, const float* __restrict__ div_p,
+    float* __restrict__ gsrc, float* __restrict__ gtar, AtenSum a, int budget) {
+    constexpr int kTar = kWave * 48, kG = kWave * 36;
+    __shared__ __attribute__((aligned(16))) char slab[kWavesPerBlock][kTar + kG];
     extern __shared__ float terms[];  // [2][F]: this workgroup's terms of each parameter
     const int c = blockIdx.y;
     const AtenRun R(a, c);
-    const int64_t G = rect_sum_group(R);
+    const int64_t G = rect_sum_group(R, budget);
     const int64_t sums = (R.nb + G - 1) / G;
     const int64_t u = blockIdx.x;
     if (u > sums) return;  // workgroup-uniform
@@ -61,50 +74,74 @@ __global__ __launch_bounds__(kRectSumThreads) void rect_backward_sum_l0(
     const int64_t off = (int64_t)c * a.chunk;  // the run's first float in its row
     const int64_t g0 = off + F0, g1 = off + F1;
     const int64_t p0 = g0 / 3, p1 = (g1 + 2) / 3;
+    const int64_t q0 = p0 & ~(int64_t)3;  // tiles start 4-aligned: dL/dH slabs 16-B aligned
     float* const row0 = a.x;
     float* const row1 = a.x + a.row_stride;
     const float scale = scale_p[0], div = div_p[0];
     const float sc[3] = {scale, scale, scale}, dv[3] = {div, div, div};
-    for (int64_t p = p0 + threadIdx.x; p < p1; p += kRectSumThreads) {
-        float tr[12], g[9], gt[12];
-        load_row8<float, NT>(tar + p * 12, *reinterpret_cast<float(*)[8]>(tr));
-        {
-            const u32x4 w = ld16<NT>(reinterpret_cast<const char*>(tar + p * 12 + 8));
-            __builtin_memcpy(tr + 8, &w, 16);
-        }
+    const int lane = threadIdx.x & (kWave - 1);
+    const int wave = threadIdx.x / kWave;
+    char* lds = slab[wave];
+    const int64_t tiles = (p1 - q0 + kWave - 1) / kWave;
+    for (int64_t t = wave; t < tiles; t += kWavesPerBlock) {
+        const int64_t base = q0 + t * kWave;
+        const int64_t p = base + lane;
+        float tr[12], g[9], gt[12], mx, my;
+        const bool full = base + kWave <= B;  // wave-uniform
+        if (full) {
+            mx = NT ? __builtin_nontemporal_load(src + p * 12 + 0) : src[p * 12 + 0];
+            my = NT ? __builtin_nontemporal_load(src + p * 12 + 4) : src[p * 12 + 4];
+            dma_slab_issue<kTar, NT>(reinterpret_cast<const char*>(tar + base * 12), lds, lane);
+            dma_slab_issue<kG, NT>(reinterpret_cast<const char*>(gH + base * 9), lds + kTar, lane);
+            dma_wait_sync();
+            __builtin_memcpy(tr, lds + lane * 48, 48);
 #pragma unroll
-        for (int k = 0; k < 9; ++k) g[k] = NT ? __builtin_nontemporal_load(gH + p * 9 + k) : gH[p * 9 + k];
-        const float mx = NT ? __builtin_nontemporal_load(src + p * 12) : src[p * 12];
-        const float my = NT ? __builtin_nontemporal_load(src + p * 12 + 4) : src[p * 12 + 4];
+            for (int k = 0; k < 9; ++k) g[k] = reinterpret_cast<const float*>(lds + kTar)[lane * 9 + k];
+        } else {
+            const int64_t q = p < B ? p : B - 1;  // lanes past the batch compute a copy, write nothing
+#pragma unroll
+            for (int k = 0; k < 12; ++k) tr[k] = tar[q * 12 + k];
+#pragma unroll
+            for (int k = 0; k < 9; ++k) g[k] = gH[q * 9 + k];
+            mx = src[q * 12 + 0];
+            my = src[q * 12 + 4];
+        }
         float gmx, gmy, gs, gd, gsr[3], gdr[3];
         tensor_aca_rect_grad_rows<kAtenCpu>(tr, mx, my, sc, dv, g, gt, gmx, gmy, gs, gd, gsr, gdr);
-        if (3 * p >= g0) {  // this workgroup holds the problem's first term: its gradients
-#pragma unroll
-            for (int q = 0; q < 3; ++q) {
-                u32x4 w;
-                __builtin_memcpy(&w, gt + 4 * q, 16);
-                st16<NT>(reinterpret_cast<char*>(gtar + p * 12 + 4 * q), w);
-            }
-            if constexpr (WANT_SRC) {
-                const float z[12] = {gmx, 0.f, 0.f, 0.f, gmy, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        const float gsv[12] = {gmx, 0.f, 0.f, 0.f, gmy, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        // the whole tile is this workgroup's: first terms 3 base ... 3 (base + 63) in range
+        if (full && 3 * base >= g0 && 3 * (base + kWave - 1) < g1) {
+            wave_lds_sync();  // the staging below reuses the input bytes
+            store_rows_staged<12, NT>(reinterpret_cast<char*>(gtar + base * 12), gt, lds, lane);
+            if constexpr (WANT_SRC)
+                store_rows_staged<12, NT>(reinterpret_cast<char*>(gsrc + base * 12), gsv, lds, lane);
+        } else {
+            if (p < B && 3 * p >= g0 && 3 * p < g1) {
 #pragma unroll
                 for (int q = 0; q < 3; ++q) {
                     u32x4 w;
-                    __builtin_memcpy(&w, z + 4 * q, 16);
-                    st16<NT>(reinterpret_cast<char*>(gsrc + p * 12 + 4 * q), w);
+                    __builtin_memcpy(&w, gt + 4 * q, 16);
+                    st16<NT>(reinterpret_cast<char*>(gtar + p * 12 + 4 * q), w);
+                    if constexpr (WANT_SRC) {
+                        __builtin_memcpy(&w, gsv + 4 * q, 16);
+                        st16<NT>(reinterpret_cast<char*>(gsrc + p * 12 + 4 * q), w);
+                    }
                 }
             }
+            wave_lds_sync();  // this tile's slab reads are done before the next tile's DMA
         }
+        if (p < B) {
 #pragma unroll
-        for (int r = 0; r < 3; ++r) {
-            const int64_t e = 3 * p + r;
-            if (e < g0 || e >= g1) continue;
-            if (raw) {  // the cascade adds these one by one: the scratch holds them as they are
-                row0[e] = gsr[r];
-                row1[e] = gdr[r];
-            } else {
-                terms[e - g0] = gsr[r];
-                terms[F + (e - g0)] = gdr[r];
+            for (int r = 0; r < 3; ++r) {
+                const int64_t e = 3 * p + r;
+                if (e < g0 || e >= g1) continue;
+                if (raw) {  // the cascade adds these one by one: the scratch holds them as they are
+                    row0[e] = gsr[r];
+                    row1[e] = gdr[r];
+                } else {
+                    terms[e - g0] = gsr[r];
+                    terms[F + (e - g0)] = gdr[r];
+                }
             }
         }
     }
