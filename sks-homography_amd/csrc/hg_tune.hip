@@ -819,6 +819,11 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 25: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 1>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 26: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 2>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 27: return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // round 6: the packed-pair shape in 16-wave blocks, plain and with
+        // the sc1 buffer stores (per-row resources in SGPRs), beside 22-27
+        case 28: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 29: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 2>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 30: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

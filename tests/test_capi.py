@@ -405,6 +405,39 @@ def test_pmc_families_name_built_kernels_and_match_their_code():
     stale = {k: (rec["detail"][k].get("code"), now[k]) for k in pt.KEYS
              if rec["detail"][k].get("code") != now[k]}
     assert not stale, f"kernel code changed since the PMC run: {stale}"
+    # bench.py matches a record by the prefix stored IN it (a record whose
+    # stored prefix no longer named the kernel printed `traffic_bytes: null` on the box)
+    moved = {k: (rec["detail"][k].get("prefix"), prefix) for k, (prefix, _) in pt.KEYS.items()
+             if rec["detail"][k].get("prefix") != prefix}
+    assert not moved, f"recorded prefixes differ from tools/pmc_traffic.py's: {moved}"
+
+
+def test_every_quoted_pmc_figure_is_current():
+    """Every family bench.py quotes a `traffic` for (pmc_detail / pmc_traffic) has a record in
+    profiles/pmc_traffic.json whose machine code is the built library's: pmc_detail, run here
+    on the CPU, returns a figure for each -- never `traffic_bytes: null`."""
+    import json
+    import re
+    import bench
+    sys.path.insert(0, os.path.join(ROOT, "sks-homography_amd"))
+    try:
+        import build_lib as bl
+    finally:
+        sys.path.pop(0)
+    with open(bench.PMC_TRAFFIC) as f:
+        measured_with = json.load(f).get("provenance", {}).get("compiler")
+    if measured_with and measured_with != bl.compiler_id():
+        pytest.skip(f"PMC figures measured with another compiler ({measured_with})")
+    with open(os.path.join(ROOT, "bench.py")) as f:
+        text = f.read()
+    keys = sorted(set(re.findall(r'pmc_detail\(\s*"([a-z0-9_]+)"', text)))
+    assert len(keys) >= 10, keys
+    bench._FAMILY_CODE.clear()
+    missing = {k: bench.pmc_detail(k).get("reason") for k in keys
+               if bench.pmc_detail(k).get("traffic_bytes") is None}
+    assert not missing, missing
+    for k in ("aca_f32_aos_norm", "sks_f32_aos_norm"):  # the headline's roofline.traffic
+        assert bench.pmc_traffic(k) is not None, k
 
 
 def test_kernel_code_digest_reads_the_headline_entry_points(pkg):

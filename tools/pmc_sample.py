@@ -28,6 +28,20 @@ def run():
         for _ in range(3):
             pkg.sample_solve_seeded(ps, pt, N, 11, 0, algo=algo)
         torch.cuda.synchronize()
+    # SAMPLE_VARIANTS="26,28,29": seeded tune shapes (hg_tune_sample_seeded), ACA, 3 launches each
+    variants = [int(v) for v in os.environ.get("SAMPLE_VARIANTS", "").split(",") if v]
+    if variants:
+        import ctypes
+        fs = pkg._lib.tune().hg_tune_sample_seeded
+        fs.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                       ctypes.c_uint64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_int,
+                       ctypes.c_void_p]
+        H = torch.empty((N, 9), device=dev)
+        st = torch.cuda.current_stream(dev).cuda_stream
+        for v in variants:
+            for _ in range(3):
+                assert fs(v, ps.data_ptr(), pt.data_ptr(), ps.shape[0], 11, 0, H.data_ptr(), N, 0, 1, st) == 0
+            torch.cuda.synchronize()
     print("pmc_sample done")
 
 
@@ -51,7 +65,9 @@ def reduce(path):
             "lds_wave_instr_per_128_hypotheses": round(med["SQ_INSTS_LDS"] / (N / 128), 1),
             "valu_busy_quadcycles_per_simd": round(quad),
             "busy_cycles_per_cu": round(busy),
-            "valu_busy_frac_if_4_cycles_per_wave64_instr": round(4 * quad / busy, 3)}}
+            "valu_busy_frac_if_4_cycles_per_wave64_instr": round(4 * quad / busy, 3),
+            **({"waves_per_simd": round(4 * med["SQ_WAVE_CYCLES"] / (CUS * 4) / busy, 2)}
+               if "SQ_WAVE_CYCLES" in med else {})}}
     print(json.dumps({k[:80]: v["derived"] for k, v in out.items()}, indent=1))
     return out
 
