@@ -241,14 +241,18 @@ Registry& registry() {
 constexpr size_t kSmallStageBytes = 128 << 10;
 constexpr int kDevSlots = 64;
 
-// Ring shape: 32 MiB stages, 6 deep (192 MiB of pinned memory while a large call runs).  At 10 M
-// f32 AoS from pageable memory, 8 copy threads (tools/ring_probe.py, profiles/r06/ring_*.json):
-// 8 MiB x 4 18.8 ms, 16 x 6 17.2, 32 x 6 16.1, 64 x 6 14.6 -- larger stages keep more of the
-// PCIe link busy per kernel but hold more pinned memory and lengthen the ring's fill and drain.
+// Ring shape: 12 MiB stages, 6 deep (72 MiB of pinned memory and 72 MiB of device buffers while
+// a large call runs), 8 copy threads.  At 10 M f32 AoS from pageable memory (tools/ring_probe.py,
+// profiles/r06/ring_*.json), chunks through device buffers by the copy engines: 4 MiB x 6 16.2-16.4
+// ms, 8 x 6 14.0-16.3, 12 x 6 14.1-14.5, 32 x 6 15.8, 64 x 6 16.1; with the kernel reading the
+// stage itself instead: 8 x 4 18.8, 32 x 6 16.1, 64 x 6 14.6 (the pinned zero-copy call: 12.0).
 struct StageConfig {
-    std::atomic<int64_t> ring_bytes{32 << 20};  // one ring stage
+    std::atomic<int64_t> ring_bytes{12 << 20};  // one ring stage
     std::atomic<int> depth{6};                  // ring stages (and streams) a call cycles through
     std::atomic<int> coherent{1};              // stage memory fine-grained (1) or not (0)
+    std::atomic<int> probe{0};  // tools only, wrong results: 1 no host copies, 2 no kernels
+    std::atomic<int> dma{1};    // ring chunks through device buffers by the copy engines (1) or
+                                // read / written in the stage by the kernel over PCIe (0)
 };
 
 StageConfig& stage_config() {
@@ -428,6 +432,44 @@ StreamPool& stream_pool() {
     return *p;
 }
 
+// Device buffers of the ring's DMA form, per device and size: made on first need, never freed
+// (device memory, HBM: a few stages' worth per concurrent call), handed to one call at a time.
+struct DevPool {
+    struct Buf {
+        int dev;
+        size_t bytes;
+        char* p;
+    };
+    std::mutex mu;
+    std::vector<Buf> idle;
+
+    int take(int dev, size_t bytes, char*& out) {
+        {
+            std::lock_guard<std::mutex> lock(mu);
+            for (size_t i = idle.size(); i-- > 0;) {
+                if (idle[i].dev != dev || idle[i].bytes != bytes) continue;
+                out = idle[i].p;
+                idle.erase(idle.begin() + (long)i);
+                return 0;
+            }
+        }
+        void* p = nullptr;
+        const hipError_t e = hipMalloc(&p, bytes);
+        if (e != hipSuccess) return (int)e;
+        out = static_cast<char*>(p);
+        return 0;
+    }
+    void give_back(int dev, size_t bytes, char* p) {
+        std::lock_guard<std::mutex> lock(mu);
+        idle.push_back({dev, bytes, p});
+    }
+};
+
+DevPool& dev_pool() {
+    static DevPool* p = new DevPool();  // never destroyed
+    return *p;
+}
+
 // The staged solve of a batch with at least one pageable buffer (v[i].dev == nullptr).  `s` is
 // the caller's stream: device-memory buffers are ordered after the work queued on it.
 template <typename T>
@@ -456,19 +498,28 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
     const int D = (int)std::min<int64_t>(K, std::max(1, stage_config().depth.load()));
     // one chunk: the caller's stream; several: a ring stream per stage
     const bool ring = K > 1;
+    // Past the small stage the chunks go through device buffers: the copy engines move each
+    // stage in and its H out (both PCIe directions at their DMA rate, consecutive chunks' copies
+    // overlapping on the ring's streams) and the kernel runs from HBM.  A chunk kernel reading
+    // the stage over PCIe itself runs one round of waves, its reads and writes barely
+    // overlapping: 15 ms of kernels alone at 10 M against 12 ms for one zero-copy kernel over
+    // pinned memory (tools/ring_probe.py `parts`, profiles/r06).
+    const bool dma = !small && stage_config().dma.load() != 0;
     std::vector<Stage*> st((size_t)D, nullptr);
     std::vector<char*> sd((size_t)D, nullptr);
+    std::vector<char*> db((size_t)D, nullptr);  // device buffers (dma)
     std::vector<hipStream_t> ss((size_t)D, s);
     std::vector<bool> own((size_t)D, false);
     std::vector<hipEvent_t> ev;
     int rc = 0, dev = 0;
     const int coherent = stage_config().coherent.load();
+    rc = (int)hipGetDevice(&dev);
     for (int j = 0; j < D && !rc; ++j) {
         rc = stage_pool().take(cap, coherent, st[(size_t)j]);
         if (!rc) rc = stage_dev(st[(size_t)j], sd[(size_t)j]);
+        if (!rc && dma) rc = dev_pool().take(dev, cap, db[(size_t)j]);
     }
     if (!rc && ring) {
-        rc = (int)hipGetDevice(&dev);
         for (int j = 0; j < D && !rc; ++j) {
             rc = stream_pool().take(dev, ss[(size_t)j]);
             own[(size_t)j] = rc == 0;
@@ -499,7 +550,9 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
     };
     const size_t E = sizeof(T);
     StageStats& stats = stage_stats();
+    const int probe = stage_config().probe.load();
     auto run_pieces = [&]() {
+        if (probe & 1) return;
         const int64_t t0 = now_ns();
         pool.run(pieces);
         stats.copy_ns += now_ns() - t0;
@@ -544,27 +597,40 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
         run_pieces();
         const int64_t lo = p.lo(k), c = p.count(k);
         char* ptr[3];
+        bool host_ptr = !dma;  // a kernel pointer into host memory: the host cache policy
+        char* const buf = dma ? db[(size_t)j] : sd[(size_t)j];  // where the staged regions live
         for (int i = 0; i < 3; ++i) {
-            if (p.mode[i] == host::kDirect)  // AoS (or a one-chunk SoA batch): in place
+            if (p.mode[i] == host::kDirect) {  // AoS (or a one-chunk SoA batch): in place
                 ptr[i] = static_cast<char*>(v[i].dev) + (size_t)lo * p.per_problem(i);
-            else
-                ptr[i] = sd[(size_t)j] + p.off[i];
+                host_ptr = host_ptr || v[i].in_host;
+            } else {
+                ptr[i] = buf + p.off[i];
+            }
         }
-        for (int i = 0; i < 2 && !rc; ++i)  // device-memory SoA rows into the stage
-            if (p.mode[i] == host::kDma)
-                rc = (int)hipMemcpy2DAsync(st[(size_t)j]->host + p.off[i], (size_t)c * E,
+        for (int i = 0; i < 2 && !rc; ++i) {
+            const size_t bytes = (size_t)c * p.per_problem(i);  // the region, rows c wide in SoA
+            if (p.mode[i] == host::kCpu && dma)  // the stage's region to the device buffer
+                rc = (int)hipMemcpyAsync(buf + p.off[i], st[(size_t)j]->host + p.off[i], bytes,
+                                         hipMemcpyHostToDevice, q);
+            else if (p.mode[i] == host::kDma)  // device-memory SoA rows, cut to the chunk
+                rc = (int)hipMemcpy2DAsync(dma ? buf + p.off[i] : st[(size_t)j]->host + p.off[i],
+                                           (size_t)c * E,
                                            static_cast<const char*>(v[i].dev) + (size_t)lo * E,
                                            (size_t)n * E, (size_t)c * E, (size_t)p.rows[i],
-                                           hipMemcpyDeviceToHost, q);
-        if (!rc)
+                                           dma ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, q);
+        }
+        if (!rc && !(probe & 2))
             rc = launch<T>(algo, reinterpret_cast<const T*>(ptr[0]),
                            reinterpret_cast<const T*>(ptr[1]), reinterpret_cast<T*>(ptr[2]), c,
-                           layout, flags, q, true);
+                           layout, flags, q, host_ptr);
+        if (!rc && p.mode[2] == host::kCpu && dma)  // H to the stage
+            rc = (int)hipMemcpyAsync(st[(size_t)j]->host + p.off[2], buf + p.off[2],
+                                     (size_t)c * p.per_problem(2), hipMemcpyDeviceToHost, q);
         if (!rc && p.mode[2] == host::kDma)
             rc = (int)hipMemcpy2DAsync(static_cast<char*>(v[2].dev) + (size_t)lo * E,
-                                       (size_t)n * E, st[(size_t)j]->host + p.off[2],
+                                       (size_t)n * E, dma ? buf + p.off[2] : st[(size_t)j]->host + p.off[2],
                                        (size_t)c * E, (size_t)c * E, (size_t)p.rows[2],
-                                       hipMemcpyHostToDevice, q);
+                                       dma ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, q);
         if (!rc && ring) rc = (int)hipEventRecord(ev[(size_t)j], q);
         ++stats.chunks;
     }
@@ -594,8 +660,10 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
         if (x) (void)hipEventDestroy(x);
     // a stream that did not drain may still have a kernel reading or writing a stage: neither
     // is handed to another call
-    for (int j = 0; j < D; ++j)
+    for (int j = 0; j < D; ++j) {
         if (own[(size_t)j] && e == hipSuccess) stream_pool().give_back(dev, ss[(size_t)j]);
+        if (db[(size_t)j] && e == hipSuccess) dev_pool().give_back(dev, cap, db[(size_t)j]);
+    }
     for (Stage* x : st) {
         if (!x) continue;
         if (e == hipSuccess) stage_pool().give_back(x);
@@ -721,6 +789,24 @@ int hg_internal_host_stage_coherent(int coherent) {
     StageConfig& c = stage_config();
     const int prev = c.coherent.load();
     if (coherent == 0 || coherent == 1) c.coherent = coherent;
+    return prev;
+}
+
+// Library-internal (tools/ring_probe.py, timing only -- results are WRONG while set): 1 skips
+// the ring's host copies, 2 its kernels, 0 restores.  Returns the previous setting.
+int hg_internal_host_stage_probe(int probe) {
+    StageConfig& c = stage_config();
+    const int prev = c.probe.load();
+    if (probe >= 0 && probe <= 3) c.probe = probe;
+    return prev;
+}
+
+// Library-internal (tools/ring_probe.py): the ring's chunks through device buffers by the copy
+// engines (1, the default) or read and written in the stage by the kernel (0); -1 queries.
+int hg_internal_host_stage_dma(int dma) {
+    StageConfig& c = stage_config();
+    const int prev = c.dma.load();
+    if (dma == 0 || dma == 1) c.dma = dma;
     return prev;
 }
 

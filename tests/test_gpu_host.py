@@ -452,3 +452,19 @@ def test_shared_host_batch_solve_block(pkg, dev):
         b.rank = 0
         b.close()
     assert not os.path.exists(f"/dev/shm/sks_hg_gpu_test_{os.getpid()}")
+
+
+def test_staged_calls_alternate_devices(pkg, dev, small_ring):
+    """the stage pool is shared by every device of the process -- stages are
+    portable pinned memory, their device address looked up per device, ring streams pooled per
+    device.  Small (one stage) and ring (many chunks) calls alternate between cuda:0 and cuda:1,
+    every result bit-exact.  Needs two GPUs (skipped on the one-GPU boxes)."""
+    if torch.cuda.device_count() < 2:
+        pytest.skip("one GPU: the cross-device stage reuse needs two")
+    for n in (500, 70001):
+        ds, dt = _inputs(pkg, dev, n, torch.float32, "aos", off=n)
+        want = pkg.solve("aca", ds, dt).cpu()
+        hs, ht = ds.cpu(), dt.cpu()
+        for d in (0, 1, 0, 1):
+            got = pkg.solve_host("aca", hs, ht, device=d)
+            assert torch.equal(_bits(got), _bits(want)), (n, d)

@@ -43,6 +43,7 @@ def main():
     ap.add_argument("--stages", default="", help="MiB list, e.g. 16,32,64")
     ap.add_argument("--depths", default="")
     ap.add_argument("--threads", default="")
+    ap.add_argument("--dma", type=int, default=-1, help="1 device buffers by copy engines, 0 kernel reads the stage")
     a = ap.parse_args()
     import bench  # the bench's own NUMA binding, before anything touches the GPU
     numa = bench.bind_numa(0) if not a.no_numa else None
@@ -56,6 +57,8 @@ def main():
         lib.hg_internal_host_stage_stats(st)
         return list(st)
     lib.hg_internal_host_stage_config.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, p64]
+    if a.dma in (0, 1):
+        lib.hg_internal_host_stage_dma(a.dma)
     dev = torch.device("cuda:0")
     n = a.n
     ds = pkg.fill_uniform(n * 8, 11, 0, device=dev).view(n, 8)
@@ -67,7 +70,8 @@ def main():
     h2d_s, h2d_t = torch.empty_like(ds), torch.empty_like(dt)
     prev = (ctypes.c_int64 * 3)()
     lib.hg_internal_host_stage_config(0, 0, 0, prev)
-    out = {"n": n, "default": list(prev), "cpus": len(os.sched_getaffinity(0)), "numa": numa}
+    out = {"n": n, "default": list(prev), "cpus": len(os.sched_getaffinity(0)), "numa": numa,
+           "dma": lib.hg_internal_host_stage_dma(-1)}
 
     def h2d():
         h2d_s.copy_(ps, non_blocking=True)
@@ -99,6 +103,20 @@ def main():
                       "wait_ms_per_call": round((s1[6] - s0[6]) / calls / 1e6, 3),
                       "copy_GBps": round((s1[7] - s0[7]) / max(1, s1[5] - s0[5]), 1)})
         print(json.dumps(sweep[-1]), flush=True)
+    # the ring's two halves apart (timing only, wrong results): kernels without the host copies,
+    # host copies without the kernels, at each stage size of the sweep with 8 threads
+    parts = []
+    for sb in stages:
+        for dp in depths:
+            assert lib.hg_internal_host_stage_config(sb, dp, 8, None) == 0
+            rec = {"stage_MiB": sb >> 20, "depth": dp}
+            for probe, name in ((1, "kernels_only_ms"), (2, "copies_only_ms")):
+                lib.hg_internal_host_stage_probe(probe)
+                rec[name] = round(best_ms(lambda: pkg.solve_host("aca", qs, qt, out=qH), reps=3), 3)
+                lib.hg_internal_host_stage_probe(0)
+            parts.append(rec)
+            print(json.dumps(rec), flush=True)
+    out["parts"] = parts
     lib.hg_internal_host_stage_config(prev[0], prev[1], prev[2], None)
     qH.fill_(float("nan"))
     out["default_staged_ms"] = round(best_ms(lambda: pkg.solve_host("aca", qs, qt, out=qH)), 3)
