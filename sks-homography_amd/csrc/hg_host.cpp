@@ -504,7 +504,7 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
     // the stage over PCIe itself runs one round of waves, its reads and writes barely
     // overlapping: 15 ms of kernels alone at 10 M against 12 ms for one zero-copy kernel over
     // pinned memory (tools/ring_probe.py `parts`, profiles/r06).
-    const bool dma = !small && stage_config().dma.load() != 0;
+    bool dma = !small && stage_config().dma.load() != 0;
     std::vector<Stage*> st((size_t)D, nullptr);
     std::vector<char*> sd((size_t)D, nullptr);
     std::vector<char*> db((size_t)D, nullptr);  // device buffers (dma)
@@ -517,7 +517,14 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
     for (int j = 0; j < D && !rc; ++j) {
         rc = stage_pool().take(cap, coherent, st[(size_t)j]);
         if (!rc) rc = stage_dev(st[(size_t)j], sd[(size_t)j]);
-        if (!rc && dma) rc = dev_pool().take(dev, cap, db[(size_t)j]);
+        if (!rc && dma && dev_pool().take(dev, cap, db[(size_t)j]) != 0) {
+            // device memory short (another allocation holds the card): this call's kernels read
+            // the stages over PCIe instead -- slower, same bits
+            (void)hipGetLastError();
+            for (int i = 0; i < j; ++i) dev_pool().give_back(dev, cap, db[(size_t)i]);
+            std::fill(db.begin(), db.end(), nullptr);
+            dma = false;
+        }
     }
     if (!rc && ring) {
         for (int j = 0; j < D && !rc; ++j) {
