@@ -468,3 +468,36 @@ def test_staged_calls_alternate_devices(pkg, dev, small_ring):
         for d in (0, 1, 0, 1):
             got = pkg.solve_host("aca", hs, ht, device=d)
             assert torch.equal(_bits(got), _bits(want)), (n, d)
+
+
+def test_staged_rings_from_threads(pkg, dev, small_ring):
+    """Four threads, each running many-chunk rings at once (64 KiB stages, 3 deep: every call
+    takes 3 stages, 3 device buffers and 3 ring streams from the shared pools), AoS and SoA,
+    f32 and f64, 6 calls each: every H bit-exact, no stage withheld, no registration made."""
+    lib = small_ring
+    stats = (ctypes.c_int64 * 4)()
+    assert lib.hg_internal_host_registry_stats(stats) == 0
+    made = stats[1]
+    jobs = []
+    for k, (dtype, layout) in enumerate([(torch.float32, "aos"), (torch.float64, "soa"),
+                                         (torch.float64, "aos"), (torch.float32, "soa")]):
+        n = 30011 + 977 * k
+        ds, dt = _inputs(pkg, dev, n, dtype, layout, off=17 * k)
+        jobs.append((ds.cpu(), dt.cpu(), layout, pkg.solve("sks", ds, dt, layout=layout).cpu()))
+    bad = []
+
+    def work(k):
+        s, t, layout, want = jobs[k]
+        for _ in range(6):
+            got = pkg.solve_host("sks", s, t, layout=layout)
+            if not torch.equal(_bits(got), _bits(want)):
+                bad.append(k)
+
+    th = [threading.Thread(target=work, args=(k,)) for k in range(len(jobs))]
+    for x in th:
+        x.start()
+    for x in th:
+        x.join()
+    assert not bad, bad
+    assert _stage_stats(lib)[3] == 0
+    assert lib.hg_internal_host_registry_stats(stats) == 0 and stats[1] == made
