@@ -241,18 +241,21 @@ Registry& registry() {
 constexpr size_t kSmallStageBytes = 128 << 10;
 constexpr int kDevSlots = 64;
 
-// Ring shape: 12 MiB stages, 6 deep (72 MiB of pinned memory and 72 MiB of device buffers while
-// a large call runs), 8 copy threads.  At 10 M f32 AoS from pageable memory (tools/ring_probe.py,
-// profiles/r06/ring_*.json), chunks through device buffers by the copy engines: 4 MiB x 6 16.2-16.4
-// ms, 8 x 6 14.0-16.3, 12 x 6 14.1-14.5, 32 x 6 15.8, 64 x 6 16.1; with the kernel reading the
-// stage itself instead: 8 x 4 18.8, 32 x 6 16.1, 64 x 6 14.6 (the pinned zero-copy call: 12.0).
+// Ring shape: 8 MiB stages, 6 deep (48 MiB of pinned memory and 48 MiB of device buffers while a
+// large call runs), 8 copy threads, the copy engines moving each stage in and the kernel writing
+// H straight into the stage.  At 10 M f32 AoS from pageable memory (tools/ring_probe.py,
+// profiles/r06/ring_*.json): 8 MiB x 4 / x 6 13.1 ms, 12 x 6 13.3, 16 x 6 13.6, 32 x 4 13.0 (the GPU
+// side alone 11.6-12.5: the host copies are what is left); with H brought back by the copy
+// engines too (mode 1) 14.2-14.5 -- one engine's queue serialises the two directions; with the
+// kernel reading the stage itself (mode 0) 16.1 at 32 x 6 (the pinned zero-copy call: 12.0).
 struct StageConfig {
-    std::atomic<int64_t> ring_bytes{12 << 20};  // one ring stage
+    std::atomic<int64_t> ring_bytes{8 << 20};  // one ring stage
     std::atomic<int> depth{6};                  // ring stages (and streams) a call cycles through
     std::atomic<int> coherent{1};              // stage memory fine-grained (1) or not (0)
     std::atomic<int> probe{0};  // tools only, wrong results: 1 no host copies, 2 no kernels
-    std::atomic<int> dma{1};    // ring chunks through device buffers by the copy engines (1) or
-                                // read / written in the stage by the kernel over PCIe (0)
+    std::atomic<int> dma{2};    // ring chunks: in by the copy engines, H by the kernel into the
+                                // stage (2); both ways by the copy engines (1); read and written
+                                // in the stage by the kernel over PCIe (0)
 };
 
 StageConfig& stage_config() {
@@ -498,13 +501,16 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
     const int D = (int)std::min<int64_t>(K, std::max(1, stage_config().depth.load()));
     // one chunk: the caller's stream; several: a ring stream per stage
     const bool ring = K > 1;
-    // Past the small stage the chunks go through device buffers: the copy engines move each
-    // stage in and its H out (both PCIe directions at their DMA rate, consecutive chunks' copies
-    // overlapping on the ring's streams) and the kernel runs from HBM.  A chunk kernel reading
-    // the stage over PCIe itself runs one round of waves, its reads and writes barely
-    // overlapping: 15 ms of kernels alone at 10 M against 12 ms for one zero-copy kernel over
-    // pinned memory (tools/ring_probe.py `parts`, profiles/r06).
+    // Past the small stage the copy engines move each stage's src / tar to a device buffer and
+    // the kernel reads them from HBM, writing H straight into the stage over PCIe (posted
+    // writes): the link's two directions are driven by different agents.  A chunk kernel that
+    // also reads the stage over PCIe runs one round of waves whose reads barely overlap (15 ms
+    // of kernels alone at 10 M against 12 ms for one zero-copy kernel over pinned memory), and
+    // H brought back by the copy engines too shares their queue with the inputs (13.6 ms of GPU
+    // side alone); this form's GPU side takes 11.6-12.5 ms (tools/ring_probe.py `parts`,
+    // profiles/r06).
     bool dma = !small && stage_config().dma.load() != 0;
+    const bool h_by_kernel = stage_config().dma.load() == 2;
     std::vector<Stage*> st((size_t)D, nullptr);
     std::vector<char*> sd((size_t)D, nullptr);
     std::vector<char*> db((size_t)D, nullptr);  // device buffers (dma)
@@ -614,6 +620,11 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
                 ptr[i] = buf + p.off[i];
             }
         }
+        const bool h_direct = dma && h_by_kernel && p.mode[2] == host::kCpu;
+        if (h_direct) {  // H into the stage by the kernel itself
+            ptr[2] = sd[(size_t)j] + p.off[2];
+            host_ptr = true;
+        }
         for (int i = 0; i < 2 && !rc; ++i) {
             const size_t bytes = (size_t)c * p.per_problem(i);  // the region, rows c wide in SoA
             if (p.mode[i] == host::kCpu && dma)  // the stage's region to the device buffer
@@ -630,7 +641,7 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
             rc = launch<T>(algo, reinterpret_cast<const T*>(ptr[0]),
                            reinterpret_cast<const T*>(ptr[1]), reinterpret_cast<T*>(ptr[2]), c,
                            layout, flags, q, host_ptr);
-        if (!rc && p.mode[2] == host::kCpu && dma)  // H to the stage
+        if (!rc && p.mode[2] == host::kCpu && dma && !h_direct)  // H to the stage
             rc = (int)hipMemcpyAsync(st[(size_t)j]->host + p.off[2], buf + p.off[2],
                                      (size_t)c * p.per_problem(2), hipMemcpyDeviceToHost, q);
         if (!rc && p.mode[2] == host::kDma)
@@ -808,12 +819,13 @@ int hg_internal_host_stage_probe(int probe) {
     return prev;
 }
 
-// Library-internal (tools/ring_probe.py): the ring's chunks through device buffers by the copy
-// engines (1, the default) or read and written in the stage by the kernel (0); -1 queries.
+// Library-internal (tools/ring_probe.py): the ring's chunks in by the copy engines and H written
+// into the stage by the kernel (2, the default), both ways by the copy engines (1), or read and
+// written in the stage by the kernel (0); -1 queries.
 int hg_internal_host_stage_dma(int dma) {
     StageConfig& c = stage_config();
     const int prev = c.dma.load();
-    if (dma == 0 || dma == 1) c.dma = dma;
+    if (dma >= 0 && dma <= 2) c.dma = dma;
     return prev;
 }
 

@@ -43,7 +43,8 @@ def main():
     ap.add_argument("--stages", default="", help="MiB list, e.g. 16,32,64")
     ap.add_argument("--depths", default="")
     ap.add_argument("--threads", default="")
-    ap.add_argument("--dma", type=int, default=-1, help="1 device buffers by copy engines, 0 kernel reads the stage")
+    ap.add_argument("--dma", type=int, default=-1,
+                    help="1 device buffers by copy engines, 2 in by copy engines / H by the kernel, 0 kernel reads the stage")
     a = ap.parse_args()
     import bench  # the bench's own NUMA binding, before anything touches the GPU
     numa = bench.bind_numa(0) if not a.no_numa else None
@@ -57,7 +58,7 @@ def main():
         lib.hg_internal_host_stage_stats(st)
         return list(st)
     lib.hg_internal_host_stage_config.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int, p64]
-    if a.dma in (0, 1):
+    if a.dma in (0, 1, 2):
         lib.hg_internal_host_stage_dma(a.dma)
     dev = torch.device("cuda:0")
     n = a.n
