@@ -3,7 +3,7 @@
 For batch sizes n = 1 ... 10 M of host-resident AoS f32 problems (the reference's own data
 placement: std::vector / numpy, pageable), times
   * gpu_batch_pageable -- sks::runKernel_ACA_batch on the host arrays (hg_solve_host_f32:
-    registered for the call, the kernel reads and writes host memory over PCIe),
+    since 0.3 copied through the library's pinned stages; up to 0.2 registered for the call),
   * gpu_batch_pinned   -- the same on pinned arrays (no registration),
   * gpu_single_loop    -- n calls of the single-problem sks::runKernel_ACA (n <= 10 K),
   * cpu_1core / cpu_cores -- the reference's own ACA_SKS.cpp (oracle/_ref) over the same
