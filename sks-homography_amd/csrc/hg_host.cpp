@@ -9,6 +9,7 @@
 // GPU after hipHostUnregister, which is how heap pages reach a later HIP copy
 // in the state the round-4/5 faults came from.
 #include <hip/hip_runtime_api.h>
+#include <emmintrin.h>
 #include <sched.h>
 
 #include <algorithm>
@@ -473,6 +474,22 @@ DevPool& dev_pool() {
     return *p;
 }
 
+// Waits for `ev` by polling: hipEventSynchronize may put the thread to sleep, and each wake-up
+// cost the ring ~0.5 ms a chunk at 1 M problems (8.7 ms a call against 1.6 ms polled;
+// tools/crossover.py, profiles/r06).  After 50 ms of polling the wait blocks in HIP instead, so
+// a long kernel does not keep a core busy.  (Stream drains keep hipStreamSynchronize: polling
+// hipStreamQuery made the one-chunk calls 4-5 us slower.)
+int wait_poll(hipEvent_t ev) {
+    const int64_t t0 = now_ns();
+    for (;;) {
+        const hipError_t q = hipEventQuery(ev);
+        if (q != hipErrorNotReady) return (int)q;
+        if (now_ns() - t0 > 50000000) break;
+        _mm_pause();
+    }
+    return (int)hipEventSynchronize(ev);
+}
+
 // The staged solve of a batch with at least one pageable buffer (v[i].dev == nullptr).  `s` is
 // the caller's stream: device-memory buffers are ordered after the work queued on it.
 template <typename T>
@@ -582,7 +599,7 @@ int solve_staged(int algo, View (&v)[3], int64_t n, int layout, int flags, hipSt
             if (ring) {
                 if (wait_first) {
                     const int64_t t0 = now_ns();
-                    const int e = (int)hipEventSynchronize(ev[(size_t)j]);
+                    const int e = wait_poll(ev[(size_t)j]);
                     stats.wait_ns += now_ns() - t0;
                     if (e) return e;
                     wait_first = false;
