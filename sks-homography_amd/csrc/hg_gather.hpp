@@ -223,7 +223,8 @@ constexpr size_t mrg_words_lds() { return (size_t)2 * 4 * Q * (KB / 4) * 4; }
 constexpr int kMrgGroupBatch = 8;  // groups whose engine bases one pass makes
 constexpr size_t kMrgStaticLds = 2 * kMrgGroupBatch * 24 * 4;
 
-// Ablations for the tune library only (wrong bits, timing only): the shipped kernel is ABL 0.
+// Ablations (tune library only: wrong bits, timing only) and shape flags (same bits).  The
+// shipped kernel is kMrgStBuf | kMrgIdxF64 (kMrgIdxF64 alone when 8 n >= 2^32; hg_table8.hip).
 enum MrgAblation : int {
     kMrgAblNone = 0,
     kMrgAblNoSolve = 1,   // draws + gather, H = a cheap function of the gathered points
@@ -238,6 +239,9 @@ enum MrgAblation : int {
                           // its solves, in one basic block (the chunk loop unrolled by the three
                           // engine phases, the draws unconditional): the scheduler may overlap the
                           // independent draw and solve chains (same bits)
+    kMrgIdxF64 = 256,     // the engines write pool indices, not words: mrg::step_index, the
+                          // remainder in binary64 from the word's own binary64 value (same bits;
+                          // `magic` carries fmod_f64_magic(size))
 };
 
 // the value of the other lane of an even/odd lane pair (DPP quad_perm [1, 0, 3, 2])
@@ -271,6 +275,8 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
         }
     }
     __shared__ uint32_t base_u[kMrgGroupBatch][24], base_v[kMrgGroupBatch][24];
+    const double inv_d = __builtin_bit_cast(double, magic), half_inv_d = 0.5 * inv_d;  // kMrgIdxF64
+    const double dd = (double)size;
     const int k = threadIdx.x / kC;  // engine row; also the solve's position in the chunk
     const int c = threadIdx.x % kC;
     const int64_t cols = n < mrg::kOrder ? n : mrg::kOrder;
@@ -326,7 +332,16 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
             auto steps = [&](auto p) {
                 constexpr int P = decltype(p)::value;
 #pragma unroll
-                for (int i = 0; i < kQ; ++i) w[i * kC] = mrg::step_at(st, (P + i) % 3);  // folds
+                for (int i = 0; i < kQ; ++i) {
+                    if constexpr ((ABL & kMrgIdxF64) != 0) {
+                        const int sl = (P + i) % 3;  // folds
+                        w[i * kC] = sl == 0 ? mrg::step_index<0>(st, inv_d, half_inv_d, dd)
+                                            : (sl == 1 ? mrg::step_index<1>(st, inv_d, half_inv_d, dd)
+                                                       : mrg::step_index<2>(st, inv_d, half_inv_d, dd));
+                    } else {
+                        w[i * kC] = mrg::step_at(st, (P + i) % 3);  // folds
+                    }
+                }
             };
             if (phase == 0) steps(std::integral_constant<int, 0>());
             else if (phase == 1) steps(std::integral_constant<int, 1>());
@@ -337,7 +352,7 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
         gen(0, 0);
         __syncthreads();
         if constexpr ((ABL & kMrgInterleave) != 0) {
-            static_assert((ABL & kMrgStBuf) != 0 && (ABL & ~(kMrgInterleave | kMrgStBuf)) == 0,
+            static_assert((ABL & kMrgStBuf) != 0 && (ABL & ~(kMrgInterleave | kMrgStBuf | kMrgIdxF64)) == 0,
                           "the interleaved chunk is the shipped one with buffer stores");
             int buf = 0;
             int64_t q0 = 0;
@@ -349,7 +364,7 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
 #pragma unroll
                     for (int r = 0; r < 4; ++r) {
                         const uint32_t w = words[((buf * 4 + r) * kQ + k + 4 * j) * kC + c];
-                        const uint32_t ix = fastmod_u32(w, magic, size);
+                        const uint32_t ix = (ABL & kMrgIdxF64) != 0 ? w : fastmod_u32(w, magic, size);
                         double2 ps, pt;
                         if constexpr (POOL_LDS) {
                             ps = pool[2 * ix];
@@ -365,7 +380,16 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
                 {  // the next chunk's words (past a group's last chunk: drawn, never read)
                     uint32_t* w = words + ((buf ^ 1) * 4 + k) * kQ * kC + c;
 #pragma unroll
-                    for (int i = 0; i < kQ; ++i) w[i * kC] = mrg::step_at(st, (PN + i) % 3);
+                    for (int i = 0; i < kQ; ++i) {
+                        if constexpr ((ABL & kMrgIdxF64) != 0) {
+                            const int sl = (PN + i) % 3;
+                            w[i * kC] = sl == 0 ? mrg::step_index<0>(st, inv_d, half_inv_d, dd)
+                                                : (sl == 1 ? mrg::step_index<1>(st, inv_d, half_inv_d, dd)
+                                                           : mrg::step_index<2>(st, inv_d, half_inv_d, dd));
+                        } else {
+                            w[i * kC] = mrg::step_at(st, (PN + i) % 3);
+                        }
+                    }
                 }
 #pragma unroll
                 for (int j = 0; j < kPer; ++j) {
@@ -412,7 +436,7 @@ __global__ __launch_bounds__(KB) void mrg_gather_solve_f64_kernel(
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
                     const uint32_t w = words[((buf * 4 + r) * kQ + qq) * kC + c];
-                    const uint32_t ix = fastmod_u32(w, magic, size);
+                    const uint32_t ix = (ABL & kMrgIdxF64) != 0 ? w : fastmod_u32(w, magic, size);
                     double2 ps, pt;
                     if constexpr ((ABL & kMrgAblNoGather) != 0) {
                         ps = double2((double)w, (double)(w >> 1));
@@ -532,7 +556,7 @@ inline int launch_rand_gather_solve(const double2* ps, const double2* pt, uint32
     }
     const int64_t cols = n < mrg::kOrder ? n : mrg::kOrder;
     const int64_t groups = (cols + kB / 4 - 1) / (kB / 4);
-    const uint64_t magic = fastmod_magic(size);
+    const uint64_t magic = (ABL & kMrgIdxF64) != 0 ? fmod_f64_magic(size) : fastmod_magic(size);
     const size_t words = mrg_words_lds<ALGO, Q, KB>();
     const bool pool_lds = variant != 0 && kMrgStaticLds + words + (size_t)size * 32 <= kLdsMax;
     const size_t lds = pool_lds ? words + (size_t)size * 32 : words;

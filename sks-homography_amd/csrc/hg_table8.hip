@@ -141,14 +141,17 @@ int hg_rand_gather_solve_f64(int algo, const double* pool_src, const double* poo
     hipStream_t s = reinterpret_cast<hipStream_t>(stream);
     const bool norm = (flags & HG_FLAG_NORMALIZE) != 0;
     // H rows through buffer stores (row resources in SGPRs, one 32-bit lane offset: 16 VGPRs
-    // fewer, 1-3 % faster at 10 M, tools/kbench_t8q.py) while a row's bytes fit 32 bits
+    // fewer, 1-3 % faster at 10 M, tools/kbench_t8q.py) while a row's bytes fit 32 bits.  The
+    // engines hand the solves pool indices, the remainder made in binary64 from the word's
+    // binary64 value (kMrgIdxF64: 16 VALU fewer per 64 hypotheses, 5-8 % at 10 M; round 6)
     const bool buf = n < (INT64_C(1) << 29);
-#define HG_RGS(A)                                                                                    \
-    if (buf)                                                                                         \
-        return norm ? hg::launch_rand_gather_solve<A, true, hg::kMrgStBuf>(ps, pt, size, seed, H, n, s) \
-                    : hg::launch_rand_gather_solve<A, false, hg::kMrgStBuf>(ps, pt, size, seed, H, n, s); \
-    return norm ? hg::launch_rand_gather_solve<A, true>(ps, pt, size, seed, H, n, s)                 \
-                : hg::launch_rand_gather_solve<A, false>(ps, pt, size, seed, H, n, s)
+    constexpr int kBuf = hg::kMrgStBuf | hg::kMrgIdxF64, kFlat = hg::kMrgIdxF64;
+#define HG_RGS(A)                                                                                \
+    if (buf)                                                                                     \
+        return norm ? hg::launch_rand_gather_solve<A, true, kBuf>(ps, pt, size, seed, H, n, s)   \
+                    : hg::launch_rand_gather_solve<A, false, kBuf>(ps, pt, size, seed, H, n, s); \
+    return norm ? hg::launch_rand_gather_solve<A, true, kFlat>(ps, pt, size, seed, H, n, s)      \
+                : hg::launch_rand_gather_solve<A, false, kFlat>(ps, pt, size, seed, H, n, s)
     switch (algo) {
         case HG_ALGO_ACA: HG_RGS(hg::kACA);
         case HG_ALGO_SKS: HG_RGS(hg::kSKS);

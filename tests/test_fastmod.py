@@ -75,3 +75,25 @@ def test_fmod_f64_matches_modulo_below_2_31():
         assert u >= 0 and u.as_integer_ratio()[0] * d >= u.as_integer_ratio()[1]
         for r in _numerators(d, rng):
             assert fmod_f64(r, u, d) == r % d, (d, r)
+
+
+def t8_index(w, u, d):
+    """mrg::step_index (hg_mrg32k3a.hpp): q = trunc(RN(w u + u/2)) with ONE rounding (the FMA,
+    restated with exact rationals: float(Fraction) rounds to nearest), then w - q d exactly."""
+    from fractions import Fraction
+    uf = Fraction(float(u))
+    q = int(float(Fraction(w) * uf + uf / 2))  # trunc: the value is >= 0
+    assert q == int(Fraction(2 * w + 1, 2 * d))  # floor((w + 1/2) / d) = floor(w / d): no correction
+    return w - q * d
+
+
+def test_table8_index_form_matches_modulo():
+    rng = np.random.default_rng(7)
+    ds = set(range(1, 1025)) | {2540, 4096, 5120, 9088, 20_000, 65_537, M32, M32 - 1, (1 << 31) + 1}
+    for k in range(1, 32):
+        ds |= {(1 << k) - 1, 1 << k, (1 << k) + 1}
+    ds |= set(int(x) for x in rng.integers(1, 1 << 32, 120, dtype=np.uint64))
+    for d in sorted(ds):
+        u = fmod_f64_magic(d)
+        for w in _numerators(d, rng):
+            assert t8_index(w, u, d) == w % d, (d, w)

@@ -26,9 +26,13 @@ VARIANTS = {  # hg_tune_rand_gather_solve_f64 variant -> shape
     16: "Q4 KB1024 (r04 shape)", 21: "Q4 KB1024 buffer stores (r05 shipped)",
     23: "Q4 KB1024 buffer stores, next chunk's draws interleaved with the solves",
     22: "Q8 KB1024 buffer stores",
+    25: "Q4 KB1024 buffer stores, engines write pool indices (binary64 remainder)",
+    26: "23 with the engines writing pool indices",
 }
 if os.environ.get("KB_ALL"):
     VARIANTS.update({20: "Q4 KB768", 18: "Q8 KB768", 19: "Q8 KB512", 15: "Q8 KB1024 (6 VGPRs spilled)"})
+if os.environ.get("KB_VARIANTS"):  # e.g. KB_VARIANTS=21,25: only these
+    VARIANTS = {int(v): VARIANTS[int(v)] for v in os.environ["KB_VARIANTS"].split(",")}
 NBUF = int(os.environ.get("KB_NBUF", "3"))  # output buffers per variant, used in turn: the
 # 10 M figures move with where the 720 MB of H land (KERNEL_NOTES.md), so every variant is
 # timed over the same number of distinct placements
@@ -49,6 +53,28 @@ def timeit(fns, loops):
             e1.synchronize()
             times[k].append(e0.elapsed_time(e1) * 1e3 / loops)
     return {k: (round(statistics.median(v), 2), round(min(v), 2)) for k, v in times.items()}
+
+
+def sustained(fns, keys, reps=3):
+    """bench.py's launch_stats shape: per key 5 warm-up launches, then 10 groups of 10
+    back-to-back launches (the clocks settle under this VALU-heavy load), median of the group
+    means; keys in turn, `reps` times, median over the reps."""
+    res = {k: [] for k in keys}
+    for _ in range(reps):
+        for k in keys:
+            for _ in range(5):
+                fns[k]()
+            ts = []
+            for _ in range(10):
+                e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                e0.record()
+                for _ in range(10):
+                    fns[k]()
+                e1.record()
+                e1.synchronize()
+                ts.append(e0.elapsed_time(e1) * 1e3 / 10)
+            res[k].append(statistics.median(ts))
+    return {k: round(statistics.median(v), 2) for k, v in res.items()}
 
 
 def main():
@@ -92,6 +118,10 @@ def main():
         same = {v: bool(torch.equal(H[v].view(torch.int64), H["shipped"].view(torch.int64)))
                 for v in VARIANTS}
         r = timeit(fns, 6)
+        if os.environ.get("KB_SUSTAINED"):
+            sus = sustained(fns, ["shipped", *VARIANTS, "write_only_72B"])
+            print(f"{algo} sustained (bench launch_stats shape)", sus, flush=True)
+            out[f"{algo} sustained_us"] = sus
         w_us = r["write_only_72B"][0]
         for k, (us, best) in r.items():
             rec = {"us": us, "best_us": best, "ghyp_s": round(n / (us * 1e-6) / 1e9, 2),

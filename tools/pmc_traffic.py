@@ -51,8 +51,8 @@ KEYS = {
     "sample_solve_seeded": ("void hg::sample_solve_lds_kernel<0, true, 2, 0, 4, 1", M16 * 36),
     "gather_solve_f64_aca": ("void hg::gather_solve_f64_kernel<0", M10 * 88),
     "mrg_words": ("hg::mrg_words_kernel<0>", 40_000_000 * 4),
-    "rand_gather_solve_f64_aca": ("void hg::mrg_gather_solve_f64_kernel<0, false, true, 64", M10 * 72),
-    "rand_gather_solve_f64_sks": ("void hg::mrg_gather_solve_f64_kernel<1, false, true, 64", M10 * 72),
+    "rand_gather_solve_f64_aca": ("void hg::mrg_gather_solve_f64_kernel<0, false, true, 320", M10 * 72),
+    "rand_gather_solve_f64_sks": ("void hg::mrg_gather_solve_f64_kernel<1, false, true, 320", M10 * 72),
 }
 
 
