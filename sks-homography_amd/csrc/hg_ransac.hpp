@@ -238,12 +238,24 @@ inline uint64_t fmod_f64_magic(uint32_t d) {
     return bits;
 }
 
-// Remainder forms: 0 fastmod_u32 (shipped), 1 fastmod64_u32, 2 fmod_f64_u32; 3 (tune
-// ablation only, wrong indices) r & 1023 clamped to the pool -- the loop without a remainder.
+// The binary64 form without a correction (round 6; the Table-8 kernel's mrg::step_index):
+// q = trunc(RN(r u + u/2)) is floor(r/d) exactly -- (r + 1/2)/d lies 1/(2d) from every
+// integer, the product errs by < 2^-19/d -- so r - q d (one exact FMA) is the remainder, for
+// every d < 2^32.  Same magic as fmod_f64_u32.
+__device__ __forceinline__ uint32_t fmod_f64_exact_u32(uint32_t r, uint64_t inv_bits, uint32_t d) {
+    const double w = (double)r, u = __builtin_bit_cast(double, inv_bits);
+    const double q = __builtin_trunc(__builtin_fma(w, u, 0.5 * u));
+    return (uint32_t)__builtin_fma(-q, (double)d, w);
+}
+
+// Remainder forms: 0 fastmod_u32 (shipped), 1 fastmod64_u32, 2 fmod_f64_u32, 4
+// fmod_f64_exact_u32; 3 (tune ablation only, wrong indices) r & 1023 clamped to the pool -- the
+// loop without a remainder.
 template <int RED>
 __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uint32_t d) {
     if constexpr (RED == 1) return fastmod64_u32(r, magic, d);
     else if constexpr (RED == 2) return fmod_f64_u32(r, magic, d);
+    else if constexpr (RED == 4) return fmod_f64_exact_u32(r, magic, d);
     else if constexpr (RED == 3) return (r & 1023u) < d ? (r & 1023u) : 0u;
     else return fastmod_u32(r, magic, d);
 }
@@ -251,7 +263,7 @@ __device__ __forceinline__ uint32_t reduce_index(uint32_t r, uint64_t magic, uin
 template <int RED>
 inline uint64_t reduce_magic(uint32_t d) {
     if constexpr (RED == 1) return fastmod64_magic(d);
-    else if constexpr (RED == 2) return fmod_f64_magic(d);
+    else if constexpr (RED == 2 || RED == 4) return fmod_f64_magic(d);
     else return fastmod_magic(d);
 }
 

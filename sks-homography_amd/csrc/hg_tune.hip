@@ -824,6 +824,11 @@ int hg_tune_sample_seeded(int variant, const float* pool_src, const float* pool_
         case 28: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 29: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 2>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         case 30: return launch_sample_seeded<2, 16, kDrawsPaired, 0, 0, kPairPacked, 3>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        // the binary64 remainder without a correction (fmod_f64_exact_u32) in the 4-, 8- and
+        // 16-wave packed-pair shapes (same bits)
+        case 31: return launch_sample_seeded<2, 4, kDrawsPaired, 4, 0, kPairPacked, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 32: return launch_sample_seeded<2, 8, kDrawsPaired, 4, 0, kPairPacked, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
+        case 33: return launch_sample_seeded<2, 16, kDrawsPaired, 4, 0, kPairPacked, 0>(ps, pt, npool, seed, offset, H, n, algo, norm, st);
         default: return (int)hipErrorInvalidValue;
     }
 }

@@ -51,7 +51,10 @@ SEEDED = {0: "seeded shipped (packed pairs; 8 waves, ACA from 4 M 4)", 1: "seede
           26: "seeded P2 pairs, 8 waves, sc1 buffer H stores",
           27: "seeded P2 pairs, 8 waves, sc1|nt buffer H stores",
           28: "seeded P2 pairs, 16 waves", 29: "seeded P2 pairs, 16 waves, sc1 buffer H stores",
-          30: "seeded P2 pairs, 16 waves, sc1|nt buffer H stores"}
+          30: "seeded P2 pairs, 16 waves, sc1|nt buffer H stores",
+          31: "seeded P2 pairs, 4 waves, exact binary64 remainder (no correction)",
+          32: "seeded P2 pairs, 8 waves, exact binary64 remainder (no correction)",
+          33: "seeded P2 pairs, 16 waves, exact binary64 remainder (no correction)"}
 # KB_SEEDED_ONLY=1: the seeded variants only (plus the indexed reference for the bits), at 4 M and 16 M
 SEEDED_ONLY = os.environ.get("KB_SEEDED_ONLY") == "1"
 OTHER_STREAM = (5, 6, 15, 16, 17, 19, 20, 21)  # other streams / ablations: not comparable bit for bit
