@@ -1,0 +1,40 @@
+"""bench.py's host_boundary section alone (one rank, the bench's NUMA binding), with the
+library's ring counters around it: where the pageable path's time goes in the bench's own
+process shape.  Output: one JSON line (gpurun_out/host_boundary_probe.json)."""
+import ctypes
+import json
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+
+
+def main():
+    numa = bench.bind_numa(0)  # before anything touches the GPU, as bench.py does
+    import __graft_entry__ as ge
+    pkg = ge.load_package()
+    d = bench.Dist("nccl")
+    lib = pkg.lib()
+    p64 = ctypes.POINTER(ctypes.c_int64)
+    lib.hg_internal_host_stage_stats.argtypes = [p64]
+    st0 = (ctypes.c_int64 * 8)()
+    lib.hg_internal_host_stage_stats(st0)
+    out = bench.host_boundary_section(d, pkg, 10_000_000)
+    st1 = (ctypes.c_int64 * 8)()
+    lib.hg_internal_host_stage_stats(st1)
+    ring_calls = max(1, st1[4] - st0[4])
+    out["ring_stats"] = {"ring_calls": st1[4] - st0[4],
+                         "copy_ms_per_ring_call": round((st1[5] - st0[5]) / ring_calls / 1e6, 3),
+                         "wait_ms_per_ring_call": round((st1[6] - st0[6]) / ring_calls / 1e6, 3)}
+    out["numa"] = numa
+    out["cpus"] = len(os.sched_getaffinity(0))
+    os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+    with open(os.path.join(ROOT, "gpurun_out", "host_boundary_probe.json"), "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out))
+
+
+if __name__ == "__main__":
+    main()
