@@ -28,6 +28,26 @@ def main():
     out["ring_stats"] = {"ring_calls": st1[4] - st0[4],
                          "copy_ms_per_ring_call": round((st1[5] - st0[5]) / ring_calls / 1e6, 3),
                          "wait_ms_per_ring_call": round((st1[6] - st0[6]) / ring_calls / 1e6, 3)}
+    # a fresh batch in this process, each call apart: wall, host-copy and event-wait times
+    import time
+    import torch
+    n = 10_000_000
+    ds = pkg.fill_uniform(n * 8, 11, 0, device=d.dev).view(n, 8)
+    dt = pkg.fill_uniform(n * 8, 11, n * 8, device=d.dev).view(n, 8)
+    qs, qt = ds.cpu(), dt.cpu()
+    qH = torch.empty((n, 9))
+    per_call = []
+    for _ in range(10):
+        a = (ctypes.c_int64 * 8)()
+        lib.hg_internal_host_stage_stats(a)
+        t0 = time.perf_counter()
+        pkg.solve_host("aca", qs, qt, out=qH)
+        wall = (time.perf_counter() - t0) * 1e3
+        b = (ctypes.c_int64 * 8)()
+        lib.hg_internal_host_stage_stats(b)
+        per_call.append({"ms": round(wall, 2), "copy_ms": round((b[5] - a[5]) / 1e6, 2),
+                         "wait_ms": round((b[6] - a[6]) / 1e6, 2), "stages_made": b[0] - a[0]})
+    out["fresh_batch_calls"] = per_call
     out["numa"] = numa
     out["cpus"] = len(os.sched_getaffinity(0))
     os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
