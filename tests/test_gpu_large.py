@@ -127,3 +127,34 @@ def test_soa_f32_beyond_2_31_vs_oracle(orc, oracle, pkg, dev):
     finally:
         del src, tar
         torch.cuda.empty_cache()
+
+
+N_T8 = (1 << 29) + 4099  # 8 n >= 2^32: H's row offsets leave 32 bits (no buffer stores)
+
+
+def test_table8_fused_beyond_2_29_vs_unfused(orc, pkg, dev):
+    """hg_rand_gather_solve_f64 past 2^29 hypotheses, where a (9,n) binary64 row's byte offsets
+    need more than 32 bits and the launch takes the 64-bit-address form (hg_table8.hip kFlat),
+    with the engines' pool indices (kMrgIdxF64): slices at the start, across h = 2^29 and at
+    the end equal the unfused words -> gather -> solve path on the same 4 n MRG32K3A words
+    (also past 2^31 words)."""
+    need = N_T8 * (72 + 16) + (4 << 30)
+    if _free_bytes(dev) < need:
+        pytest.skip(f"needs {need / 1e9:.0f} GB of free device memory")
+    g = np.load(os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "cpp_wall.npz"))
+    ps = torch.from_numpy(g["pool_src"].astype(np.float64)).to(dev)
+    pt = torch.from_numpy(g["pool_tar"].astype(np.float64)).to(dev)
+    seed = 11
+    rl = pkg.rand_mrg32k3a(4 * N_T8, seed, dev).view(4, N_T8)
+    b29 = 1 << 29
+    try:
+        for algo in ("aca", "sks"):
+            H = pkg.rand_gather_solve(ps, pt, N_T8, seed, algo)
+            for a, b in [(0, 1000), (b29 - 700, b29 + 700), (N_T8 - 1000, N_T8)]:
+                want = pkg.gather_solve(ps, pt, rl[:, a:b].contiguous(), algo)
+                ok = orc.same_bits(H[:, a:b].cpu().numpy(), want.cpu().numpy())
+                assert ok.all(), f"{algo} hypotheses [{a},{b}): {(~ok).sum()} differ"
+            del H
+    finally:
+        del rl
+        torch.cuda.empty_cache()
