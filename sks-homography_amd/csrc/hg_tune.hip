@@ -1009,6 +1009,8 @@ static int rand_gather_variant(int variant, const double2* ps, const double2* pt
             return launch_rand_gather_solve<ALGO, false, kMrgStBuf | kMrgIdxF64, 4>(ps, pt, size, seed, H, n, s);
         case 26:  // 23 with the same
             return launch_rand_gather_solve<ALGO, false, kMrgStBuf | kMrgInterleave | kMrgIdxF64, 4>(ps, pt, size, seed, H, n, s);
+        case 27:  // Q = 8, buffer stores, pool indices from the engines
+            return launch_rand_gather_solve<ALGO, false, kMrgStBuf | kMrgIdxF64, 8>(ps, pt, size, seed, H, n, s);
         default: return (int)hipErrorInvalidValue;
     }
 }
@@ -1018,7 +1020,7 @@ extern "C" {
 int hg_tune_rand_gather_solve_f64(int variant, int algo, const double* pool_src,
                                   const double* pool_tar, uint32_t size, uint64_t seed, double* H,
                                   int64_t n, void* stream) {
-    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 26)
+    if (n <= 0 || size == 0 || (algo != 0 && algo != 1) || variant < 0 || variant > 27)
         return (int)hipErrorInvalidValue;
     if ((variant == 10 || variant == 11 || variant == 14) && ((n & 1) || (reinterpret_cast<uintptr_t>(H) & 15)))
         return (int)hipErrorInvalidValue;

@@ -28,6 +28,7 @@ VARIANTS = {  # hg_tune_rand_gather_solve_f64 variant -> shape
     22: "Q8 KB1024 buffer stores",
     25: "Q4 KB1024 buffer stores, engines write pool indices (binary64 remainder)",
     26: "23 with the engines writing pool indices",
+    27: "Q8 KB1024 buffer stores, engines write pool indices",
 }
 if os.environ.get("KB_ALL"):
     VARIANTS.update({20: "Q4 KB768", 18: "Q8 KB768", 19: "Q8 KB512", 15: "Q8 KB1024 (6 VGPRs spilled)"})
