@@ -463,6 +463,28 @@ def launch_stats(d: Dist, fn, groups: int = 40, per_group: int = 10):
             "min_us": round(float(ts[0]), 2)}
 
 
+def settle(d: Dist, fn, ms: float = 80.0, cap: int = 2000) -> int:
+    """Back-to-back launches of `fn` until `ms` of device time have run (at most `cap`
+    launches); returns the launches made.  Under a VALU-heavy load the card's clock takes a few
+    hundred launches to settle after any change of load: 10 M SKS Table-8 launches go
+    186 -> 133 us over ~300 launches, again after a 2 s idle gap (tools/t8_ramp_probe.py,
+    profiles/r06/t8_ramp_r06z.json).  The reference's own statistic is a ~10 s mean
+    (cal_ACA, GPU_Runtime Test.cu:1183-1200), i.e. the settled rate."""
+    stream = torch.cuda.current_stream(d.dev)
+    done_ms, n = 0.0, 0
+    while done_ms < ms and n < cap:
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record(stream)
+        for _ in range(20):
+            fn()
+        e1.record(stream)
+        e1.synchronize()
+        done_ms += e0.elapsed_time(e1)
+        n += 20
+    return n
+
+
 def reference_statistic(d: Dist, fn):
     """cal_ACA's own statistic (GPU_Runtime Test.cu:1183-1200): time one launch,
     loops = 10000 / ms (about 10 s of back-to-back launches), report the mean."""
@@ -1273,6 +1295,7 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
             f_one()
             f_two()
             f_write()
+        settled = settle(d, f_one)
         ms_one = launch_stats(d, f_one, groups=10)["median_us"] * 1e-3
         ms_write = launch_stats(d, f_write, groups=10)["median_us"] * 1e-3
         _, ms_two = timed_region(d, f_two, 20)
@@ -1285,7 +1308,7 @@ def table8_pipeline_section(d: Dist, pkg, n: int = 1_000_000):
             "write_only_stream_gbps": round(big * 72 / (ms_write * 1e-3) / 1e9, 1),
             "frac_of_write_only_stream": round(ms_write / ms_one, 4),
             "draws_then_gather_solve_us": round(ms_two * 1e3, 2),
-            "placements": len(Hbs)}
+            "placements": len(Hbs), "settle_launches": settled}
         del Hb, Hbs
     del wbuf, wb
     return out
@@ -1461,6 +1484,7 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
         f_two()
         f_seed()
     ms_two = launch_stats(d, f_two, groups=20)["median_us"] * 1e-3
+    settled_seed = settle(d, f_seed)
     ms_seed = launch_stats(d, f_seed, groups=20)["median_us"] * 1e-3
     seeded_same = bool(torch.equal(pkg.sample_solve_seeded(ps, pt, hyps, SEED, 0).view(torch.int32),
                                    H.view(torch.int32)))
@@ -1499,7 +1523,7 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
             "frac_of_write_only_stream": round(ms_write / ms_seed, 4),
             "draws_then_indexed_us": round(ms_two * 1e3, 2),
             "speedup_vs_two_launch": round(ms_two / ms_seed, 2),
-            "bit_identical_to_indexed": seeded_same},
+            "bit_identical_to_indexed": seeded_same, "settle_launches": settled_seed},
         "score_ms": round(ms_score, 3),
         "score_G_pairs_per_s": round(pairs / (ms_score * 1e-3) / 1e9, 1),
         "best_inliers": int(counts.max().item()),
