@@ -1460,10 +1460,11 @@ def ransac_section(d: Dist, pkg, hyps: int = 1 << 20, thresh: float = 3.0):
     for _ in range(3):
         f_solve()
     _, ms_solve = timed_region(d, f_solve, 20)
-    # the scorer is VALU-bound (~0.8 ms a launch): warm ~25 ms, then the median of 10
-    # three-launch groups (clock wander, as for the 16M samplers below)
-    for _ in range(30):
+    # the scorer is VALU-bound (~0.7 ms a launch): settled clock (`settle`), then the median
+    # of 10 three-launch groups
+    for _ in range(3):
         f_score()
+    settle(d, f_score)
     ms_score = launch_stats(d, f_score, groups=10, per_group=3)["median_us"] * 1e-3
     counts = pkg.ransac_score(H, ps, pt, thresh)
     pairs = hyps * ps.shape[0]
