@@ -734,8 +734,11 @@ constexpr int64_t kSeededPairMinN = int64_t(1) << 22;
 inline int launch_sample_seeded_shipped(const float2* ps, const float2* pt, uint32_t npool,
                                         uint64_t seed, uint64_t offset, float* H, int64_t n,
                                         int algo, bool norm, hipStream_t s) {
+    // ACA from 4 M: the binary64 remainder without a correction (RED 4, fmod_f64_exact_u32; same
+    // indices): 149.8 -> 137.8 VALU per 64 hypotheses (profiles/r06/pmc_table8_r06v.json); its
+    // time is within the sweeps' spread (round 6)
     if (algo == 0 && n >= kSeededPairMinN)
-        return launch_sample_seeded<2, 4, kDrawsPaired, 0, 0, kPairPacked>(ps, pt, npool, seed,
+        return launch_sample_seeded<2, 4, kDrawsPaired, 4, 0, kPairPacked>(ps, pt, npool, seed,
                                                                             offset, H, n, algo, norm, s);
     return launch_sample_seeded<2, 8, kDrawsPaired, 0, 0, kPairPacked>(ps, pt, npool, seed, offset,
                                                                         H, n, algo, norm, s);

@@ -143,7 +143,7 @@ int hg_rand_gather_solve_f64(int algo, const double* pool_src, const double* poo
     // H rows through buffer stores (row resources in SGPRs, one 32-bit lane offset: 16 VGPRs
     // fewer, 1-3 % faster at 10 M, tools/kbench_t8q.py) while a row's bytes fit 32 bits.  The
     // engines hand the solves pool indices, the remainder made in binary64 from the word's
-    // binary64 value (kMrgIdxF64: 16 VALU fewer per 64 hypotheses, 5-8 % at 10 M; round 6)
+    // binary64 value (kMrgIdxF64: 16 VALU fewer per 64 hypotheses; round 6)
     const bool buf = n < (INT64_C(1) << 29);
     constexpr int kBuf = hg::kMrgStBuf | hg::kMrgIdxF64, kFlat = hg::kMrgIdxF64;
 #define HG_RGS(A)                                                                                \

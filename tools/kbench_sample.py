@@ -103,10 +103,21 @@ def main():
         # equal up to NaN payload and sign (the contract against the CPU reference)
         nan_eq = {v: bool(((outs[v].view(torch.int32) == outs[0].view(torch.int32))
                            | (outs[v].isnan() & outs[0].isnan())).all()) for v in keys}
+        # settle the card's clock under this VALU-heavy load first (bench.py `settle`):
+        # ~200 ms of launches, every variant in turn
+        import time as _time
+        t_end = _time.perf_counter() + 0.2
+        while _time.perf_counter() < t_end:
+            for v in keys:
+                run(v)
+            torch.cuda.synchronize()
         times = {v: [] for v in keys}
         reps = 20
-        for _ in range(int(os.environ.get("KB_ROUNDS", "7"))):
-            for v in keys:
+        for rnd in range(int(os.environ.get("KB_ROUNDS", "7"))):
+            # rotated start, so no variant always follows the same one (each variant writes its
+            # own output buffer: the same kernel under two keys differs by up to 5 % with the
+            # buffer's placement, profiles/r06/kbench_sample_ab_r06v.log)
+            for v in keys[rnd % len(keys):] + keys[:rnd % len(keys)]:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
                 for _ in range(reps):

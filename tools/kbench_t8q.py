@@ -44,8 +44,11 @@ def timeit(fns, loops):
         for _ in range(3):
             f()
     times = {k: [] for k in fns}
-    for _ in range(ROUNDS):
-        for k, f in fns.items():
+    keys = list(fns)
+    for rnd in range(ROUNDS):
+        # each round starts at another variant, so no variant always follows the same one
+        for k in keys[rnd % len(keys):] + keys[:rnd % len(keys)]:
+            f = fns[k]
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(loops):
